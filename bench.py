@@ -1,0 +1,151 @@
+"""Benchmark: fused tri-modal samples/s @ batch 256 per GPU (BASELINE.json metric).
+
+One step = one pass of the whole hot path over one synthetic batch already resident in
+HBM: speech DNN + BERT-base (L=128) + ResNet50 (48x48 u8 -> 224) encoders, then the
+attention-MLP fusion, then (N>1) the RCCL all-gather of the 34-float result rows.
+Weak scaling: every rank processes its own batch of 256.
+
+    python bench.py [--gpus N] [--steps K] [--warmup W] [--batch B] [--no-cpu-baseline]
+    python -m torch.distributed.run --nproc-per-node N ... bench.py --gpus N
+"""
+import argparse
+import json
+import os
+import sys
+import time
+
+ROOT = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, os.path.join(ROOT, 'multimodal-emotion-classification_amd'))
+
+import numpy as np  # noqa: E402
+import torch  # noqa: E402
+import torch.distributed as dist  # noqa: E402
+
+# Algorithmic work (BASELINE.md "Work per unit")
+FLOP_PER_SAMPLE = {'text': 2 * 11_174_221_056, 'image': 2 * 4_088_188_416, 'speech': 2 * 463_296,
+                   'fusion': 2 * 2_020_000}
+MI355X_F16_DENSE_TFLOPS = 2500.0  # MI355X_MICROARCH.md: ~2.5 PF dense bf16/f16 MFMA
+
+
+def parse():
+    ap = argparse.ArgumentParser()
+    ap.add_argument('--gpus', type=int, default=1)
+    ap.add_argument('--steps', type=int, default=10)
+    ap.add_argument('--warmup', type=int, default=3)
+    ap.add_argument('--batch', type=int, default=256)
+    ap.add_argument('--no-cpu-baseline', action='store_true')
+    ap.add_argument('--cpu-seconds', type=float, default=12.0)
+    return ap.parse_args()
+
+
+def cpu_baseline(seconds: float):
+    """Time the CPU oracle (fp32 restatement: our 'port' of the reference arithmetic) on a
+    bounded sample of the same workload: fused samples in batches of 2 until `seconds`."""
+    sys.path.insert(0, ROOT)
+    from mec import synthetic as syn
+    from oracle import fusion as o_f, image as o_i, speech as o_s, text as o_t
+    w = {k: syn.weights(k) for k in ('speech', 'text', 'image', 'fusion')}
+    Bc = 2
+    x = syn.speech_inputs(Bc, seed=0)
+    ids, mask = syn.text_inputs(Bc, 128, seed=0)
+    gray = syn.image_inputs(Bc, seed=0)
+
+    def one():
+        sf, _, sp = o_s.forward(w['speech'], x)
+        tf, _, tp = o_t.forward(w['text'], ids, mask)
+        imf, _, ip = o_i.forward(w['image'], gray)
+        o_f.forward(w['fusion'], sf, tf, imf, sp, tp, ip)
+
+    one()  # warm-up
+    n, t0 = 0, time.perf_counter()
+    while True:
+        one()
+        n += Bc
+        el = time.perf_counter() - t0
+        if el >= seconds:
+            break
+    return {'value': n / el, 'unit': 'fused samples/s', 'cores': torch.get_num_threads(), 'kind': 'port',
+            'sample': f'{n} fused samples (batches of {Bc}, L=128, 48x48 u8) through oracle/ fp32 torch-CPU, '
+                      f'{el:.1f}s'}
+
+
+def main():
+    a = parse()
+    world = int(os.environ.get('WORLD_SIZE', '1'))
+    rank = int(os.environ.get('RANK', '0'))
+    local = int(os.environ.get('LOCAL_RANK', '0'))
+    if world > 1:
+        torch.cuda.set_device(local)
+        dist.init_process_group('nccl', device_id=torch.device('cuda', local))
+    dev = torch.device('cuda', local)
+    torch.cuda.set_device(dev)
+
+    from mec import engine, synthetic as syn
+    B = a.batch
+    pipe = engine.FusedPipeline(seed=1234, device=dev)
+    x = engine.to_device(syn.speech_inputs(B, seed=rank), dev)
+    ids_np, mask_np = syn.text_inputs(B, 128, seed=rank, ragged=False)
+    ids, mask = engine.to_device(ids_np, dev), engine.to_device(mask_np, dev)
+    gray = engine.to_device(syn.image_inputs(B, seed=rank), dev)
+    gathered = torch.empty((world * B, engine.ROW), device=dev) if world > 1 else None
+
+    def step():
+        out = pipe.forward(x, ids, mask, gray)
+        rows = pipe.pack_rows(out)
+        if world > 1:
+            dist.all_gather_into_tensor(gathered, rows)
+        return rows
+
+    for _ in range(a.warmup):
+        step()
+    # hipEvent timing of the dominant kernel (BERT FFN1 GEMM) inside the timed region
+    pipe.text.prof_enable('bert_ffn1')
+    if world > 1:
+        dist.barrier()
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    for _ in range(a.steps):
+        step()
+    if world > 1:
+        dist.barrier()
+    torch.cuda.synchronize()
+    el = time.perf_counter() - t0
+    ffn_ms, ffn_n = pipe.text.prof_read()
+    pipe.text.prof_enable(0)
+    t = torch.tensor([el], device=dev, dtype=torch.float64)
+    if world > 1:
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+    el = float(t.item())
+
+    if rank == 0:
+        M = B * 128
+        ffn_flop = 2.0 * M * 3072 * 768
+        avg_s = (ffn_ms / max(ffn_n, 1)) / 1e3
+        achieved = ffn_flop / avg_s / 1e12 if ffn_n else None
+        roof = {'bound': 'mfma', 'kernel': 'gemm_f16_kernel<128,128,A_PLAIN> (BERT FFN1, M=%d N=3072 K=768)' % M,
+                'achieved': achieved, 'peak': MI355X_F16_DENSE_TFLOPS, 'unit': 'TFLOP/s',
+                'frac': (achieved / MI355X_F16_DENSE_TFLOPS) if achieved else None, 'traffic': None,
+                'avg_launch_ms': avg_s * 1e3, 'launches': ffn_n}
+        total = world * B * a.steps
+        flop = sum(FLOP_PER_SAMPLE.values()) * total
+        res = {
+            'metric': 'fused tri-modal samples/sec @ batch 256',
+            'value': total / el, 'unit': 'samples/s', 'n_gpus': world, 'steps': a.steps, 'warmup': a.warmup,
+            'ms_per_step': el / a.steps * 1e3, 'higher_is_better': True, 'scaling': 'weak', 'vs_baseline': None,
+            'dtype': 'f16 MFMA operands / fp32 accumulate, LN & softmax & residual fp32; speech+fusion fp32',
+            'data': 'synthetic (seeded inputs: 56-d features, 128-token ids, 48x48 u8; seeded synthetic weights)',
+            'config': {'workload': 'fused tri-modal: speech DNN + BERT-base L=128 + ResNet50@224 + attention fusion',
+                       'batch_per_gpu': B, 'global_batch': world * B, 'seq_len': 128,
+                       'parallelism': f'dp{world} (sample-sharded, all-gather of 34-float rows)'},
+            'achieved_tflops_whole_step': flop / el / 1e12,
+            'roofline': roof,
+        }
+        if world == 1 and not a.no_cpu_baseline:
+            res['cpu_baseline'] = cpu_baseline(a.cpu_seconds)
+        print(json.dumps(res))
+    if world > 1:
+        dist.destroy_process_group()
+
+
+if __name__ == '__main__':
+    main()

@@ -1,0 +1,96 @@
+/*
+ * mec.h — C ABI of libmec_hip.so, the MI355X (gfx950) batched tri-modal emotion
+ * inference path. Drop-in boundary for the reference's inference/ classes
+ * (RachaCodez/multimodal-emotion-classification); see INTEGRATION.md for the Python
+ * (ctypes) binding the reference-side classes use.
+ *
+ * Conventions
+ *   - Every data pointer is a DEVICE pointer owned by the caller; row-major, contiguous.
+ *   - Calls are asynchronous on `stream` (a hipStream_t; NULL = default stream).
+ *   - Return 0 on success, -1 on failure; mec_last_error() (thread-local) says why.
+ *   - A model handle owns its packed device weights and a grow-only workspace; it may be
+ *     used by one host thread at a time.
+ *   - Host weight blobs are fp32, in the canonical order of mec/synthetic.py:spec(kind),
+ *     i.e. the reference's own state_dict / Keras layer order.
+ */
+#ifndef MEC_H_
+#define MEC_H_
+
+#include <stddef.h>
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+typedef struct mec_model mec_model;
+
+enum { MEC_SPEECH = 0, MEC_TEXT = 1, MEC_IMAGE = 2, MEC_FUSION = 3 };
+
+/* Version / diagnostics. */
+const char* mec_version(void);
+const char* mec_last_error(void);
+
+/* Number of fp32 values the host blob for `kind` must hold (-1 if kind is unknown). */
+long long mec_blob_size(int kind);
+
+/* Create a model of `kind` on `device` from a host fp32 blob of `n` floats.
+ * Replaces the per-request model loads of the reference:
+ *   speech  tf.keras.models.load_model + joblib scaler   inference/speech_inference.py:21-28
+ *   text    BertForSequenceClassification.from_pretrained inference/text_inference.py:40-43
+ *   image   _build_model + load_state_dict               inference/image_inference.py:35-40
+ *   fusion  _build_fusion_model + load_state_dict        inference/multimodal_fusion.py:43-56 */
+int mec_create(int kind, const float* host_blob, size_t n, int device, mec_model** out);
+int mec_destroy(mec_model* m);
+
+/* Speech DNN. x: raw (pre-scaler) features f32[B,56]. Outputs feat f32[B,64] (block-5
+ * ReLU = layers[-3]), logits f32[B,7], probs f32[B,7].
+ * Replaces SpeechInference.predict / extract_features model arithmetic
+ *   inference/speech_inference.py:66-69, :86-103. */
+int mec_speech_fwd(mec_model* m, const float* x, int B, float* feat, float* logits, float* probs,
+                   void* stream);
+
+/* BERT-base text encoder + classifier. ids/mask int32[B,L] with L == 128
+ * (padding='max_length'). Outputs cls f32[B,768] (last_hidden_state[:,0]), logits,
+ * probs f32[B,7]. Replaces TextInference.predict / extract_features model arithmetic
+ *   inference/text_inference.py:87-94, :119-128. */
+int mec_text_fwd(mec_model* m, const int32_t* ids, const int32_t* mask, int B, int L, float* cls,
+                 float* logits, float* probs, void* stream);
+
+/* ResNet50 image encoder + head. gray: u8[B,48,48]; the PIL RGB/resize/ToTensor/Normalize
+ * transform runs on the GPU. Outputs feat f32[B,512] (fc[2]), logits, probs f32[B,7].
+ * Replaces ImageInference.predict / extract_features (after Image.open)
+ *   inference/image_inference.py:112-119, :137-144. */
+int mec_image_fwd(mec_model* m, const uint8_t* gray, int B, float* feat, float* logits, float* probs,
+                  void* stream);
+
+/* Attention-MLP fusion. Outputs logits/probs f32[B,7], attn_w/dec_w f32[B,3].
+ * Replaces MultimodalFusion.fuse_with_attention  inference/multimodal_fusion.py:201-239. */
+int mec_fusion_fwd(mec_model* m, const float* s_feat, const float* t_feat, const float* i_feat,
+                   const float* s_pred, const float* t_pred, const float* i_pred, int B, float* logits,
+                   float* probs, float* attn_w, float* dec_w, void* stream);
+
+/* Weighted-average fallback (float64, like numpy); any of s/t/i may be NULL (= zeros).
+ * Replaces MultimodalFusion.fuse_predictions  inference/multimodal_fusion.py:184-199. */
+int mec_fuse_weighted(const float* s_probs, const float* t_probs, const float* i_probs, int B,
+                      double* out, void* stream);
+
+/* Kernel-level entry points (parity tests / microbenchmarks). */
+int mec_resize_u8(const uint8_t* in, int B, int H, int W, uint8_t* out, int OH, int OW, void* stream);
+/* C[M,N] = act(A[M,K] . B[N,K]^T + bias (+ R)); f16 operands, fp32 accumulate.
+ * act: 0 none, 1 relu, 2 gelu(erf). Any of bias/R/C16/C32 may be NULL (not both outputs). */
+int mec_gemm_f16(const void* A, const void* B, const float* bias, const void* R, int r_is_f32, void* C16,
+                 float* C32, int M, int N, int K, int act, void* stream);
+/* Implicit-GEMM conv on NHWC f16: x[n,H,W,C], w[Cout][ks][ks][C], y[n,OH,OW,Cout]. */
+int mec_conv_f16(const void* x, const void* w, const float* bias, const void* R, void* y, int n, int H, int W,
+                 int C, int Cout, int ks, int stride, int pad, int act, void* stream);
+
+/* hipEvent timing hook: time every launch of kernel class `tag`. */
+int mec_prof_enable(mec_model* m, int tag);
+int mec_prof_read(mec_model* m, double* total_ms, int* count);
+
+#ifdef __cplusplus
+}
+#endif
+
+#endif /* MEC_H_ */

@@ -1,0 +1,205 @@
+// extern "C" boundary (include/mec.h).
+#include "../../include/mec.h"
+
+#include <exception>
+#include <new>
+
+#include "models.h"
+
+namespace mec {
+const char* last_error();
+
+size_t blob_floats(int kind) {
+  switch (kind) {
+    case KIND_SPEECH: {
+      const int d[6] = {56, 512, 512, 256, 128, 64};
+      size_t s = 112;
+      for (int i = 0; i < 5; ++i) s += (size_t)d[i] * d[i + 1] + 5 * d[i + 1];
+      return s + 64 * 7 + 7;
+    }
+    case KIND_TEXT: {
+      size_t s = (size_t)30522 * 768 + 512 * 768 + 2 * 768 + 2 * 768;
+      const size_t layer = 4 * ((size_t)768 * 768 + 768) + 2 * 768 + ((size_t)3072 * 768 + 3072) +
+                           ((size_t)768 * 3072 + 768) + 2 * 768;
+      return s + 12 * layer + (size_t)768 * 768 + 768 + 7 * 768 + 7;
+    }
+    case KIND_IMAGE: {
+      size_t s = 64 * 3 * 49 + 4 * 64;
+      const int L[4][3] = {{64, 3, 1}, {128, 4, 2}, {256, 6, 2}, {512, 3, 2}};
+      int cin = 64;
+      for (int l = 0; l < 4; ++l)
+        for (int b = 0; b < L[l][1]; ++b) {
+          const int w = L[l][0];
+          s += (size_t)w * cin + 4 * w + (size_t)w * w * 9 + 4 * w + (size_t)4 * w * w + 16 * w;
+          if (b == 0) s += (size_t)4 * w * cin + 16 * w;
+          cin = 4 * w;
+        }
+      return s + (size_t)512 * 2048 + 512 + 7 * 512 + 7;
+    }
+    case KIND_FUSION: {
+      size_t s = 0;
+      const int d[3] = {64, 768, 512};
+      for (int m = 0; m < 3; ++m) s += (size_t)256 * d[m] + 256 + 512;
+      s += 3 * ((size_t)768 * 256 + 768 + 256 * 256 + 256 + 512);
+      s += 3 * ((size_t)256 * 256 + 256 + 512);
+      s += (size_t)256 * 768 + 256 + 3 * 256 + 3 + 64 * 21 + 64 + 3 * 64 + 3;
+      s += (size_t)256 * 263 + 256 + 512 + 128 * 256 + 128 + 7 * 128 + 7;
+      return s;
+    }
+    default: return 0;
+  }
+}
+}  // namespace mec
+
+using namespace mec;
+
+struct mec_model {
+  Model* impl;
+};
+
+#define API_GUARD(body)                                  \
+  try {                                                  \
+    body                                                 \
+  } catch (const std::bad_alloc&) {                      \
+    set_error("host allocation failed");                 \
+    return -1;                                           \
+  } catch (const std::exception& e) {                    \
+    set_error(e.what());                                 \
+    return -1;                                           \
+  }
+
+static hipStream_t S(void* s) { return reinterpret_cast<hipStream_t>(s); }
+
+template <class T>
+static T* as(mec_model* m, int kind) {
+  if (!m || !m->impl) { set_error("null model handle"); return nullptr; }
+  if (m->impl->kind != kind) { set_error("model handle has the wrong kind for this call"); return nullptr; }
+  if (hipSetDevice(m->impl->device) != hipSuccess) { set_error("hipSetDevice failed"); return nullptr; }
+  return static_cast<T*>(m->impl);
+}
+
+extern "C" {
+
+const char* mec_version(void) { return "mec-hip 0.1 (gfx950)"; }
+const char* mec_last_error(void) { return last_error(); }
+
+long long mec_blob_size(int kind) {
+  const size_t n = blob_floats(kind);
+  return n ? (long long)n : -1;
+}
+
+int mec_create(int kind, const float* host_blob, size_t n, int device, mec_model** out) {
+  API_GUARD({
+    if (!out) { set_error("mec_create: out is null"); return -1; }
+    *out = nullptr;
+    const size_t want = blob_floats(kind);
+    if (!want) { set_error("mec_create: unknown kind"); return -1; }
+    if (!host_blob || n != want) {
+      set_error("mec_create: blob has " + std::to_string(n) + " floats, expected " + std::to_string(want));
+      return -1;
+    }
+    MEC_HIP(hipSetDevice(device));
+    Model* impl = nullptr;
+    int rc = -1;
+    switch (kind) {
+      case KIND_SPEECH: { auto* p = new SpeechModel(); impl = p; rc = p->create(host_blob, n); break; }
+      case KIND_TEXT: { auto* p = new TextModel(); impl = p; rc = p->create(host_blob, n); break; }
+      case KIND_IMAGE: { auto* p = new ImageModel(); impl = p; rc = p->create(host_blob, n); break; }
+      case KIND_FUSION: { auto* p = new FusionModel(); impl = p; rc = p->create(host_blob, n); break; }
+    }
+    if (rc != 0) { delete impl; return -1; }
+    impl->kind = kind;
+    impl->device = device;
+    *out = new mec_model{impl};
+    return 0;
+  })
+}
+
+int mec_destroy(mec_model* m) {
+  if (!m) return 0;
+  if (m->impl) (void)hipSetDevice(m->impl->device);
+  delete m->impl;
+  delete m;
+  return 0;
+}
+
+int mec_speech_fwd(mec_model* m, const float* x, int B, float* feat, float* logits, float* probs, void* stream) {
+  API_GUARD({
+    auto* p = as<SpeechModel>(m, KIND_SPEECH);
+    if (!p) return -1;
+    return p->forward(x, B, feat, logits, probs, S(stream));
+  })
+}
+
+int mec_text_fwd(mec_model* m, const int32_t* ids, const int32_t* mask, int B, int L, float* cls, float* logits,
+                 float* probs, void* stream) {
+  API_GUARD({
+    auto* p = as<TextModel>(m, KIND_TEXT);
+    if (!p) return -1;
+    return p->forward(ids, mask, B, L, cls, logits, probs, S(stream));
+  })
+}
+
+int mec_image_fwd(mec_model* m, const uint8_t* gray, int B, float* feat, float* logits, float* probs,
+                  void* stream) {
+  API_GUARD({
+    auto* p = as<ImageModel>(m, KIND_IMAGE);
+    if (!p) return -1;
+    return p->forward(gray, B, feat, logits, probs, S(stream));
+  })
+}
+
+int mec_fusion_fwd(mec_model* m, const float* s_feat, const float* t_feat, const float* i_feat, const float* s_pred,
+                   const float* t_pred, const float* i_pred, int B, float* logits, float* probs, float* attn_w,
+                   float* dec_w, void* stream) {
+  API_GUARD({
+    auto* p = as<FusionModel>(m, KIND_FUSION);
+    if (!p) return -1;
+    return p->forward(s_feat, t_feat, i_feat, s_pred, t_pred, i_pred, B, logits, probs, attn_w, dec_w, S(stream));
+  })
+}
+
+int mec_fuse_weighted(const float* s, const float* t, const float* i, int B, double* out, void* stream) {
+  API_GUARD({ return fuse_weighted(s, t, i, B, out, S(stream)); })
+}
+
+int mec_resize_u8(const uint8_t* in, int B, int H, int W, uint8_t* out, int OH, int OW, void* stream) {
+  API_GUARD({ return resize_u8(in, B, H, W, out, OH, OW, S(stream)); })
+}
+
+int mec_gemm_f16(const void* A, const void* B, const float* bias, const void* R, int r_is_f32, void* C16,
+                 float* C32, int M, int N, int K, int act, void* stream) {
+  API_GUARD({
+    GemmParams g;
+    g.A = A; g.B = reinterpret_cast<const f16*>(B); g.bias = bias; g.R = R; g.r_f32 = r_is_f32;
+    g.C16 = reinterpret_cast<f16*>(C16); g.C32 = C32; g.M = M; g.N = N; g.K = K; g.act = act;
+    return launch_gemm(g, S(stream), nullptr, TAG_NONE);
+  })
+}
+
+int mec_conv_f16(const void* x, const void* w, const float* bias, const void* R, void* y, int n, int H, int W,
+                 int C, int Cout, int ks, int stride, int pad, int act, void* stream) {
+  API_GUARD({
+    GemmParams g;
+    g.amode = A_CONV; g.A = x; g.B = reinterpret_cast<const f16*>(w); g.bias = bias; g.R = R;
+    g.C16 = reinterpret_cast<f16*>(y); g.act = act;
+    g.H = H; g.W = W; g.C = C; g.ks = ks; g.stride = stride; g.pad = pad;
+    g.OH = (H + 2 * pad - ks) / stride + 1; g.OW = (W + 2 * pad - ks) / stride + 1;
+    g.M = n * g.OH * g.OW; g.N = Cout; g.K = ks * ks * C;
+    return launch_gemm(g, S(stream), nullptr, TAG_NONE);
+  })
+}
+
+int mec_prof_enable(mec_model* m, int tag) {
+  if (!m || !m->impl) { set_error("null model handle"); return -1; }
+  m->impl->prof.tag = tag;
+  m->impl->prof.reset();
+  return 0;
+}
+
+int mec_prof_read(mec_model* m, double* total_ms, int* count) {
+  if (!m || !m->impl || !total_ms || !count) { set_error("mec_prof_read: bad args"); return -1; }
+  return m->impl->prof.read(total_ms, count);
+}
+
+}  // extern "C"

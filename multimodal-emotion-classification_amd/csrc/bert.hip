@@ -1,0 +1,392 @@
+// BERT-base encoder + sequence-classification head (the arithmetic the reference runs
+// through transformers' BertForSequenceClassification: inference/text_inference.py:41,
+// :92-93, :124-128; transformers==4.30.0 eager attention, requirements.txt:16).
+//
+// Per layer (M = B*L token rows; residual stream kept in fp32, GEMM operands in f16):
+//   qkv16  = h16 . Wqkv^T + b                    gemm (N=2304)
+//   ctx16  = softmax(QK^T/8 + mask_bias) V       bert_attention_kernel (MFMA, LDS)
+//   t32    = ctx16 . Wo^T + bo + h32             gemm, f32 out (residual fused)
+//   h      = LN(t32)  -> h32, h16                layernorm_kernel (eps 1e-12)
+//   i16    = GELU(h16 . Wi^T + bi)               gemm (N=3072), erf-GELU fused
+//   t32    = i16 . Wo2^T + bo2 + h32             gemm, f32 out
+//   h      = LN(t32)
+// Head: cls = h32[:,0,:] (pre-pooler CLS feature, text_inference.py:125);
+//       probs = softmax(Wc tanh(Wp cls + bp) + bc).
+#include "block_ops.h"
+#include "models.h"
+
+namespace mec {
+
+constexpr int BH = 768, BI = 3072, BHEADS = 12, BDH = 64, BLAYERS = 12, BVOCAB = 30522, BMAXPOS = 512;
+
+// ----------------------------------------------------------------------------- embed+LN
+// One wave per token row; each lane owns 12 of the 768 features (3 float4).
+__global__ __launch_bounds__(256) void bert_embed_ln_kernel(const int32_t* __restrict__ ids, int M, int L,
+                                                            const float* __restrict__ word,
+                                                            const float* __restrict__ pos,
+                                                            const float* __restrict__ type,
+                                                            const float* __restrict__ g,
+                                                            const float* __restrict__ b, float* h32,
+                                                            f16* h16) {
+  const int lane = threadIdx.x & 63;
+  const int row = blockIdx.x * 4 + (threadIdx.x >> 6);
+  if (row >= M) return;
+  int id = ids[row];
+  id = id < 0 ? 0 : (id >= BVOCAB ? BVOCAB - 1 : id);
+  const int l = row % L;
+  float v[12];
+#pragma unroll
+  for (int j = 0; j < 3; ++j) {
+    const int c = j * 256 + lane * 4;
+    const float4 w = *reinterpret_cast<const float4*>(word + (size_t)id * BH + c);
+    const float4 t = *reinterpret_cast<const float4*>(type + c);
+    const float4 p = *reinterpret_cast<const float4*>(pos + (size_t)l * BH + c);
+    // HF: (inputs_embeds + token_type_embeddings) + position_embeddings
+    v[4 * j + 0] = (w.x + t.x) + p.x;
+    v[4 * j + 1] = (w.y + t.y) + p.y;
+    v[4 * j + 2] = (w.z + t.z) + p.z;
+    v[4 * j + 3] = (w.w + t.w) + p.w;
+  }
+  float s = 0.f;
+#pragma unroll
+  for (int i = 0; i < 12; ++i) s += v[i];
+  const float mean = wave_sum(s) * (1.0f / BH);
+  float q = 0.f;
+#pragma unroll
+  for (int i = 0; i < 12; ++i) { const float d = v[i] - mean; q += d * d; }
+  const float rstd = 1.0f / sqrtf(wave_sum(q) * (1.0f / BH) + 1e-12f);
+#pragma unroll
+  for (int j = 0; j < 3; ++j) {
+    const int c = j * 256 + lane * 4;
+    float4 o;
+    o.x = (v[4 * j + 0] - mean) * rstd * g[c + 0] + b[c + 0];
+    o.y = (v[4 * j + 1] - mean) * rstd * g[c + 1] + b[c + 1];
+    o.z = (v[4 * j + 2] - mean) * rstd * g[c + 2] + b[c + 2];
+    o.w = (v[4 * j + 3] - mean) * rstd * g[c + 3] + b[c + 3];
+    *reinterpret_cast<float4*>(h32 + (size_t)row * BH + c) = o;
+    half4 hh = {(f16)o.x, (f16)o.y, (f16)o.z, (f16)o.w};
+    *reinterpret_cast<half4*>(h16 + (size_t)row * BH + c) = hh;
+  }
+}
+
+// ----------------------------------------------------------------------------- LayerNorm
+__global__ __launch_bounds__(256) void bert_layernorm_kernel(const float* __restrict__ x, int M,
+                                                             const float* __restrict__ g,
+                                                             const float* __restrict__ b, float* h32,
+                                                             f16* h16) {
+  const int lane = threadIdx.x & 63;
+  const int row = blockIdx.x * 4 + (threadIdx.x >> 6);
+  if (row >= M) return;
+  float v[12];
+#pragma unroll
+  for (int j = 0; j < 3; ++j) {
+    const float4 t = *reinterpret_cast<const float4*>(x + (size_t)row * BH + j * 256 + lane * 4);
+    v[4 * j + 0] = t.x; v[4 * j + 1] = t.y; v[4 * j + 2] = t.z; v[4 * j + 3] = t.w;
+  }
+  float s = 0.f;
+#pragma unroll
+  for (int i = 0; i < 12; ++i) s += v[i];
+  const float mean = wave_sum(s) * (1.0f / BH);
+  float q = 0.f;
+#pragma unroll
+  for (int i = 0; i < 12; ++i) { const float d = v[i] - mean; q += d * d; }
+  const float rstd = 1.0f / sqrtf(wave_sum(q) * (1.0f / BH) + 1e-12f);
+#pragma unroll
+  for (int j = 0; j < 3; ++j) {
+    const int c = j * 256 + lane * 4;
+    float4 o;
+    o.x = (v[4 * j + 0] - mean) * rstd * g[c + 0] + b[c + 0];
+    o.y = (v[4 * j + 1] - mean) * rstd * g[c + 1] + b[c + 1];
+    o.z = (v[4 * j + 2] - mean) * rstd * g[c + 2] + b[c + 2];
+    o.w = (v[4 * j + 3] - mean) * rstd * g[c + 3] + b[c + 3];
+    *reinterpret_cast<float4*>(h32 + (size_t)row * BH + c) = o;
+    half4 hh = {(f16)o.x, (f16)o.y, (f16)o.z, (f16)o.w};
+    *reinterpret_cast<half4*>(h16 + (size_t)row * BH + c) = hh;
+  }
+}
+
+// ----------------------------------------------------------------------------- attention
+// One workgroup per (sequence, head), L = 128 (padding='max_length', text_inference.py:
+// 81-83). Wave w owns queries 32w..32w+31. S^T = K Q^T is computed so that each lane holds
+// one query's scores (keys in registers): the row softmax is lane-local plus one
+// cross-half shuffle, and the f32 score tile becomes the B operand of O^T = V^T P^T with
+// no LDS round trip (k order permuted; V^T is read to match).
+constexpr int ATT_L = 128;
+constexpr int VT_LD = ATT_L + 4;  // padded row (264 B): conflict-free ds_read_b64
+
+__device__ __forceinline__ int aswz(int row, int kc) { return kc ^ ((row >> 1) & 7); }
+
+__global__ __launch_bounds__(256) void bert_attention_kernel(const f16* __restrict__ qkv,
+                                                             const int32_t* __restrict__ mask,
+                                                             f16* __restrict__ ctx) {
+  __shared__ __attribute__((aligned(16))) f16 sQ[ATT_L * BDH];
+  __shared__ __attribute__((aligned(16))) f16 sK[ATT_L * BDH];
+  __shared__ __attribute__((aligned(16))) f16 sVt[BDH * VT_LD];
+  __shared__ float sBias[ATT_L];
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int b = blockIdx.x / BHEADS, h = blockIdx.x - (blockIdx.x / BHEADS) * BHEADS;
+  const f16* base = qkv + (size_t)b * ATT_L * (3 * BH) + h * BDH;
+#pragma unroll
+  for (int i = 0; i < 4; ++i) {
+    const int c = tid + 256 * i;
+    const int row = c >> 3, kc = c & 7;
+    const f16* src = base + (size_t)row * (3 * BH) + kc * 8;
+    const uint4 q = *reinterpret_cast<const uint4*>(src);
+    const uint4 k = *reinterpret_cast<const uint4*>(src + BH);
+    const uint4 v = *reinterpret_cast<const uint4*>(src + 2 * BH);
+    *reinterpret_cast<uint4*>(sQ + row * BDH + aswz(row, kc) * 8) = q;
+    *reinterpret_cast<uint4*>(sK + row * BDH + aswz(row, kc) * 8) = k;
+    const f16* vv = reinterpret_cast<const f16*>(&v);
+#pragma unroll
+    for (int e = 0; e < 8; ++e) sVt[(kc * 8 + e) * VT_LD + row] = vv[e];
+  }
+  if (tid < ATT_L) sBias[tid] = mask[(size_t)b * ATT_L + tid] ? 0.f : -3.4028234663852886e38f;  // finfo(f32).min
+  __syncthreads();
+
+  const int lr = lane & 31, lh = lane >> 5;
+  floatx16 s[4];
+#pragma unroll
+  for (int t = 0; t < 4; ++t) {
+#pragma unroll
+    for (int e = 0; e < 16; ++e) s[t][e] = 0.f;
+#pragma unroll
+    for (int kk = 0; kk < 4; ++kk) {
+      const int kc = 2 * kk + lh;
+      const int rk = 32 * t + lr, rq = 32 * wave + lr;
+      const half8 a = *reinterpret_cast<const half8*>(sK + rk * BDH + aswz(rk, kc) * 8);
+      const half8 bq = *reinterpret_cast<const half8*>(sQ + rq * BDH + aswz(rq, kc) * 8);
+      s[t] = __builtin_amdgcn_mfma_f32_32x32x16_f16(a, bq, s[t], 0, 0, 0);
+    }
+  }
+  // s[t][e] = S[query 32w+lr][key 32t + (e&3) + 8(e>>2) + 4lh]
+  float mx = -INFINITY;
+#pragma unroll
+  for (int t = 0; t < 4; ++t)
+#pragma unroll
+    for (int e = 0; e < 16; ++e) {
+      const int key = 32 * t + (e & 3) + 8 * (e >> 2) + 4 * lh;
+      const float v = s[t][e] * 0.125f + sBias[key];  // /sqrt(64) then + additive mask
+      s[t][e] = v;
+      mx = fmaxf(mx, v);
+    }
+  mx = fmaxf(mx, __shfl_xor(mx, 32, 64));
+  float sum = 0.f;
+#pragma unroll
+  for (int t = 0; t < 4; ++t)
+#pragma unroll
+    for (int e = 0; e < 16; ++e) {
+      const float p = expf(s[t][e] - mx);
+      s[t][e] = p;
+      sum += p;
+    }
+  sum += __shfl_xor(sum, 32, 64);
+  const float inv = 1.0f / sum;
+
+  floatx16 o[2];
+#pragma unroll
+  for (int u = 0; u < 2; ++u)
+#pragma unroll
+    for (int e = 0; e < 16; ++e) o[u][e] = 0.f;
+#pragma unroll
+  for (int st = 0; st < 8; ++st) {
+    const int t = st >> 1, sp = st & 1;
+    half8 pb;
+#pragma unroll
+    for (int j = 0; j < 8; ++j) pb[j] = (f16)(s[t][8 * sp + j] * inv);
+    const int kb = 32 * t + 16 * sp + 4 * lh;  // keys kb..kb+3 (j<4) and kb+8..kb+11 (j>=4)
+#pragma unroll
+    for (int u = 0; u < 2; ++u) {
+      const int d = 32 * u + lr;
+      const half4 lo = *reinterpret_cast<const half4*>(sVt + d * VT_LD + kb);
+      const half4 hi = *reinterpret_cast<const half4*>(sVt + d * VT_LD + kb + 8);
+      half8 va = {lo[0], lo[1], lo[2], lo[3], hi[0], hi[1], hi[2], hi[3]};
+      o[u] = __builtin_amdgcn_mfma_f32_32x32x16_f16(va, pb, o[u], 0, 0, 0);
+    }
+  }
+  // o[u][e] = O[query 32w+lr][d = 32u + (e&3) + 8(e>>2) + 4lh]
+  f16* dst = ctx + ((size_t)b * ATT_L + 32 * wave + lr) * BH + h * BDH;
+#pragma unroll
+  for (int u = 0; u < 2; ++u)
+#pragma unroll
+    for (int gq = 0; gq < 4; ++gq) {
+      half4 hv = {(f16)o[u][4 * gq + 0], (f16)o[u][4 * gq + 1], (f16)o[u][4 * gq + 2], (f16)o[u][4 * gq + 3]};
+      *reinterpret_cast<half4*>(dst + 32 * u + 8 * gq + 4 * lh) = hv;
+    }
+}
+
+// ----------------------------------------------------------------------------- head
+constexpr int HEAD_R = 8;
+__global__ __launch_bounds__(256) void bert_head_kernel(const float* __restrict__ h32, int B, int L,
+                                                        const float* __restrict__ WpT, const float* __restrict__ bp,
+                                                        const float* __restrict__ WcT, const float* __restrict__ bc,
+                                                        float* cls, float* logits, float* probs) {
+  constexpr int R = HEAD_R;
+  __shared__ float X[R * BH], Y[R * BH], red[R * 256];
+  const int tid = threadIdx.x;
+  const int r0 = blockIdx.x * R, nr = min(R, B - r0);
+  for (int idx = tid; idx < R * BH; idx += blockDim.x) {
+    const int r = idx / BH, c = idx - r * BH;
+    const float v = r < nr ? h32[((size_t)(r0 + r) * L) * BH + c] : 0.f;
+    X[idx] = v;
+    if (r < nr) cls[(size_t)(r0 + r) * BH + c] = v;
+  }
+  __syncthreads();
+  block_linear<R>(X, BH, BH, WpT, bp, BH, Y, BH, red);
+  for (int idx = tid; idx < R * BH; idx += blockDim.x) Y[idx] = tanhf(Y[idx]);
+  __syncthreads();
+  block_linear<R>(Y, BH, BH, WcT, bc, 7, X, BH, red);
+  for (int idx = tid; idx < nr * 7; idx += blockDim.x) {
+    const int r = idx / 7, c = idx - r * 7;
+    logits[(size_t)(r0 + r) * 7 + c] = X[r * BH + c];
+  }
+  __syncthreads();
+  block_softmax_small<R>(X, BH, 7, nullptr, 0);
+  for (int idx = tid; idx < nr * 7; idx += blockDim.x) {
+    const int r = idx / 7, c = idx - r * 7;
+    probs[(size_t)(r0 + r) * 7 + c] = X[r * BH + c];
+  }
+}
+
+// ----------------------------------------------------------------------------- model
+// prm layout per layer (floats): bqkv 2304 | bo 768 | ln1g 768 | ln1b 768 | bi 3072 | bo2 768 |
+// ln2g 768 | ln2b 768  => 9984 ; then head: WpT 768*768 | bp 768 | WcT 768*7 | bc 7
+constexpr size_t PRM_LAYER = 2304 + 768 * 3 + 3072 + 768 * 3;
+constexpr size_t WT_LAYER = (size_t)2304 * 768 + 768 * 768 + 3072 * 768 + 768 * 3072;
+
+static void to_f16(std::vector<f16>& dst, size_t off, const float* src, size_t n) {
+  for (size_t i = 0; i < n; ++i) dst[off + i] = (f16)src[i];
+}
+
+int TextModel::create(const float* blob, size_t n) {
+  BlobReader rd(blob, n);
+  std::vector<float> e;
+  const float* word = rd.take((size_t)BVOCAB * BH);
+  const float* pos = rd.take((size_t)BMAXPOS * BH);
+  const float* type = rd.take(2 * BH);
+  const float* lg = rd.take(BH);
+  const float* lb = rd.take(BH);
+  if (!rd.ok) { set_error("text blob too small"); return -1; }
+  e.insert(e.end(), word, word + (size_t)BVOCAB * BH);
+  e.insert(e.end(), pos, pos + (size_t)BMAXPOS * BH);
+  e.insert(e.end(), type, type + 2 * BH);
+  e.insert(e.end(), lg, lg + BH);
+  e.insert(e.end(), lb, lb + BH);
+  std::vector<f16> w(WT_LAYER * BLAYERS);
+  std::vector<float> pr(PRM_LAYER * BLAYERS + (size_t)BH * BH + BH + BH * 7 + 7);
+  for (int l = 0; l < BLAYERS; ++l) {
+    f16* dummy = nullptr;
+    (void)dummy;
+    const size_t wo = WT_LAYER * l;
+    const size_t po = PRM_LAYER * l;
+    // Wqkv rows: query | key | value (torch Linear weight [out,in] = GEMM B [N,K])
+    for (int q = 0; q < 3; ++q) {
+      to_f16(w, wo + (size_t)q * BH * BH, rd.take((size_t)BH * BH), (size_t)BH * BH);
+      const float* bb = rd.take(BH);
+      std::copy(bb, bb + BH, pr.begin() + po + q * BH);
+    }
+    to_f16(w, wo + (size_t)2304 * BH, rd.take((size_t)BH * BH), (size_t)BH * BH);
+    { const float* x = rd.take(BH); std::copy(x, x + BH, pr.begin() + po + 2304); }
+    { const float* x = rd.take(BH); std::copy(x, x + BH, pr.begin() + po + 2304 + 768); }
+    { const float* x = rd.take(BH); std::copy(x, x + BH, pr.begin() + po + 2304 + 1536); }
+    to_f16(w, wo + (size_t)2304 * BH + BH * BH, rd.take((size_t)BI * BH), (size_t)BI * BH);
+    { const float* x = rd.take(BI); std::copy(x, x + BI, pr.begin() + po + 2304 + 2304); }
+    to_f16(w, wo + (size_t)2304 * BH + BH * BH + (size_t)BI * BH, rd.take((size_t)BH * BI), (size_t)BH * BI);
+    { const float* x = rd.take(BH); std::copy(x, x + BH, pr.begin() + po + 2304 + 2304 + 3072); }
+    { const float* x = rd.take(BH); std::copy(x, x + BH, pr.begin() + po + 2304 + 2304 + 3072 + 768); }
+    { const float* x = rd.take(BH); std::copy(x, x + BH, pr.begin() + po + 2304 + 2304 + 3072 + 1536); }
+  }
+  size_t ho = PRM_LAYER * BLAYERS;
+  const float* wp = rd.take((size_t)BH * BH);
+  const float* bp = rd.take(BH);
+  const float* wc = rd.take((size_t)7 * BH);
+  const float* bc = rd.take(7);
+  MEC_REQUIRE(rd.ok && rd.off == n, "text blob size mismatch");
+  for (int i = 0; i < BH; ++i)
+    for (int j = 0; j < BH; ++j) pr[ho + (size_t)i * BH + j] = wp[(size_t)j * BH + i];
+  ho += (size_t)BH * BH;
+  std::copy(bp, bp + BH, pr.begin() + ho);
+  ho += BH;
+  for (int i = 0; i < BH; ++i)
+    for (int j = 0; j < 7; ++j) pr[ho + (size_t)i * 7 + j] = wc[(size_t)j * BH + i];
+  ho += (size_t)BH * 7;
+  std::copy(bc, bc + 7, pr.begin() + ho);
+  MEC_TRY(upload(emb, e.data(), e.size() * sizeof(float)));
+  MEC_TRY(upload(wts, w.data(), w.size() * sizeof(f16)));
+  MEC_TRY(upload(prm, pr.data(), pr.size() * sizeof(float)));
+  return 0;
+}
+
+int TextModel::forward(const int32_t* ids, const int32_t* mask, int B, int L, float* cls, float* logits,
+                       float* probs, hipStream_t s) {
+  MEC_REQUIRE(B >= 0, "text: B < 0");
+  if (B == 0) return 0;
+  MEC_REQUIRE(L == ATT_L, "text: L must be 128 (padding='max_length', MAX_TEXT_LENGTH=128)");
+  MEC_REQUIRE(ids && mask && cls && logits && probs, "text: null pointer");
+  const int M = B * L;
+  // workspace: h32 | t32 (f32 [M,768]) ; h16 | ctx16 (f16 [M,768]) ; qkv16 [M,2304] / i16 [M,3072]
+  const size_t need = (size_t)M * BH * 4 * 2 + (size_t)M * BH * 2 * 2 + (size_t)M * BI * 2;
+  if (M > ws_tokens) {
+    MEC_TRY(ws.ensure(need));
+    ws_tokens = M;
+  }
+  char* p = ws.as<char>();
+  float* h32 = reinterpret_cast<float*>(p); p += (size_t)M * BH * 4;
+  float* t32 = reinterpret_cast<float*>(p); p += (size_t)M * BH * 4;
+  f16* h16 = reinterpret_cast<f16*>(p); p += (size_t)M * BH * 2;
+  f16* ctx16 = reinterpret_cast<f16*>(p); p += (size_t)M * BH * 2;
+  f16* big16 = reinterpret_cast<f16*>(p);  // qkv16 [M,2304] then i16 [M,3072]
+
+  const float* E = emb.as<float>();
+  const float* word = E;
+  const float* pos = word + (size_t)BVOCAB * BH;
+  const float* type = pos + (size_t)BMAXPOS * BH;
+  const float* lng = type + 2 * BH;
+  const float* lnb = lng + BH;
+  const dim3 rows_grid((M + 3) / 4);
+  hipLaunchKernelGGL(bert_embed_ln_kernel, rows_grid, dim3(256), 0, s, ids, M, L, word, pos, type, lng, lnb, h32,
+                     h16);
+  MEC_LAUNCH_CHECK();
+  const f16* W = wts.as<f16>();
+  const float* P = prm.as<float>();
+  for (int l = 0; l < BLAYERS; ++l) {
+    const f16* wqkv = W + WT_LAYER * l;
+    const f16* wo = wqkv + (size_t)2304 * BH;
+    const f16* wi = wo + (size_t)BH * BH;
+    const f16* wo2 = wi + (size_t)BI * BH;
+    const float* pl = P + PRM_LAYER * l;
+    const float *bqkv = pl, *bo = pl + 2304, *g1 = pl + 3072, *b1 = pl + 3840, *bi = pl + 4608,
+                *bo2 = pl + 7680, *g2 = pl + 8448, *b2 = pl + 9216;
+    GemmParams g;
+    g.A = h16; g.B = wqkv; g.bias = bqkv; g.C16 = big16; g.M = M; g.N = 2304; g.K = BH;
+    MEC_TRY(launch_gemm(g, s, &prof, TAG_BERT_QKV));
+    MEC_TRY(prof.begin(TAG_BERT_ATTN, s));
+    hipLaunchKernelGGL(bert_attention_kernel, dim3(B * BHEADS), dim3(256), 0, s, big16, mask, ctx16);
+    MEC_LAUNCH_CHECK();
+    MEC_TRY(prof.end(TAG_BERT_ATTN, s));
+    g = GemmParams();
+    g.A = ctx16; g.B = wo; g.bias = bo; g.R = h32; g.r_f32 = 1; g.C32 = t32; g.M = M; g.N = BH; g.K = BH;
+    MEC_TRY(launch_gemm(g, s, &prof, TAG_BERT_OPROJ));
+    MEC_TRY(prof.begin(TAG_BERT_LN, s));
+    hipLaunchKernelGGL(bert_layernorm_kernel, rows_grid, dim3(256), 0, s, t32, M, g1, b1, h32, h16);
+    MEC_LAUNCH_CHECK();
+    MEC_TRY(prof.end(TAG_BERT_LN, s));
+    g = GemmParams();
+    g.A = h16; g.B = wi; g.bias = bi; g.act = ACT_GELU; g.C16 = big16; g.M = M; g.N = BI; g.K = BH;
+    MEC_TRY(launch_gemm(g, s, &prof, TAG_BERT_FFN1));
+    g = GemmParams();
+    g.A = big16; g.B = wo2; g.bias = bo2; g.R = h32; g.r_f32 = 1; g.C32 = t32; g.M = M; g.N = BH; g.K = BI;
+    MEC_TRY(launch_gemm(g, s, &prof, TAG_BERT_FFN2));
+    MEC_TRY(prof.begin(TAG_BERT_LN, s));
+    hipLaunchKernelGGL(bert_layernorm_kernel, rows_grid, dim3(256), 0, s, t32, M, g2, b2, h32, h16);
+    MEC_LAUNCH_CHECK();
+    MEC_TRY(prof.end(TAG_BERT_LN, s));
+  }
+  const float* head = P + PRM_LAYER * BLAYERS;
+  const float *WpT = head, *bp = WpT + (size_t)BH * BH, *WcT = bp + BH, *bc = WcT + (size_t)BH * 7;
+  hipLaunchKernelGGL(bert_head_kernel, dim3((B + HEAD_R - 1) / HEAD_R), dim3(256), 0, s, h32, B, L, WpT, bp, WcT,
+                     bc, cls, logits, probs);
+  MEC_LAUNCH_CHECK();
+  return 0;
+}
+
+}  // namespace mec

@@ -1,0 +1,121 @@
+// Shared definitions for the MI355X (gfx950) emotion-inference HIP library.
+#pragma once
+#include <hip/hip_runtime.h>
+#include <cstddef>
+#include <cstdint>
+#include <string>
+#include <vector>
+
+typedef _Float16 f16;
+typedef _Float16 half8 __attribute__((ext_vector_type(8)));
+typedef _Float16 half4 __attribute__((ext_vector_type(4)));
+typedef float floatx16 __attribute__((ext_vector_type(16)));
+typedef float floatx4 __attribute__((ext_vector_type(4)));
+
+namespace mec {
+
+void set_error(const std::string& msg);
+
+#define MEC_HIP(x)                                                                        \
+  do {                                                                                    \
+    hipError_t e_ = (x);                                                                  \
+    if (e_ != hipSuccess) {                                                               \
+      ::mec::set_error(std::string(#x) + " failed: " + hipGetErrorString(e_) + " @" +     \
+                       __FILE__ + ":" + std::to_string(__LINE__));                        \
+      return -1;                                                                          \
+    }                                                                                     \
+  } while (0)
+
+#define MEC_REQUIRE(cond, msg)                                                            \
+  do {                                                                                    \
+    if (!(cond)) {                                                                        \
+      ::mec::set_error(std::string("requirement failed: ") + (msg));                     \
+      return -1;                                                                          \
+    }                                                                                     \
+  } while (0)
+
+#define MEC_TRY(x)                                                                        \
+  do {                                                                                    \
+    if ((x) != 0) return -1;                                                              \
+  } while (0)
+
+#define MEC_LAUNCH_CHECK() MEC_HIP(hipGetLastError())
+
+// Kernel tags for the hipEvent timing hook (mec_prof_enable); see DESIGN.md §Measurement.
+enum KernelTag : int {
+  TAG_NONE = 0,
+  TAG_BERT_QKV = 1,
+  TAG_BERT_ATTN = 2,
+  TAG_BERT_OPROJ = 3,
+  TAG_BERT_FFN1 = 4,
+  TAG_BERT_FFN2 = 5,
+  TAG_BERT_LN = 6,
+  TAG_RESNET_CONV3X3 = 7,
+  TAG_RESNET_CONV1X1 = 8,
+  TAG_RESNET_STEM = 9,
+  TAG_SPEECH = 10,
+  TAG_FUSION = 11,
+};
+
+// hipEvent pairs recorded around every launch whose tag matches `tag`.
+struct Prof {
+  int tag = TAG_NONE;
+  std::vector<hipEvent_t> ev;
+  size_t used = 0;
+  int begin(int t, hipStream_t s);
+  int end(int t, hipStream_t s);
+  int read(double* total_ms, int* count);
+  void reset() { used = 0; }
+  ~Prof();
+};
+
+// Device buffer owned by a model handle (grow-only).
+struct DevBuf {
+  void* p = nullptr;
+  size_t bytes = 0;
+  int ensure(size_t n);
+  void release();
+  template <class T> T* as() const { return reinterpret_cast<T*>(p); }
+  ~DevBuf() { release(); }
+};
+
+int upload(DevBuf& b, const void* host, size_t bytes);
+
+// Sequential reader over the canonical fp32 host blob (mec/synthetic.py: spec()).
+struct BlobReader {
+  const float* p;
+  size_t n, off = 0;
+  bool ok = true;
+  BlobReader(const float* p_, size_t n_) : p(p_), n(n_) {}
+  const float* take(size_t count) {
+    if (off + count > n) { ok = false; return p; }
+    const float* r = p + off;
+    off += count;
+    return r;
+  }
+};
+
+// fp16 MFMA GEMM / implicit-GEMM convolution ------------------------------------------
+// C[M,N] = epilogue( A'[M,K] . B[N,K]^T ), A' = A (plain) or the im2col view of an NHWC
+// tensor (conv), or the folded single-channel stem view of a u8 image (stem).
+enum AMode : int { A_PLAIN = 0, A_CONV = 1, A_STEM = 2 };
+enum Act : int { ACT_NONE = 0, ACT_RELU = 1, ACT_GELU = 2 };
+
+struct GemmParams {
+  const void* A = nullptr;   // f16 [M,K] | f16 NHWC [n,H,W,C] | u8 [n,H,W]
+  const f16* B = nullptr;    // f16 [N,K], K contiguous
+  const float* bias = nullptr;  // [N]
+  const void* R = nullptr;      // residual [M,N] (f16 or f32) or null
+  int r_f32 = 0;
+  f16* C16 = nullptr;           // [M,N] f16 out or null
+  float* C32 = nullptr;         // [M,N] f32 out or null
+  int M = 0, N = 0, K = 0;
+  int act = ACT_NONE;
+  int amode = A_PLAIN;
+  // conv / stem geometry (NHWC input)
+  int H = 1, W = 1, C = 0, OH = 1, OW = 1, ks = 1, stride = 1, pad = 0;
+};
+
+int launch_gemm(const GemmParams& p, hipStream_t s, Prof* prof, int tag);
+
+}  // namespace mec

@@ -1,0 +1,76 @@
+// Model handles behind the C-ABI (include/mec.h). Each handle owns its packed device
+// weights and a grow-only activation workspace; forwards are asynchronous on the caller's
+// stream. One handle is used by one host thread at a time (the Python wrapper locks).
+#pragma once
+#include "mec_common.h"
+
+namespace mec {
+
+enum ModelKind : int { KIND_SPEECH = 0, KIND_TEXT = 1, KIND_IMAGE = 2, KIND_FUSION = 3 };
+
+size_t blob_floats(int kind);
+
+struct Model {
+  int kind = -1;
+  int device = 0;
+  Prof prof;
+  virtual ~Model() {}
+};
+
+// ---------------------------------------------------------------- speech DNN
+struct SpeechModel : Model {
+  DevBuf w;  // fp32: mean, scale, {W,b,inv,shift} x5, W6, b6
+  size_t off_mean = 0, off_scale = 0, off_W[6] = {}, off_b[6] = {}, off_inv[5] = {}, off_shift[5] = {};
+  int create(const float* blob, size_t n);
+  int forward(const float* x, int B, float* feat, float* logits, float* probs, hipStream_t s);
+};
+
+// ---------------------------------------------------------------- fusion model
+struct FusionModel : Model {
+  DevBuf w;  // fp32, transposed Linear weights ([in][out]) + biases + LN params
+  std::vector<size_t> off;  // offsets by FusionParam index
+  int create(const float* blob, size_t n);
+  int forward(const float* sf, const float* tf, const float* imf, const float* sp, const float* tp,
+              const float* ip, int B, float* logits, float* probs, float* attn_w, float* dec_w,
+              hipStream_t s);
+};
+
+int fuse_weighted(const float* s, const float* t, const float* i, int B, double* out, hipStream_t st);
+
+// ---------------------------------------------------------------- BERT-base
+struct TextModel : Model {
+  DevBuf emb;      // fp32 word | pos | type | ln_g | ln_b
+  DevBuf wts;      // f16 per layer: Wqkv[2304x768] Wo[768x768] Wi[3072x768] Wo2[768x3072]
+  DevBuf prm;      // fp32 per layer: bqkv bo ln1g ln1b bi bo2 ln2g ln2b ; head: WpT bp WcT bc
+  DevBuf ws;       // workspace
+  int ws_tokens = 0;
+  int create(const float* blob, size_t n);
+  int forward(const int32_t* ids, const int32_t* mask, int B, int L, float* cls, float* logits,
+              float* probs, hipStream_t s);
+};
+
+// ---------------------------------------------------------------- ResNet50 + head
+struct ConvLayer {
+  size_t w_off = 0;   // f16 [Cout][kh][kw][Cin] (BN scale folded)
+  size_t b_off = 0;   // f32 [Cout] (BN shift)
+  int cin = 0, cout = 0, ks = 1, stride = 1, pad = 0;
+};
+struct Bottleneck {
+  ConvLayer c1, c2, c3, ds;
+  bool has_ds = false;
+};
+struct ImageModel : Model {
+  DevBuf wts;   // f16 conv weights
+  DevBuf prm;   // fp32 biases, stem weights, head
+  DevBuf ws;    // workspace
+  int ws_batch = 0;
+  ConvLayer stem;
+  std::vector<Bottleneck> blocks;
+  size_t fc1_off = 0, fc1b_off = 0, fc2_off = 0, fc2b_off = 0;
+  int create(const float* blob, size_t n);
+  int forward(const uint8_t* gray, int B, float* feat, float* logits, float* probs, hipStream_t s);
+};
+
+int resize_u8(const uint8_t* in, int B, int H, int W, uint8_t* out, int OH, int OW, hipStream_t s);
+
+}  // namespace mec

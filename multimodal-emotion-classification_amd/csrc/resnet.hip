@@ -1,0 +1,361 @@
+// Image path: PIL-exact bilinear resize (u8) -> ResNet50 (NHWC f16, BN folded, MFMA
+// implicit-GEMM convs) -> avgpool + 2048->512->7 head (fp32), restating
+// inference/image_inference.py:28-32 (transform), :55-65 (network + head), :70-90 (512-d
+// fc[2] feature), :117-119 (softmax).
+#include <cmath>
+
+#include "block_ops.h"
+#include "models.h"
+
+namespace mec {
+
+// ----------------------------------------------------------------------------- resize
+// Pillow ImagingResample (bilinear, 8bpc): 22-bit fixed-point taps, horizontal pass into
+// a u8 intermediate, then the vertical pass; clip8((acc + 2^21) >> 22).
+constexpr int RS_MAXK = 3;  // upscale: support 1 -> ksize = 3
+constexpr int RS_PREC = 22;
+
+struct ResizeTaps {
+  int xmin[224], xn[224], xk[224][RS_MAXK];
+  int ymin[224], yn[224], yk[224][RS_MAXK];
+};
+
+static bool make_taps(int in_size, int out_size, int* mins, int* ns, int (*kk)[RS_MAXK]) {
+  const double scale = (double)in_size / out_size;
+  const double filterscale = scale < 1.0 ? 1.0 : scale;
+  const double support = 1.0 * filterscale;
+  const int ksize = (int)std::ceil(support) * 2 + 1;
+  if (ksize > RS_MAXK) return false;  // downscale not needed on this path
+  for (int xx = 0; xx < out_size; ++xx) {
+    const double center = (xx + 0.5) * scale;
+    const double ss = 1.0 / filterscale;
+    int xmin = (int)(center - support + 0.5);
+    if (xmin < 0) xmin = 0;
+    int xmax = (int)(center + support + 0.5);
+    if (xmax > in_size) xmax = in_size;
+    xmax -= xmin;
+    double w[RS_MAXK] = {0, 0, 0}, ww = 0.0;
+    for (int x = 0; x < xmax; ++x) {
+      double t = (x + xmin - center + 0.5) * ss;
+      if (t < 0) t = -t;
+      w[x] = t < 1.0 ? 1.0 - t : 0.0;
+      ww += w[x];
+    }
+    for (int x = 0; x < RS_MAXK; ++x) {
+      double v = (x < xmax && ww != 0.0) ? w[x] / ww : (x < xmax ? w[x] : 0.0);
+      kk[xx][x] = v < 0 ? (int)(-0.5 + v * (1 << RS_PREC)) : (int)(0.5 + v * (1 << RS_PREC));
+    }
+    mins[xx] = xmin;
+    ns[xx] = xmax;
+  }
+  return true;
+}
+
+template <int IH, int IW, int OH, int OW>
+__global__ __launch_bounds__(256) void resize_u8_kernel(const uint8_t* __restrict__ in, uint8_t* __restrict__ out,
+                                                        const ResizeTaps* __restrict__ taps) {
+  __shared__ uint8_t src[IH * IW];
+  __shared__ uint8_t tmp[IH * OW];
+  const int b = blockIdx.x, tid = threadIdx.x;
+  const uint8_t* im = in + (size_t)b * IH * IW;
+  for (int i = tid; i < IH * IW; i += 256) src[i] = im[i];
+  __syncthreads();
+  for (int i = tid; i < IH * OW; i += 256) {  // horizontal
+    const int y = i / OW, xx = i - y * OW;
+    int acc = 1 << (RS_PREC - 1);
+    const int x0 = taps->xmin[xx];
+    for (int x = 0; x < taps->xn[xx]; ++x) acc += (int)src[y * IW + x0 + x] * taps->xk[xx][x];
+    acc >>= RS_PREC;
+    tmp[i] = (uint8_t)(acc < 0 ? 0 : (acc > 255 ? 255 : acc));
+  }
+  __syncthreads();
+  uint8_t* o = out + (size_t)b * OH * OW;
+  for (int i = tid; i < OH * OW; i += 256) {  // vertical
+    const int yy = i / OW, x = i - yy * OW;
+    int acc = 1 << (RS_PREC - 1);
+    const int y0 = taps->ymin[yy];
+    for (int y = 0; y < taps->yn[yy]; ++y) acc += (int)tmp[(y0 + y) * OW + x] * taps->yk[yy][y];
+    acc >>= RS_PREC;
+    o[i] = (uint8_t)(acc < 0 ? 0 : (acc > 255 ? 255 : acc));
+  }
+}
+
+static ResizeTaps* g_taps = nullptr;  // device copy, built once per process
+
+static int ensure_taps() {
+  if (g_taps) return 0;
+  ResizeTaps h;
+  if (!make_taps(48, 224, h.xmin, h.xn, h.xk) || !make_taps(48, 224, h.ymin, h.yn, h.yk)) {
+    set_error("resize taps");
+    return -1;
+  }
+  MEC_HIP(hipMalloc(&g_taps, sizeof(ResizeTaps)));
+  MEC_HIP(hipMemcpy(g_taps, &h, sizeof(ResizeTaps), hipMemcpyHostToDevice));
+  return 0;
+}
+
+int resize_u8(const uint8_t* in, int B, int H, int W, uint8_t* out, int OH, int OW, hipStream_t s) {
+  MEC_REQUIRE(H == 48 && W == 48 && OH == 224 && OW == 224, "resize: only 48x48 -> 224x224 (FER2013 -> IMAGE_SIZE)");
+  if (B == 0) return 0;
+  MEC_TRY(ensure_taps());
+  hipLaunchKernelGGL((resize_u8_kernel<48, 48, 224, 224>), dim3(B), dim3(256), 0, s, in, out, g_taps);
+  MEC_LAUNCH_CHECK();
+  return 0;
+}
+
+// ----------------------------------------------------------------------------- maxpool
+// 3x3 / stride 2 / pad 1 on NHWC f16 (torch max_pool2d pads with -inf).
+__global__ __launch_bounds__(256) void maxpool3s2_kernel(const f16* __restrict__ x, f16* __restrict__ y, int B,
+                                                         int H, int W, int C, int OH, int OW) {
+  const int c8 = C / 8;
+  const size_t total = (size_t)B * OH * OW * c8;
+  const size_t i = (size_t)blockIdx.x * 256 + threadIdx.x;
+  if (i >= total) return;
+  const int cc = (int)(i % c8);
+  size_t r = i / c8;
+  const int ow = (int)(r % OW); r /= OW;
+  const int oh = (int)(r % OH);
+  const int n = (int)(r / OH);
+  float m[8];
+#pragma unroll
+  for (int e = 0; e < 8; ++e) m[e] = -INFINITY;
+  for (int kh = 0; kh < 3; ++kh) {
+    const int ih = oh * 2 - 1 + kh;
+    if (ih < 0 || ih >= H) continue;
+    for (int kw = 0; kw < 3; ++kw) {
+      const int iw = ow * 2 - 1 + kw;
+      if (iw < 0 || iw >= W) continue;
+      const uint4 v = *reinterpret_cast<const uint4*>(x + (((size_t)n * H + ih) * W + iw) * C + cc * 8);
+      const f16* hv = reinterpret_cast<const f16*>(&v);
+#pragma unroll
+      for (int e = 0; e < 8; ++e) m[e] = fmaxf(m[e], (float)hv[e]);
+    }
+  }
+  half8 o;
+#pragma unroll
+  for (int e = 0; e < 8; ++e) o[e] = (f16)m[e];
+  *reinterpret_cast<half8*>(y + (((size_t)n * OH + oh) * OW + ow) * C + cc * 8) = o;
+}
+
+// ----------------------------------------------------------------------------- head
+constexpr int IHEAD_R = 8;
+__global__ __launch_bounds__(256) void resnet_head_kernel(const f16* __restrict__ x, int B, int HW,
+                                                          const float* __restrict__ W1T, const float* __restrict__ b1,
+                                                          const float* __restrict__ W2T, const float* __restrict__ b2,
+                                                          float* feat, float* logits, float* probs) {
+  constexpr int R = IHEAD_R, C = 2048;
+  __shared__ float X[R * C];
+  __shared__ float Y[R * 512];
+  __shared__ float red[R * 256];
+  const int tid = threadIdx.x;
+  const int r0 = blockIdx.x * R, nr = min(R, B - r0);
+  // AdaptiveAvgPool2d(1): mean over the HW positions
+  for (int idx = tid; idx < R * C; idx += 256) {
+    const int r = idx / C, c = idx - r * C;
+    float s = 0.f;
+    if (r < nr) {
+      const f16* p = x + (size_t)(r0 + r) * HW * C + c;
+      for (int q = 0; q < HW; ++q) s += (float)p[(size_t)q * C];
+    }
+    X[idx] = s / (float)HW;
+  }
+  __syncthreads();
+  block_linear<R>(X, C, C, W1T, b1, 512, Y, 512, red);
+  for (int idx = tid; idx < R * 512; idx += 256) {
+    const int r = idx >> 9, n = idx & 511;
+    const float v = fmaxf(Y[idx], 0.f);
+    Y[idx] = v;
+    if (r < nr) feat[(size_t)(r0 + r) * 512 + n] = v;  // fc[2] ReLU output (extract_features)
+  }
+  __syncthreads();
+  block_linear<R>(Y, 512, 512, W2T, b2, 7, X, C, red);
+  for (int idx = tid; idx < nr * 7; idx += 256) {
+    const int r = idx / 7, c = idx - r * 7;
+    logits[(size_t)(r0 + r) * 7 + c] = X[r * C + c];
+  }
+  __syncthreads();
+  block_softmax_small<R>(X, C, 7, nullptr, 0);
+  for (int idx = tid; idx < nr * 7; idx += 256) {
+    const int r = idx / 7, c = idx - r * 7;
+    probs[(size_t)(r0 + r) * 7 + c] = X[r * C + c];
+  }
+}
+
+// ----------------------------------------------------------------------------- model
+static const int kLayers[4][3] = {{64, 3, 1}, {128, 4, 2}, {256, 6, 2}, {512, 3, 2}};
+
+int ImageModel::create(const float* blob, size_t n) {
+  BlobReader rd(blob, n);
+  std::vector<f16> w;
+  std::vector<float> pr;
+  auto bn_fold = [&](int c, std::vector<float>& scale) {  // -> bias offset in pr
+    const float* g = rd.take(c);
+    const float* b = rd.take(c);
+    const float* rm = rd.take(c);
+    const float* rv = rd.take(c);
+    scale.resize(c);
+    size_t off = pr.size();
+    for (int i = 0; i < c; ++i) {
+      const double s = (double)g[i] / std::sqrt((double)rv[i] + 1e-5);
+      scale[i] = (float)s;
+      pr.push_back((float)((double)b[i] - (double)rm[i] * s));
+    }
+    return off;
+  };
+  auto conv = [&](int cout, int cin, int ks, int stride, int pad) {
+    ConvLayer L;
+    L.cin = cin; L.cout = cout; L.ks = ks; L.stride = stride; L.pad = pad;
+    const float* src = rd.take((size_t)cout * cin * ks * ks);
+    std::vector<float> scale;
+    L.b_off = bn_fold(cout, scale);
+    L.w_off = w.size();
+    w.resize(w.size() + (size_t)cout * cin * ks * ks);
+    if (!rd.ok) return L;
+    for (int o = 0; o < cout; ++o)
+      for (int kh = 0; kh < ks; ++kh)
+        for (int kw = 0; kw < ks; ++kw)
+          for (int c = 0; c < cin; ++c)
+            w[L.w_off + (((size_t)o * ks + kh) * ks + kw) * cin + c] =
+                (f16)((double)src[(((size_t)o * cin + c) * ks + kh) * ks + kw] * scale[o]);
+    return L;
+  };
+  // stem: fold RGB replication + ToTensor(/255) + Normalize + BN scale into K=128 rows
+  {
+    const float* src = rd.take((size_t)64 * 3 * 49);
+    std::vector<float> scale;
+    stem.b_off = bn_fold(64, scale);
+    stem.w_off = w.size();
+    stem.cin = 1; stem.cout = 64; stem.ks = 7; stem.stride = 2; stem.pad = 3;
+    const double mean[3] = {0.485, 0.456, 0.406}, stdv[3] = {0.229, 0.224, 0.225};
+    w.resize(w.size() + 64 * 128, (f16)0.f);
+    if (rd.ok) {
+      for (int o = 0; o < 64; ++o)
+        for (int t = 0; t < 49; ++t) {
+          double a = 0.0, c0 = 0.0;
+          for (int c = 0; c < 3; ++c) {
+            const double wv = src[((size_t)o * 3 + c) * 49 + t];
+            const double mf = (double)(float)mean[c], sf = (double)(float)stdv[c];
+            a += wv / (255.0 * sf);
+            c0 -= wv * mf / sf;
+          }
+          w[stem.w_off + (size_t)o * 128 + t] = (f16)(a * scale[o]);
+          w[stem.w_off + (size_t)o * 128 + 64 + t] = (f16)(c0 * scale[o]);
+        }
+    }
+  }
+  blocks.clear();
+  int cin = 64;
+  for (int li = 0; li < 4; ++li) {
+    const int wd = kLayers[li][0], nb = kLayers[li][1], st = kLayers[li][2];
+    for (int b = 0; b < nb; ++b) {
+      Bottleneck bk;
+      const int s = b == 0 ? st : 1;
+      bk.c1 = conv(wd, cin, 1, 1, 0);
+      bk.c2 = conv(wd, wd, 3, s, 1);
+      bk.c3 = conv(4 * wd, wd, 1, 1, 0);
+      if (b == 0) {
+        bk.has_ds = true;
+        bk.ds = conv(4 * wd, cin, 1, s, 0);
+      }
+      blocks.push_back(bk);
+      cin = 4 * wd;
+    }
+  }
+  const float* f1w = rd.take((size_t)512 * 2048);
+  const float* f1b = rd.take(512);
+  const float* f2w = rd.take((size_t)7 * 512);
+  const float* f2b = rd.take(7);
+  MEC_REQUIRE(rd.ok && rd.off == n, "image blob size mismatch");
+  fc1_off = pr.size();
+  pr.resize(pr.size() + (size_t)2048 * 512);
+  for (int i = 0; i < 2048; ++i)
+    for (int j = 0; j < 512; ++j) pr[fc1_off + (size_t)i * 512 + j] = f1w[(size_t)j * 2048 + i];
+  fc1b_off = pr.size();
+  pr.insert(pr.end(), f1b, f1b + 512);
+  fc2_off = pr.size();
+  pr.resize(pr.size() + 512 * 7);
+  for (int i = 0; i < 512; ++i)
+    for (int j = 0; j < 7; ++j) pr[fc2_off + (size_t)i * 7 + j] = f2w[(size_t)j * 512 + i];
+  fc2b_off = pr.size();
+  pr.insert(pr.end(), f2b, f2b + 7);
+  MEC_TRY(upload(wts, w.data(), w.size() * sizeof(f16)));
+  MEC_TRY(upload(prm, pr.data(), pr.size() * sizeof(float)));
+  return ensure_taps();
+}
+
+int ImageModel::forward(const uint8_t* gray, int B, float* feat, float* logits, float* probs, hipStream_t s) {
+  MEC_REQUIRE(B >= 0, "image: B < 0");
+  if (B == 0) return 0;
+  MEC_REQUIRE(gray && feat && logits && probs, "image: null pointer");
+  const size_t per_img_big = (size_t)56 * 56 * 256;  // largest NHWC activation (elements)
+  const size_t per_t1 = (size_t)56 * 56 * 128, per_t2 = (size_t)56 * 56 * 64;
+  const size_t per_img = 224 * 224 + (3 * per_img_big + per_t1 + per_t2) * sizeof(f16) + 256;
+  if (B > ws_batch) {
+    MEC_TRY(ws.ensure(per_img * (size_t)B + 4096));
+    ws_batch = B;
+  }
+  char* p = ws.as<char>();
+  uint8_t* resized = reinterpret_cast<uint8_t*>(p);
+  p += ((size_t)B * 224 * 224 + 255) / 256 * 256;
+  f16* X = reinterpret_cast<f16*>(p); p += (size_t)B * per_img_big * sizeof(f16);
+  f16* Y = reinterpret_cast<f16*>(p); p += (size_t)B * per_img_big * sizeof(f16);
+  f16* DS = reinterpret_cast<f16*>(p); p += (size_t)B * per_img_big * sizeof(f16);
+  f16* T1 = reinterpret_cast<f16*>(p); p += (size_t)B * per_t1 * sizeof(f16);
+  f16* T2 = reinterpret_cast<f16*>(p);
+
+  const f16* Wt = wts.as<f16>();
+  const float* P = prm.as<float>();
+  MEC_TRY(resize_u8(gray, B, 48, 48, resized, 224, 224, s));
+  {  // stem conv 7x7/2 + BN + ReLU -> Y [B,112,112,64]
+    GemmParams g;
+    g.amode = A_STEM; g.A = resized; g.B = Wt + stem.w_off; g.bias = P + stem.b_off; g.act = ACT_RELU;
+    g.C16 = Y; g.M = B * 112 * 112; g.N = 64; g.K = 128;
+    g.H = 224; g.W = 224; g.C = 1; g.OH = 112; g.OW = 112; g.ks = 7; g.stride = 2; g.pad = 3;
+    MEC_TRY(launch_gemm(g, s, &prof, TAG_RESNET_STEM));
+  }
+  {  // maxpool -> X [B,56,56,64]
+    const size_t total = (size_t)B * 56 * 56 * 8;
+    hipLaunchKernelGGL(maxpool3s2_kernel, dim3((unsigned)((total + 255) / 256)), dim3(256), 0, s, Y, X, B, 112, 112,
+                       64, 56, 56);
+    MEC_LAUNCH_CHECK();
+  }
+  f16* cur = X;
+  f16* other = Y;
+  int H = 56;
+  for (const Bottleneck& bk : blocks) {
+    const int wd = bk.c1.cout, cin = bk.c1.cin, st = bk.c2.stride;
+    const int OH = (H + 2 - 3) / st + 1;
+    GemmParams g;
+    g.A = cur; g.B = Wt + bk.c1.w_off; g.bias = P + bk.c1.b_off; g.act = ACT_RELU; g.C16 = T1;
+    g.M = B * H * H; g.N = wd; g.K = cin;
+    MEC_TRY(launch_gemm(g, s, &prof, TAG_RESNET_CONV1X1));
+    g = GemmParams();
+    g.amode = A_CONV; g.A = T1; g.B = Wt + bk.c2.w_off; g.bias = P + bk.c2.b_off; g.act = ACT_RELU; g.C16 = T2;
+    g.M = B * OH * OH; g.N = wd; g.K = 9 * wd;
+    g.H = H; g.W = H; g.C = wd; g.OH = OH; g.OW = OH; g.ks = 3; g.stride = st; g.pad = 1;
+    MEC_TRY(launch_gemm(g, s, &prof, TAG_RESNET_CONV3X3));
+    const f16* res = cur;
+    if (bk.has_ds) {
+      g = GemmParams();
+      g.B = Wt + bk.ds.w_off; g.bias = P + bk.ds.b_off; g.C16 = DS; g.A = cur;
+      g.M = B * OH * OH; g.N = 4 * wd; g.K = cin;
+      if (st != 1) {
+        g.amode = A_CONV; g.H = H; g.W = H; g.C = cin; g.OH = OH; g.OW = OH; g.ks = 1; g.stride = st; g.pad = 0;
+      }
+      MEC_TRY(launch_gemm(g, s, &prof, TAG_RESNET_CONV1X1));
+      res = DS;
+    }
+    g = GemmParams();
+    g.A = T2; g.B = Wt + bk.c3.w_off; g.bias = P + bk.c3.b_off; g.R = res; g.act = ACT_RELU; g.C16 = other;
+    g.M = B * OH * OH; g.N = 4 * wd; g.K = wd;
+    MEC_TRY(launch_gemm(g, s, &prof, TAG_RESNET_CONV1X1));
+    std::swap(cur, other);
+    H = OH;
+  }
+  hipLaunchKernelGGL(resnet_head_kernel, dim3((B + IHEAD_R - 1) / IHEAD_R), dim3(256), 0, s, cur, B, H * H,
+                     P + fc1_off, P + fc1b_off, P + fc2_off, P + fc2b_off, feat, logits, probs);
+  MEC_LAUNCH_CHECK();
+  return 0;
+}
+
+}  // namespace mec

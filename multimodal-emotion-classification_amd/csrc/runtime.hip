@@ -1,0 +1,66 @@
+// Runtime plumbing: thread-local error string, device buffers, hipEvent timing hook.
+#include "mec_common.h"
+
+namespace mec {
+
+static thread_local std::string g_last_error;
+
+void set_error(const std::string& msg) { g_last_error = msg; }
+const char* last_error() { return g_last_error.c_str(); }
+
+int DevBuf::ensure(size_t n) {
+  if (n <= bytes) return 0;
+  release();
+  MEC_HIP(hipMalloc(&p, n));
+  bytes = n;
+  return 0;
+}
+
+void DevBuf::release() {
+  if (p) (void)hipFree(p);
+  p = nullptr;
+  bytes = 0;
+}
+
+int upload(DevBuf& b, const void* host, size_t bytes) {
+  MEC_TRY(b.ensure(bytes));
+  MEC_HIP(hipMemcpy(b.p, host, bytes, hipMemcpyHostToDevice));
+  return 0;
+}
+
+int Prof::begin(int t, hipStream_t s) {
+  if (t != tag || tag == TAG_NONE) return 0;
+  while (ev.size() < used + 2) {
+    hipEvent_t e;
+    MEC_HIP(hipEventCreate(&e));
+    ev.push_back(e);
+  }
+  MEC_HIP(hipEventRecord(ev[used], s));
+  return 0;
+}
+
+int Prof::end(int t, hipStream_t s) {
+  if (t != tag || tag == TAG_NONE) return 0;
+  MEC_HIP(hipEventRecord(ev[used + 1], s));
+  used += 2;
+  return 0;
+}
+
+int Prof::read(double* total_ms, int* count) {
+  double tot = 0.0;
+  for (size_t i = 0; i + 1 < used; i += 2) {
+    MEC_HIP(hipEventSynchronize(ev[i + 1]));
+    float ms = 0.f;
+    MEC_HIP(hipEventElapsedTime(&ms, ev[i], ev[i + 1]));
+    tot += ms;
+  }
+  *total_ms = tot;
+  *count = (int)(used / 2);
+  return 0;
+}
+
+Prof::~Prof() {
+  for (auto e : ev) (void)hipEventDestroy(e);
+}
+
+}  // namespace mec

@@ -1,0 +1,370 @@
+// Speech DNN and fusion step: one fused launch each, R samples per workgroup, all
+// activations in LDS, fp32 arithmetic (the reference computes both in fp32).
+//
+// speech_kernel   restates inference/speech_inference.py:66-69, :93-103 over the Keras
+//                 Sequential of model_training/train_speech_model.py:55-90:
+//                 StandardScaler -> 5 x [Dense, BN(eps 1e-3), ReLU] -> Dense7 -> softmax,
+//                 emitting the block-5 ReLU (layers[-3]) 64-d feature too.
+// fusion_kernel   restates MultiModalFusionModel.forward (inference/multimodal_fusion.py:
+//                 156-180) + the softmax of fuse_with_attention (:221).
+// fuse_weighted   restates fuse_predictions (:184-199) in float64 like numpy.
+#include "block_ops.h"
+#include "models.h"
+
+namespace mec {
+
+// =============================================================== speech
+struct SpeechW {
+  const float *mean, *scale;
+  const float* W[6];
+  const float* b[6];
+  const float* inv[5];
+  const float* shift[5];
+};
+
+constexpr int SPEECH_R = 8;
+__constant__ int kSpeechDims[6] = {56, 512, 512, 256, 128, 64};
+
+__global__ __launch_bounds__(256) void speech_kernel(SpeechW w, const float* __restrict__ x, int B,
+                                                     float* feat, float* logits, float* probs) {
+  constexpr int R = SPEECH_R, LD = 512;
+  __shared__ float bufA[R * LD], bufB[R * LD], red[R * 256];
+  const int tid = threadIdx.x;
+  const int r0 = blockIdx.x * R;
+  const int nr = min(R, B - r0);
+  for (int idx = tid; idx < R * 56; idx += blockDim.x) {
+    const int r = idx / 56, k = idx - r * 56;
+    // sklearn StandardScaler.transform: (X - mean_) / scale_
+    bufA[r * LD + k] = r < nr ? (x[(size_t)(r0 + r) * 56 + k] - w.mean[k]) / w.scale[k] : 0.f;
+  }
+  __syncthreads();
+  float* in = bufA;
+  float* out = bufB;
+  for (int l = 0; l < 5; ++l) {
+    const int K = kSpeechDims[l], N = kSpeechDims[l + 1];
+    block_linear<R>(in, LD, K, w.W[l], w.b[l], N, out, LD, red);
+    for (int idx = tid; idx < R * N; idx += blockDim.x) {
+      const int r = idx / N, n = idx - r * N;
+      // tf.nn.batch_normalization: x * inv + (beta - mean * inv), inv = rsqrt(var+eps)*gamma
+      const float v = out[r * LD + n] * w.inv[l][n] + w.shift[l][n];
+      out[r * LD + n] = fmaxf(v, 0.f);
+    }
+    __syncthreads();
+    float* t = in; in = out; out = t;
+  }
+  for (int idx = tid; idx < nr * 64; idx += blockDim.x) {
+    const int r = idx / 64, n = idx - r * 64;
+    feat[(size_t)(r0 + r) * 64 + n] = in[r * LD + n];
+  }
+  block_linear<R>(in, LD, 64, w.W[5], w.b[5], 7, out, LD, red);
+  for (int idx = tid; idx < nr * 7; idx += blockDim.x) {
+    const int r = idx / 7, n = idx - r * 7;
+    logits[(size_t)(r0 + r) * 7 + n] = out[r * LD + n];
+  }
+  __syncthreads();
+  block_softmax_small<R>(out, LD, 7, nullptr, 0);
+  for (int idx = tid; idx < nr * 7; idx += blockDim.x) {
+    const int r = idx / 7, n = idx - r * 7;
+    probs[(size_t)(r0 + r) * 7 + n] = out[r * LD + n];
+  }
+}
+
+int SpeechModel::create(const float* blob, size_t n) {
+  BlobReader rd(blob, n);
+  const int dims[6] = {56, 512, 512, 256, 128, 64};
+  std::vector<float> h;
+  auto put = [&](const float* src, size_t cnt) {
+    size_t o = h.size();
+    h.insert(h.end(), src, src + cnt);
+    return o;
+  };
+  off_mean = put(rd.take(56), 56);
+  off_scale = put(rd.take(56), 56);
+  for (int l = 0; l < 5; ++l) {
+    const int K = dims[l], N = dims[l + 1];
+    off_W[l] = put(rd.take((size_t)K * N), (size_t)K * N);  // Keras kernel is [in,out] already
+    off_b[l] = put(rd.take(N), N);
+    const float* g = rd.take(N);
+    const float* be = rd.take(N);
+    const float* mm = rd.take(N);
+    const float* mv = rd.take(N);
+    std::vector<float> inv(N), sh(N);
+    for (int i = 0; i < N; ++i) {
+      inv[i] = (1.0f / sqrtf(mv[i] + 1e-3f)) * g[i];
+      sh[i] = be[i] - mm[i] * inv[i];
+    }
+    off_inv[l] = put(inv.data(), N);
+    off_shift[l] = put(sh.data(), N);
+  }
+  off_W[5] = put(rd.take(64 * 7), 64 * 7);
+  off_b[5] = put(rd.take(7), 7);
+  MEC_REQUIRE(rd.ok && rd.off == n, "speech blob size mismatch");
+  return upload(w, h.data(), h.size() * sizeof(float));
+}
+
+int SpeechModel::forward(const float* x, int B, float* feat, float* logits, float* probs, hipStream_t s) {
+  MEC_REQUIRE(B >= 0, "speech: B < 0");
+  if (B == 0) return 0;
+  MEC_REQUIRE(x && feat && logits && probs, "speech: null pointer");
+  const float* base = w.as<float>();
+  SpeechW p;
+  p.mean = base + off_mean;
+  p.scale = base + off_scale;
+  for (int l = 0; l < 6; ++l) { p.W[l] = base + off_W[l]; p.b[l] = base + off_b[l]; }
+  for (int l = 0; l < 5; ++l) { p.inv[l] = base + off_inv[l]; p.shift[l] = base + off_shift[l]; }
+  MEC_TRY(prof.begin(TAG_SPEECH, s));
+  hipLaunchKernelGGL(speech_kernel, dim3((B + SPEECH_R - 1) / SPEECH_R), dim3(256), 0, s, p, x, B, feat,
+                     logits, probs);
+  MEC_LAUNCH_CHECK();
+  MEC_TRY(prof.end(TAG_SPEECH, s));
+  return 0;
+}
+
+// =============================================================== fusion
+// Pointer table layout (see FusionModel::create):
+//   [4m + {0 W,1 b,2 ln_g,3 ln_b}]        modality projections, m = speech/text/image
+//   [12 + 10m + {WqT,bq,WkT,bk,WvT,bv,WoT,bo,ln_g,ln_b}]   cross_attn_{m}
+//   [42 + 4j + {W,b,ln_g,ln_b}]          attention_fusion.projections.j
+//   54..69 att0 W,b | att2 W,b | dec0 W,b | dec2 W,b | cls0 W,b | cls1 g,b | cls4 W,b | cls7 W,b
+constexpr int FUSION_NP = 70;
+struct FusionW { const float* p[FUSION_NP]; };
+
+constexpr int FUSION_R = 4;
+constexpr int F_LDIN = 1368, F_LDP = 768, F_LDT = 1280;
+
+__device__ void cross_attention_rows(float* T, int ldt, int nr) {
+  // T[r][0:256]=q, [256]=k0, [512]=k1, [768]=v0, [1024]=v1; writes o into T[r][0:256].
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+  for (int r = wave; r < FUSION_R; r += (blockDim.x >> 6)) {
+    float* t = T + r * ldt;
+    float q[4], s0 = 0.f, s1 = 0.f;
+#pragma unroll
+    for (int c = 0; c < 4; ++c) q[c] = t[4 * lane + c] * 0.125f;  // q * sqrt(1/head_dim)
+#pragma unroll
+    for (int c = 0; c < 4; ++c) {
+      s0 = fmaf(q[c], t[256 + 4 * lane + c], s0);
+      s1 = fmaf(q[c], t[512 + 4 * lane + c], s1);
+    }
+#pragma unroll
+    for (int o = 8; o > 0; o >>= 1) {  // reduce within the 16 lanes of one head
+      s0 += __shfl_xor(s0, o, 64);
+      s1 += __shfl_xor(s1, o, 64);
+    }
+    const float m = fmaxf(s0, s1);
+    const float e0 = expf(s0 - m), e1 = expf(s1 - m);
+    const float den = e0 + e1;
+    const float a0 = e0 / den, a1 = e1 / den;
+#pragma unroll
+    for (int c = 0; c < 4; ++c) t[4 * lane + c] = a0 * t[768 + 4 * lane + c] + a1 * t[1024 + 4 * lane + c];
+  }
+  __syncthreads();
+}
+
+__global__ __launch_bounds__(256) void fusion_kernel(FusionW w, const float* __restrict__ sf,
+                                                     const float* __restrict__ tf, const float* __restrict__ imf,
+                                                     const float* __restrict__ sp, const float* __restrict__ tp,
+                                                     const float* __restrict__ ip, int B, float* logits,
+                                                     float* probs, float* attn_w, float* dec_w) {
+  constexpr int R = FUSION_R;
+  __shared__ float IN[R * F_LDIN], P[R * F_LDP], E[R * F_LDP], T[R * F_LDT], red[R * 256];
+  const int tid = threadIdx.x, T_ = blockDim.x;
+  const int r0 = blockIdx.x * R;
+  const int nr = min(R, B - r0);
+  for (int idx = tid; idx < R * F_LDIN; idx += T_) {
+    const int r = idx / F_LDIN, k = idx - r * F_LDIN;
+    const size_t b = (size_t)(r0 + r);
+    float v = 0.f;
+    if (r < nr) {
+      if (k < 64) v = sf[b * 64 + k];
+      else if (k < 832) v = tf[b * 768 + (k - 64)];
+      else if (k < 1344) v = imf[b * 512 + (k - 832)];
+      else if (k < 1351) v = sp[b * 7 + (k - 1344)];
+      else if (k < 1358) v = tp[b * 7 + (k - 1351)];
+      else if (k < 1365) v = ip[b * 7 + (k - 1358)];
+    }
+    IN[idx] = v;
+  }
+  __syncthreads();
+  const int in_off[3] = {0, 64, 832}, in_dim[3] = {64, 768, 512};
+  // modality projections: ReLU(LN(Linear)) (multimodal_fusion.py:113-130, :157-159)
+  for (int m = 0; m < 3; ++m) {
+    block_linear<R>(IN + in_off[m], F_LDIN, in_dim[m], w.p[4 * m], w.p[4 * m + 1], 256, P + 256 * m, F_LDP, red);
+    block_layernorm<R>(P + 256 * m, F_LDP, 256, w.p[4 * m + 2], w.p[4 * m + 3], 1e-5f, true);
+  }
+  // cross-modal attention (:161-167): query m attends to the other two (in order)
+  const int others[3][2] = {{1, 2}, {0, 2}, {0, 1}};
+  for (int m = 0; m < 3; ++m) {
+    const float* const* c = w.p + 12 + 10 * m;
+    block_linear<R>(P + 256 * m, F_LDP, 256, c[0], c[1], 256, T + 0, F_LDT, red);
+    block_linear<R>(P + 256 * others[m][0], F_LDP, 256, c[2], c[3], 256, T + 256, F_LDT, red);
+    block_linear<R>(P + 256 * others[m][1], F_LDP, 256, c[2], c[3], 256, T + 512, F_LDT, red);
+    block_linear<R>(P + 256 * others[m][0], F_LDP, 256, c[4], c[5], 256, T + 768, F_LDT, red);
+    block_linear<R>(P + 256 * others[m][1], F_LDP, 256, c[4], c[5], 256, T + 1024, F_LDT, red);
+    cross_attention_rows(T, F_LDT, nr);
+    block_linear<R>(T, F_LDT, 256, c[6], c[7], 256, E + 256 * m, F_LDP, red);
+    for (int idx = tid; idx < R * 256; idx += T_) {
+      const int r = idx >> 8, n = idx & 255;
+      E[r * F_LDP + 256 * m + n] = P[r * F_LDP + 256 * m + n] + E[r * F_LDP + 256 * m + n];
+    }
+    __syncthreads();
+    block_layernorm<R>(E + 256 * m, F_LDP, 256, c[8], c[9], 1e-5f, false);
+  }
+  // AttentionFusion (:79-106): per-modality projection, attention over the 768 concat
+  for (int j = 0; j < 3; ++j) {
+    block_linear<R>(E + 256 * j, F_LDP, 256, w.p[42 + 4 * j], w.p[43 + 4 * j], 256, T + 256 * j, F_LDT, red);
+    block_layernorm<R>(T + 256 * j, F_LDT, 256, w.p[44 + 4 * j], w.p[45 + 4 * j], 1e-5f, true);
+  }
+  block_linear<R>(T, F_LDT, 768, w.p[54], w.p[55], 256, T + 768, F_LDT, red);
+  for (int idx = tid; idx < R * 256; idx += T_) {
+    const int r = idx >> 8, n = idx & 255;
+    T[r * F_LDT + 768 + n] = tanhf(T[r * F_LDT + 768 + n]);
+  }
+  __syncthreads();
+  block_linear<R>(T + 768, F_LDT, 256, w.p[56], w.p[57], 3, P, F_LDP, red);
+  block_softmax_small<R>(P, F_LDP, 3, nullptr, 0);
+  for (int idx = tid; idx < R * 256; idx += T_) {  // fused = sum_j w_j * proj_j
+    const int r = idx >> 8, n = idx & 255;
+    const float* a = P + r * F_LDP;
+    const float* t = T + r * F_LDT;
+    E[r * F_LDP + n] = a[0] * t[n] + a[1] * t[256 + n] + a[2] * t[512 + n];
+  }
+  for (int idx = tid; idx < nr * 3; idx += T_) {
+    const int r = idx / 3, j = idx - r * 3;
+    attn_w[(size_t)(r0 + r) * 3 + j] = P[r * F_LDP + j];
+  }
+  __syncthreads();
+  // decision weights over the 21-d concat of softmax outputs (:138-143, :171-175)
+  block_linear<R>(IN + 1344, F_LDIN, 21, w.p[58], w.p[59], 64, P + 256, F_LDP, red);
+  for (int idx = tid; idx < R * 64; idx += T_) {
+    const int r = idx >> 6, n = idx & 63;
+    P[r * F_LDP + 256 + n] = fmaxf(P[r * F_LDP + 256 + n], 0.f);
+  }
+  __syncthreads();
+  block_linear<R>(P + 256, F_LDP, 64, w.p[60], w.p[61], 3, P + 384, F_LDP, red);
+  block_softmax_small<R>(P + 384, F_LDP, 3, nullptr, 0);
+  for (int idx = tid; idx < R * 7; idx += T_) {
+    const int r = idx / 7, c = idx - r * 7;
+    const float* d = P + r * F_LDP + 384;
+    const float* pr = IN + r * F_LDIN + 1344;
+    E[r * F_LDP + 256 + c] = pr[c] * d[0] + pr[7 + c] * d[1] + pr[14 + c] * d[2];
+  }
+  for (int idx = tid; idx < nr * 3; idx += T_) {
+    const int r = idx / 3, j = idx - r * 3;
+    dec_w[(size_t)(r0 + r) * 3 + j] = P[r * F_LDP + 384 + j];
+  }
+  __syncthreads();
+  // classifier on [fused, weighted_preds] (:145-154, :177-178)
+  block_linear<R>(E, F_LDP, 263, w.p[62], w.p[63], 256, T, F_LDT, red);
+  block_layernorm<R>(T, F_LDT, 256, w.p[64], w.p[65], 1e-5f, true);
+  block_linear<R>(T, F_LDT, 256, w.p[66], w.p[67], 128, T + 256, F_LDT, red);
+  for (int idx = tid; idx < R * 128; idx += T_) {
+    const int r = idx >> 7, n = idx & 127;
+    T[r * F_LDT + 256 + n] = fmaxf(T[r * F_LDT + 256 + n], 0.f);
+  }
+  __syncthreads();
+  block_linear<R>(T + 256, F_LDT, 128, w.p[68], w.p[69], 7, T + 384, F_LDT, red);
+  for (int idx = tid; idx < nr * 7; idx += T_) {
+    const int r = idx / 7, c = idx - r * 7;
+    logits[(size_t)(r0 + r) * 7 + c] = T[r * F_LDT + 384 + c];
+  }
+  __syncthreads();
+  block_softmax_small<R>(T + 384, F_LDT, 7, nullptr, 0);
+  for (int idx = tid; idx < nr * 7; idx += T_) {
+    const int r = idx / 7, c = idx - r * 7;
+    probs[(size_t)(r0 + r) * 7 + c] = T[r * F_LDT + 384 + c];
+  }
+}
+
+int FusionModel::create(const float* blob, size_t n) {
+  BlobReader rd(blob, n);
+  std::vector<float> h;
+  off.assign(FUSION_NP, 0);
+  auto put = [&](const float* src, size_t cnt) {
+    size_t o = h.size();
+    h.insert(h.end(), src, src + cnt);
+    return o;
+  };
+  auto putT = [&](const float* src, int out, int in) {  // torch [out,in] -> [in][out]
+    size_t o = h.size();
+    h.resize(o + (size_t)out * in);
+    for (int i = 0; i < in; ++i)
+      for (int j = 0; j < out; ++j) h[o + (size_t)i * out + j] = src[(size_t)j * in + i];
+    return o;
+  };
+  auto lin = [&](int idx, int out, int in) {
+    off[idx] = putT(rd.take((size_t)out * in), out, in);
+    off[idx + 1] = put(rd.take(out), out);
+  };
+  auto ln = [&](int idx, int c) {
+    off[idx] = put(rd.take(c), c);
+    off[idx + 1] = put(rd.take(c), c);
+  };
+  const int dims[3] = {64, 768, 512};
+  for (int m = 0; m < 3; ++m) { lin(4 * m, 256, dims[m]); ln(4 * m + 2, 256); }
+  for (int m = 0; m < 3; ++m) {
+    const int b = 12 + 10 * m;
+    const float* ipw = rd.take(768 * 256);
+    const float* ipb = rd.take(768);
+    for (int q = 0; q < 3; ++q) {
+      off[b + 2 * q] = putT(ipw + (size_t)q * 256 * 256, 256, 256);
+      off[b + 2 * q + 1] = put(ipb + q * 256, 256);
+    }
+    lin(b + 6, 256, 256);
+    ln(b + 8, 256);
+  }
+  for (int j = 0; j < 3; ++j) { lin(42 + 4 * j, 256, 256); ln(44 + 4 * j, 256); }
+  lin(54, 256, 768);
+  lin(56, 3, 256);
+  lin(58, 64, 21);
+  lin(60, 3, 64);
+  lin(62, 256, 263);
+  ln(64, 256);
+  lin(66, 128, 256);
+  lin(68, 7, 128);
+  MEC_REQUIRE(rd.ok && rd.off == n, "fusion blob size mismatch");
+  return upload(w, h.data(), h.size() * sizeof(float));
+}
+
+int FusionModel::forward(const float* sf, const float* tf, const float* imf, const float* sp,
+                         const float* tp, const float* ip, int B, float* logits, float* probs,
+                         float* attn_w, float* dec_w, hipStream_t s) {
+  MEC_REQUIRE(B >= 0, "fusion: B < 0");
+  if (B == 0) return 0;
+  MEC_REQUIRE(sf && tf && imf && sp && tp && ip && logits && probs && attn_w && dec_w,
+              "fusion: null pointer (the attention model needs all three modalities)");
+  FusionW p;
+  const float* base = w.as<float>();
+  for (int i = 0; i < FUSION_NP; ++i) p.p[i] = base + off[i];
+  MEC_TRY(prof.begin(TAG_FUSION, s));
+  hipLaunchKernelGGL(fusion_kernel, dim3((B + FUSION_R - 1) / FUSION_R), dim3(256), 0, s, p, sf, tf, imf, sp,
+                     tp, ip, B, logits, probs, attn_w, dec_w);
+  MEC_LAUNCH_CHECK();
+  MEC_TRY(prof.end(TAG_FUSION, s));
+  return 0;
+}
+
+// =============================================================== weighted average
+__global__ void fuse_weighted_kernel(const float* s, const float* t, const float* i, int B, double* out) {
+  const int b = blockIdx.x * blockDim.x + threadIdx.x;
+  if (b >= B) return;
+  double w[7];
+  for (int c = 0; c < 7; ++c) {
+    const double vs = s ? (double)s[b * 7 + c] : 0.0;
+    const double vt = t ? (double)t[b * 7 + c] : 0.0;
+    const double vi = i ? (double)i[b * 7 + c] : 0.0;
+    w[c] = 0.3 * vs + 0.35 * vt + 0.35 * vi;
+  }
+  double sum = 0.0;
+  for (int c = 0; c < 7; ++c) sum += w[c];
+  for (int c = 0; c < 7; ++c) out[b * 7 + c] = sum > 0.0 ? w[c] / sum : w[c];
+}
+
+int fuse_weighted(const float* s, const float* t, const float* i, int B, double* out, hipStream_t st) {
+  MEC_REQUIRE(B >= 0 && (B == 0 || out), "fuse_weighted: bad args");
+  if (B == 0) return 0;
+  hipLaunchKernelGGL(fuse_weighted_kernel, dim3((B + 255) / 256), dim3(256), 0, st, s, t, i, B, out);
+  MEC_LAUNCH_CHECK();
+  return 0;
+}
+
+}  // namespace mec

@@ -1,0 +1,72 @@
+"""ctypes binding of libmec_hip.so (the C ABI declared in include/mec.h).
+
+The library is built in-tree by __graft_entry__.build() (csrc/Makefile). There is no
+fallback: if the library or a GPU is missing, load() raises MecError.
+"""
+import ctypes
+import os
+import threading
+
+_HERE = os.path.dirname(os.path.abspath(__file__))
+LIB_PATH = os.path.join(_HERE, 'libmec_hip.so')
+
+c_vp = ctypes.c_void_p
+c_int = ctypes.c_int
+c_fp = ctypes.POINTER(ctypes.c_float)
+c_dp = ctypes.POINTER(ctypes.c_double)
+
+# name -> (restype, argtypes); mirrors include/mec.h one to one.
+SIGNATURES = {
+    'mec_version': (ctypes.c_char_p, []),
+    'mec_last_error': (ctypes.c_char_p, []),
+    'mec_blob_size': (ctypes.c_longlong, [c_int]),
+    'mec_create': (c_int, [c_int, c_fp, ctypes.c_size_t, c_int, ctypes.POINTER(c_vp)]),
+    'mec_destroy': (c_int, [c_vp]),
+    'mec_speech_fwd': (c_int, [c_vp, c_vp, c_int, c_vp, c_vp, c_vp, c_vp]),
+    'mec_text_fwd': (c_int, [c_vp, c_vp, c_vp, c_int, c_int, c_vp, c_vp, c_vp, c_vp]),
+    'mec_image_fwd': (c_int, [c_vp, c_vp, c_int, c_vp, c_vp, c_vp, c_vp]),
+    'mec_fusion_fwd': (c_int, [c_vp, c_vp, c_vp, c_vp, c_vp, c_vp, c_vp, c_int, c_vp, c_vp, c_vp, c_vp, c_vp]),
+    'mec_fuse_weighted': (c_int, [c_vp, c_vp, c_vp, c_int, c_vp, c_vp]),
+    'mec_resize_u8': (c_int, [c_vp, c_int, c_int, c_int, c_vp, c_int, c_int, c_vp]),
+    'mec_gemm_f16': (c_int, [c_vp, c_vp, c_vp, c_vp, c_int, c_vp, c_vp, c_int, c_int, c_int, c_int, c_vp]),
+    'mec_conv_f16': (c_int, [c_vp, c_vp, c_vp, c_vp, c_vp, c_int, c_int, c_int, c_int, c_int, c_int, c_int,
+                             c_int, c_int, c_vp]),
+    'mec_prof_enable': (c_int, [c_vp, c_int]),
+    'mec_prof_read': (c_int, [c_vp, c_dp, ctypes.POINTER(c_int)]),
+}
+
+# Kernel tags for mec_prof_enable (csrc/mec_common.h KernelTag).
+TAGS = {'bert_qkv': 1, 'bert_attn': 2, 'bert_oproj': 3, 'bert_ffn1': 4, 'bert_ffn2': 5, 'bert_ln': 6,
+        'resnet_conv3x3': 7, 'resnet_conv1x1': 8, 'resnet_stem': 9, 'speech': 10, 'fusion': 11}
+
+
+class MecError(RuntimeError):
+    pass
+
+
+_lib = None
+_lock = threading.Lock()
+
+
+def load(path: str = LIB_PATH):
+    """Load and declare the library (no GPU needed to load it)."""
+    global _lib
+    with _lock:
+        if _lib is not None and path == LIB_PATH:
+            return _lib
+        if not os.path.exists(path):
+            raise MecError(f'{path} is missing: build it with `python -c "import __graft_entry__ as g; g.build()"`')
+        lib = ctypes.CDLL(path)
+        for name, (res, args) in SIGNATURES.items():
+            fn = getattr(lib, name)
+            fn.restype = res
+            fn.argtypes = args
+        if path == LIB_PATH:
+            _lib = lib
+        return lib
+
+
+def check(rc: int, what: str):
+    if rc != 0:
+        err = load().mec_last_error()
+        raise MecError(f'{what} failed: {err.decode() if err else "unknown error"}')

@@ -1,0 +1,213 @@
+"""Batched tensor API over the C ABI: device-resident inputs in, device tensors out.
+
+Torch owns device memory and the stream (plumbing); all arithmetic runs in the HIP
+kernels of libmec_hip.so. Each call validates shapes/dtypes/devices on the host before
+any launch, and raises MecError when the library or a GPU is unavailable — there is no
+CPU fallback on this path.
+"""
+from __future__ import annotations
+
+import ctypes
+import threading
+
+import numpy as np
+import torch
+
+from . import _lib, synthetic
+from ._lib import MecError
+
+KINDS = synthetic.KIND_IDS
+
+
+def _ptr(t: torch.Tensor | None):
+    return ctypes.c_void_p(t.data_ptr()) if t is not None else ctypes.c_void_p(0)
+
+
+def _stream(device: torch.device):
+    return ctypes.c_void_p(torch.cuda.current_stream(device).cuda_stream)
+
+
+def _check_tensor(name, t, dtype, shape, device):
+    if not isinstance(t, torch.Tensor):
+        raise TypeError(f'{name}: expected a torch.Tensor, got {type(t).__name__}')
+    if t.device != device:
+        raise ValueError(f'{name}: on {t.device}, expected {device}')
+    if t.dtype != dtype:
+        raise TypeError(f'{name}: dtype {t.dtype}, expected {dtype}')
+    if tuple(t.shape) != tuple(shape):
+        raise ValueError(f'{name}: shape {tuple(t.shape)}, expected {tuple(shape)}')
+    if not t.is_contiguous():
+        raise ValueError(f'{name}: must be contiguous')
+
+
+def require_gpu(device=None) -> torch.device:
+    if not torch.cuda.is_available():
+        raise MecError('no ROCm GPU visible: the HIP inference path has no CPU fallback')
+    if device is None:
+        return torch.device('cuda', torch.cuda.current_device())
+    d = torch.device(device)
+    if d.type != 'cuda':
+        raise MecError(f'device {d}: the HIP inference path runs on a ROCm GPU only')
+    return torch.device('cuda', d.index if d.index is not None else torch.cuda.current_device())
+
+
+class HipModel:
+    """Owns one mec_model handle (packed device weights + workspace)."""
+
+    kind: str = ''
+
+    def __init__(self, weights=None, seed: int = 1234, device=None):
+        self.lib = _lib.load()
+        self.device = require_gpu(device)
+        w = weights if weights is not None else synthetic.weights(self.kind, seed)
+        blob = synthetic.pack(self.kind, w)
+        want = self.lib.mec_blob_size(KINDS[self.kind])
+        if blob.size != want:
+            raise MecError(f'{self.kind}: blob has {blob.size} floats, library expects {want}')
+        h = ctypes.c_void_p()
+        torch.cuda.set_device(self.device)
+        _lib.check(self.lib.mec_create(KINDS[self.kind], blob.ctypes.data_as(_lib.c_fp), blob.size,
+                                       self.device.index, ctypes.byref(h)), f'mec_create({self.kind})')
+        self.handle = h
+        self._lock = threading.Lock()
+
+    def close(self):
+        if getattr(self, 'handle', None):
+            self.lib.mec_destroy(self.handle)
+            self.handle = None
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+    # hipEvent timing hook
+    def prof_enable(self, tag: str | int):
+        t = _lib.TAGS[tag] if isinstance(tag, str) else int(tag)
+        _lib.check(self.lib.mec_prof_enable(self.handle, t), 'mec_prof_enable')
+
+    def prof_read(self):
+        ms = ctypes.c_double()
+        n = ctypes.c_int()
+        _lib.check(self.lib.mec_prof_read(self.handle, ctypes.byref(ms), ctypes.byref(n)), 'mec_prof_read')
+        return ms.value, n.value
+
+    def _empty(self, *shape, dtype=torch.float32):
+        return torch.empty(shape, dtype=dtype, device=self.device)
+
+
+class SpeechEncoder(HipModel):
+    kind = 'speech'
+
+    def forward(self, x: torch.Tensor):
+        """x f32 [B,56] raw features -> (feat [B,64], logits [B,7], probs [B,7])."""
+        B = x.shape[0] if x.dim() == 2 else -1
+        _check_tensor('x', x, torch.float32, (B, 56), self.device)
+        feat, logits, probs = self._empty(B, 64), self._empty(B, 7), self._empty(B, 7)
+        with self._lock:
+            _lib.check(self.lib.mec_speech_fwd(self.handle, _ptr(x), B, _ptr(feat), _ptr(logits), _ptr(probs),
+                                               _stream(self.device)), 'mec_speech_fwd')
+        return feat, logits, probs
+
+
+class TextEncoder(HipModel):
+    kind = 'text'
+
+    def forward(self, ids: torch.Tensor, mask: torch.Tensor):
+        """ids/mask int32 [B,128] -> (cls [B,768], logits [B,7], probs [B,7])."""
+        if ids.dim() != 2:
+            raise ValueError('ids: expected [B, L]')
+        B, L = ids.shape
+        if L != 128:
+            raise ValueError('ids: L must be 128 (padding=max_length, Config.MAX_TEXT_LENGTH)')
+        _check_tensor('ids', ids, torch.int32, (B, L), self.device)
+        _check_tensor('mask', mask, torch.int32, (B, L), self.device)
+        cls, logits, probs = self._empty(B, 768), self._empty(B, 7), self._empty(B, 7)
+        with self._lock:
+            _lib.check(self.lib.mec_text_fwd(self.handle, _ptr(ids), _ptr(mask), B, L, _ptr(cls), _ptr(logits),
+                                             _ptr(probs), _stream(self.device)), 'mec_text_fwd')
+        return cls, logits, probs
+
+
+class ImageEncoder(HipModel):
+    kind = 'image'
+
+    def forward(self, gray: torch.Tensor):
+        """gray u8 [B,48,48] -> (feat [B,512], logits [B,7], probs [B,7])."""
+        B = gray.shape[0] if gray.dim() == 3 else -1
+        _check_tensor('gray', gray, torch.uint8, (B, 48, 48), self.device)
+        feat, logits, probs = self._empty(B, 512), self._empty(B, 7), self._empty(B, 7)
+        with self._lock:
+            _lib.check(self.lib.mec_image_fwd(self.handle, _ptr(gray), B, _ptr(feat), _ptr(logits), _ptr(probs),
+                                              _stream(self.device)), 'mec_image_fwd')
+        return feat, logits, probs
+
+
+class FusionHead(HipModel):
+    kind = 'fusion'
+
+    def forward(self, s_feat, t_feat, i_feat, s_pred, t_pred, i_pred):
+        """-> (logits [B,7], probs [B,7], attn_w [B,3], dec_w [B,3])."""
+        B = s_feat.shape[0]
+        for n, t, d in (('s_feat', s_feat, 64), ('t_feat', t_feat, 768), ('i_feat', i_feat, 512),
+                        ('s_pred', s_pred, 7), ('t_pred', t_pred, 7), ('i_pred', i_pred, 7)):
+            _check_tensor(n, t, torch.float32, (B, d), self.device)
+        logits, probs, aw, dw = self._empty(B, 7), self._empty(B, 7), self._empty(B, 3), self._empty(B, 3)
+        with self._lock:
+            _lib.check(self.lib.mec_fusion_fwd(self.handle, _ptr(s_feat), _ptr(t_feat), _ptr(i_feat), _ptr(s_pred),
+                                               _ptr(t_pred), _ptr(i_pred), B, _ptr(logits), _ptr(probs), _ptr(aw),
+                                               _ptr(dw), _stream(self.device)), 'mec_fusion_fwd')
+        return logits, probs, aw, dw
+
+
+def fuse_weighted(s=None, t=None, i=None, device=None) -> torch.Tensor:
+    """Weighted-average fallback on the GPU (float64) -> [B,7] f64; None = missing modality."""
+    present = [x for x in (s, t, i) if x is not None]
+    lib = _lib.load()
+    dev = present[0].device if present else require_gpu(device)
+    B = present[0].shape[0] if present else 1
+    for n, x in (('s', s), ('t', t), ('i', i)):
+        if x is not None:
+            _check_tensor(n, x, torch.float32, (B, 7), dev)
+    out = torch.empty((B, 7), dtype=torch.float64, device=dev)
+    _lib.check(lib.mec_fuse_weighted(_ptr(s), _ptr(t), _ptr(i), B, _ptr(out), _stream(dev)), 'mec_fuse_weighted')
+    return out
+
+
+# Packed per-sample result row gathered across ranks: 3x7 modality probs,
+# 7 fused probs, 3 attention weights, 3 decision weights = 34 floats.
+ROW = 34
+
+
+class FusedPipeline:
+    """The whole tri-modal path: speech + text + image encoders, then the fusion model."""
+
+    def __init__(self, seed: int = 1234, device=None, weights=None):
+        weights = weights or {}
+        self.speech = SpeechEncoder(weights.get('speech'), seed, device)
+        self.text = TextEncoder(weights.get('text'), seed, device)
+        self.image = ImageEncoder(weights.get('image'), seed, device)
+        self.fusion = FusionHead(weights.get('fusion'), seed, device)
+        self.device = self.speech.device
+
+    def forward(self, x_speech, ids, mask, gray):
+        sf, sl, sp = self.speech.forward(x_speech)
+        tf, tl, tp = self.text.forward(ids, mask)
+        imf, il, ip = self.image.forward(gray)
+        fl, fp, aw, dw = self.fusion.forward(sf, tf, imf, sp, tp, ip)
+        return {'speech': (sf, sl, sp), 'text': (tf, tl, tp), 'image': (imf, il, ip),
+                'fusion': (fl, fp, aw, dw)}
+
+    @staticmethod
+    def pack_rows(out) -> torch.Tensor:
+        sp, tp, ip = out['speech'][2], out['text'][2], out['image'][2]
+        _, fp, aw, dw = out['fusion']
+        return torch.cat([sp, tp, ip, fp, aw, dw], dim=1)
+
+    def models(self):
+        return [self.speech, self.text, self.image, self.fusion]
+
+
+def to_device(a: np.ndarray, device) -> torch.Tensor:
+    return torch.from_numpy(np.ascontiguousarray(a)).to(device)

@@ -1,0 +1,98 @@
+"""Kernel-level parity on the GPU, through the C ABI: MFMA GEMM / implicit-GEMM conv vs a
+torch fp32 reference of the same op, PIL-exact resize bit-exact vs the golden fixture."""
+import ctypes
+
+import numpy as np
+import pytest
+import torch
+
+from mec import _lib
+
+pytestmark = pytest.mark.gpu
+
+
+def _p(t):
+    return ctypes.c_void_p(t.data_ptr()) if t is not None else ctypes.c_void_p(0)
+
+
+def _s():
+    return ctypes.c_void_p(torch.cuda.current_stream().cuda_stream)
+
+
+def _rel_err(got, ref):
+    return float((got - ref).abs().max() / ref.abs().max().clamp_min(1e-6))
+
+
+@pytest.mark.parametrize('M,N,K,act', [(256, 128, 64, 0), (300, 192, 128, 1), (1000, 768, 768, 2),
+                                       (77, 64, 3072, 0), (4096, 2304, 768, 0)])
+def test_gemm_f16(dev, M, N, K, act):
+    lib = _lib.load()
+    g = torch.Generator().manual_seed(M * 7 + N)
+    A = (torch.rand(M, K, generator=g) * 2 - 1).half().to(dev)
+    B = (torch.rand(N, K, generator=g) * 2 - 1).mul(K ** -0.5).half().to(dev)
+    bias = torch.rand(N, generator=g).to(dev)
+    R = torch.rand(M, N, generator=g).to(dev)
+    C16 = torch.empty(M, N, dtype=torch.float16, device=dev)
+    C32 = torch.empty(M, N, dtype=torch.float32, device=dev)
+    _lib.check(lib.mec_gemm_f16(_p(A), _p(B), _p(bias), _p(R), 1, _p(C16), _p(C32), M, N, K, act, _s()), 'gemm')
+    torch.cuda.synchronize()
+    ref = A.float() @ B.float().t() + bias + R
+    ref = torch.relu(ref) if act == 1 else (torch.nn.functional.gelu(ref) if act == 2 else ref)
+    assert _rel_err(C32, ref) < 1e-5
+    assert _rel_err(C16.float(), ref) < 2e-3
+
+
+def test_gemm_f16_residual_f16_asymmetric(dev):
+    """A = I with an asymmetric B catches a transposed C write."""
+    lib = _lib.load()
+    M = N = K = 128
+    A = torch.eye(M, dtype=torch.float16, device=dev)
+    B = torch.arange(N * K, dtype=torch.float32).reshape(N, K).remainder(97).half().to(dev)
+    R = torch.ones(M, N, dtype=torch.float16, device=dev)
+    C32 = torch.empty(M, N, device=dev)
+    _lib.check(lib.mec_gemm_f16(_p(A), _p(B), None, _p(R), 0, None, _p(C32), M, N, K, 0, _s()), 'gemm')
+    torch.cuda.synchronize()
+    assert torch.equal(C32, B.float().t() + 1)
+
+
+@pytest.mark.parametrize('n,H,C,Cout,ks,stride,pad', [(2, 14, 64, 64, 3, 1, 1), (3, 15, 128, 128, 3, 2, 1),
+                                                     (2, 28, 256, 512, 1, 2, 0), (1, 7, 512, 128, 3, 1, 1)])
+def test_conv_f16(dev, n, H, C, Cout, ks, stride, pad):
+    lib = _lib.load()
+    g = torch.Generator().manual_seed(H * C)
+    x = torch.rand(n, C, H, H, generator=g).half()
+    w = ((torch.rand(Cout, C, ks, ks, generator=g) * 2 - 1) * (C * ks * ks) ** -0.5).half()
+    bias = torch.rand(Cout, generator=g)
+    ref = torch.nn.functional.conv2d(x.float(), w.float(), bias, stride=stride, padding=pad)
+    ref = torch.relu(ref)
+    OH = ref.shape[2]
+    xd = x.permute(0, 2, 3, 1).contiguous().to(dev)
+    wd = w.permute(0, 2, 3, 1).contiguous().to(dev)
+    y = torch.empty(n, OH, OH, Cout, dtype=torch.float16, device=dev)
+    _lib.check(lib.mec_conv_f16(_p(xd), _p(wd), _p(bias.to(dev)), None, _p(y), n, H, H, C, Cout, ks, stride, pad,
+                                1, _s()), 'conv')
+    torch.cuda.synchronize()
+    got = y.float().cpu().permute(0, 3, 1, 2)
+    assert _rel_err(got, ref) < 2e-3
+
+
+def test_resize_bit_exact(dev, golden):
+    lib = _lib.load()
+    g = golden('image_resize.npz')
+    gray = torch.from_numpy(g['gray']).to(dev)
+    out = torch.empty(gray.shape[0], 224, 224, dtype=torch.uint8, device=dev)
+    _lib.check(lib.mec_resize_u8(_p(gray), gray.shape[0], 48, 48, _p(out), 224, 224, _s()), 'resize')
+    torch.cuda.synchronize()
+    assert np.array_equal(out.cpu().numpy(), g['resized'])
+
+
+def test_resize_bit_exact_many(dev):
+    from mec import synthetic as syn
+    from oracle.resize import resize_bilinear_u8
+    lib = _lib.load()
+    gray = syn.image_inputs(64, seed=99)
+    gd = torch.from_numpy(gray).to(dev)
+    out = torch.empty(64, 224, 224, dtype=torch.uint8, device=dev)
+    _lib.check(lib.mec_resize_u8(_p(gd), 64, 48, 48, _p(out), 224, 224, _s()), 'resize')
+    torch.cuda.synchronize()
+    assert np.array_equal(out.cpu().numpy(), resize_bilinear_u8(gray))

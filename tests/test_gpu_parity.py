@@ -1,0 +1,142 @@
+"""Encoder- and pipeline-level parity of the HIP path vs the CPU oracle and the golden
+fixtures (north_star: argmax exact, softmax probabilities within 1e-3)."""
+import numpy as np
+import pytest
+import torch
+
+from mec import engine, synthetic as syn
+from oracle import fusion as o_f, image as o_i, speech as o_s, text as o_t
+
+pytestmark = pytest.mark.gpu
+
+PROB_TOL = 1e-3        # north_star: softmax probabilities within 1e-3
+F32_TOL = 2e-5         # fp32 kernels (speech, fusion) vs fp32 oracle
+
+
+@pytest.fixture(scope='module')
+def models(dev):
+    return {'speech': engine.SpeechEncoder(device=dev), 'text': engine.TextEncoder(device=dev),
+            'image': engine.ImageEncoder(device=dev), 'fusion': engine.FusionHead(device=dev)}
+
+
+def _np(ts):
+    torch.cuda.synchronize()
+    return [t.cpu().numpy() for t in ts]
+
+
+def _margin_ok(ref_probs, got_probs):
+    """argmax exact wherever the oracle's top-2 gap exceeds the numeric tolerance."""
+    srt = np.sort(ref_probs, axis=1)
+    clear = (srt[:, -1] - srt[:, -2]) > 2 * PROB_TOL
+    return np.array_equal(ref_probs.argmax(1)[clear], got_probs.argmax(1)[clear]), int((~clear).sum())
+
+
+def test_speech_golden(models, dev, golden):
+    g = golden('speech.npz')
+    feat, logits, probs = _np(models['speech'].forward(engine.to_device(g['x'], dev)))
+    assert np.abs(feat - g['feat']).max() < F32_TOL * max(1, np.abs(g['feat']).max())
+    assert np.abs(logits - g['logits']).max() < 1e-4
+    assert np.abs(probs - g['probs']).max() < 1e-5
+    assert np.array_equal(probs.argmax(1), g['probs'].argmax(1))
+
+
+@pytest.mark.parametrize('B', [1, 7, 32, 256])
+def test_speech_batches(models, dev, B):
+    x = syn.speech_inputs(B, seed=B)
+    feat, logits, probs = _np(models['speech'].forward(engine.to_device(x, dev)))
+    rf, rl, rp = o_s.forward(syn.weights('speech'), x)
+    assert np.abs(probs - rp).max() < 1e-5
+    assert np.array_equal(probs.argmax(1), rp.argmax(1))
+
+
+def test_fusion_golden(models, dev, golden):
+    g = golden('fusion.npz')
+    args = [engine.to_device(g[k], dev) for k in ('s_feat', 't_feat', 'i_feat', 's_pred', 't_pred', 'i_pred')]
+    logits, probs, aw, dw = _np(models['fusion'].forward(*args))
+    assert np.abs(logits - g['logits']).max() < 1e-4
+    assert np.abs(probs - g['probs']).max() < 1e-5
+    assert np.abs(aw - g['attn_w']).max() < 1e-5
+    assert np.abs(dw - g['dec_w']).max() < 1e-5
+    assert np.array_equal(probs.argmax(1), g['probs'].argmax(1))
+
+
+def test_fuse_weighted_golden(dev, golden):
+    g = golden('fusion.npz')
+    for row, (idx, hs, ht, hi) in enumerate(g['wavg_cases']):
+        s = engine.to_device(g['s_pred'][idx:idx + 1], dev) if hs else None
+        t = engine.to_device(g['t_pred'][idx:idx + 1], dev) if ht else None
+        i = engine.to_device(g['i_pred'][idx:idx + 1], dev) if hi else None
+        out = engine.fuse_weighted(s, t, i).cpu().numpy()[0]
+        np.testing.assert_array_equal(out, g['wavg'][row])  # float64, bit-exact with numpy
+    out = engine.fuse_weighted(None, None, None, device=dev).cpu().numpy()[0]
+    np.testing.assert_array_equal(out, g['wavg_zero'])
+
+
+def test_text_golden(models, dev, golden):
+    g = golden('text_bert.npz')
+    cls, logits, probs = _np(models['text'].forward(engine.to_device(g['ids'], dev), engine.to_device(g['mask'], dev)))
+    assert np.abs(probs - g['probs']).max() < PROB_TOL
+    assert np.array_equal(probs.argmax(1), g['probs'].argmax(1))
+    assert np.abs(cls - g['cls']).max() < 0.05  # fp16 operands through 12 layers, |cls| ~ 1
+
+
+@pytest.mark.parametrize('B,ragged', [(2, True), (16, True), (64, False)])
+def test_text_vs_oracle(models, dev, B, ragged):
+    ids, mask = syn.text_inputs(B, 128, seed=100 + B, ragged=ragged)
+    cls, logits, probs = _np(models['text'].forward(engine.to_device(ids, dev), engine.to_device(mask, dev)))
+    rc, rl, rp = o_t.forward(syn.weights('text'), ids, mask)
+    assert np.abs(probs - rp).max() < PROB_TOL
+    ok, ties = _margin_ok(rp, probs)
+    assert ok, f'argmax mismatch on a clear-margin sample ({ties} near-ties excluded)'
+
+
+def test_image_golden(models, dev, golden):
+    g = golden('image_full.npz')
+    feat, logits, probs = _np(models['image'].forward(engine.to_device(g['gray'], dev)))
+    assert np.abs(probs - g['probs']).max() < PROB_TOL
+    assert np.array_equal(probs.argmax(1), g['probs'].argmax(1))
+
+
+@pytest.mark.parametrize('B', [3, 16])
+def test_image_vs_oracle(models, dev, B):
+    gray = syn.image_inputs(B, seed=200 + B)
+    feat, logits, probs = _np(models['image'].forward(engine.to_device(gray, dev)))
+    rf, rl, rp = o_i.forward(syn.weights('image'), gray)
+    assert np.abs(probs - rp).max() < PROB_TOL
+    assert np.abs(feat - rf).max() < 0.02 * max(1.0, np.abs(rf).max())
+    ok, ties = _margin_ok(rp, probs)
+    assert ok
+
+
+def test_fused_pipeline(dev):
+    B = 8
+    pipe = engine.FusedPipeline(device=dev)
+    x = syn.speech_inputs(B, seed=3)
+    ids, mask = syn.text_inputs(B, 128, seed=3, ragged=True)
+    gray = syn.image_inputs(B, seed=3)
+    out = pipe.forward(engine.to_device(x, dev), engine.to_device(ids, dev), engine.to_device(mask, dev),
+                       engine.to_device(gray, dev))
+    rows = pipe.pack_rows(out)
+    torch.cuda.synchronize()
+    assert rows.shape == (B, engine.ROW)
+    got = {k: [t.cpu().numpy() for t in v] for k, v in out.items()}
+    rf = o_f.forward(syn.weights('fusion'), got['speech'][0], got['text'][0], got['image'][0],
+                     got['speech'][2], got['text'][2], got['image'][2])
+    assert np.abs(got['fusion'][1] - rf[1]).max() < 1e-5
+    assert np.allclose(rows[:, 21:28].cpu().numpy(), got['fusion'][1])
+
+
+def test_empty_batch(models, dev):
+    x = torch.empty(0, 56, device=dev)
+    feat, logits, probs = models['speech'].forward(x)
+    assert feat.shape == (0, 64)
+
+
+def test_bad_shapes_raise(models, dev):
+    with pytest.raises(ValueError):
+        models['speech'].forward(torch.zeros(4, 55, device=dev))
+    with pytest.raises(TypeError):
+        models['image'].forward(torch.zeros(2, 48, 48, device=dev))
+    with pytest.raises(ValueError):
+        ids = torch.zeros(2, 64, dtype=torch.int32, device=dev)
+        models['text'].forward(ids, ids)
