@@ -85,6 +85,10 @@ int mec_gemm_f16(const void* A, const void* B, const float* bias, const void* R,
 int mec_conv_f16(const void* x, const void* w, const float* bias, const void* R, void* y, int n, int H, int W,
                  int C, int Cout, int ks, int stride, int pad, int act, void* stream);
 
+/* Process-wide tuning knobs (A/B benchmarking): "gemm_impl" 1|2, "gemm_bn" 0|64|128|256,
+ * "gemm_autotune" 0|1 (time each GEMM tile width on the first launch of a shape; default 1). */
+int mec_set_option(const char* key, int value);
+
 /* hipEvent timing hook: time every launch of kernel class `tag`. */
 int mec_prof_enable(mec_model* m, int tag);
 int mec_prof_read(mec_model* m, double* total_ms, int* count);

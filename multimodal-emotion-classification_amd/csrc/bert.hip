@@ -214,39 +214,6 @@ __global__ __launch_bounds__(256) void bert_attention_kernel(const f16* __restri
     }
 }
 
-// ----------------------------------------------------------------------------- head
-constexpr int HEAD_R = 8;
-__global__ __launch_bounds__(256) void bert_head_kernel(const float* __restrict__ h32, int B, int L,
-                                                        const float* __restrict__ WpT, const float* __restrict__ bp,
-                                                        const float* __restrict__ WcT, const float* __restrict__ bc,
-                                                        float* cls, float* logits, float* probs) {
-  constexpr int R = HEAD_R;
-  __shared__ float X[R * BH], Y[R * BH], red[R * 256];
-  const int tid = threadIdx.x;
-  const int r0 = blockIdx.x * R, nr = min(R, B - r0);
-  for (int idx = tid; idx < R * BH; idx += blockDim.x) {
-    const int r = idx / BH, c = idx - r * BH;
-    const float v = r < nr ? h32[((size_t)(r0 + r) * L) * BH + c] : 0.f;
-    X[idx] = v;
-    if (r < nr) cls[(size_t)(r0 + r) * BH + c] = v;
-  }
-  __syncthreads();
-  block_linear<R>(X, BH, BH, WpT, bp, BH, Y, BH, red);
-  for (int idx = tid; idx < R * BH; idx += blockDim.x) Y[idx] = tanhf(Y[idx]);
-  __syncthreads();
-  block_linear<R>(Y, BH, BH, WcT, bc, 7, X, BH, red);
-  for (int idx = tid; idx < nr * 7; idx += blockDim.x) {
-    const int r = idx / 7, c = idx - r * 7;
-    logits[(size_t)(r0 + r) * 7 + c] = X[r * BH + c];
-  }
-  __syncthreads();
-  block_softmax_small<R>(X, BH, 7, nullptr, 0);
-  for (int idx = tid; idx < nr * 7; idx += blockDim.x) {
-    const int r = idx / 7, c = idx - r * 7;
-    probs[(size_t)(r0 + r) * 7 + c] = X[r * BH + c];
-  }
-}
-
 // ----------------------------------------------------------------------------- model
 // prm layout per layer (floats): bqkv 2304 | bo 768 | ln1g 768 | ln1b 768 | bi 3072 | bo2 768 |
 // ln2g 768 | ln2b 768  => 9984 ; then head: WpT 768*768 | bp 768 | WcT 768*7 | bc 7
@@ -324,7 +291,7 @@ int TextModel::forward(const int32_t* ids, const int32_t* mask, int B, int L, fl
   MEC_REQUIRE(ids && mask && cls && logits && probs, "text: null pointer");
   const int M = B * L;
   // workspace: h32 | t32 (f32 [M,768]) ; h16 | ctx16 (f16 [M,768]) ; qkv16 [M,2304] / i16 [M,3072]
-  const size_t need = (size_t)M * BH * 4 * 2 + (size_t)M * BH * 2 * 2 + (size_t)M * BI * 2;
+  const size_t need = (size_t)M * BH * 4 * 2 + (size_t)M * BH * 2 * 2 + (size_t)M * BI * 2 + (size_t)B * BH * 4;
   if (M > ws_tokens) {
     MEC_TRY(ws.ensure(need));
     ws_tokens = M;
@@ -335,6 +302,8 @@ int TextModel::forward(const int32_t* ids, const int32_t* mask, int B, int L, fl
   f16* h16 = reinterpret_cast<f16*>(p); p += (size_t)M * BH * 2;
   f16* ctx16 = reinterpret_cast<f16*>(p); p += (size_t)M * BH * 2;
   f16* big16 = reinterpret_cast<f16*>(p);  // qkv16 [M,2304] then i16 [M,3072]
+  p += (size_t)M * BI * 2;
+  float* pooled = reinterpret_cast<float*>(p);  // [B,768]
 
   const float* E = emb.as<float>();
   const float* word = E;
@@ -383,8 +352,12 @@ int TextModel::forward(const int32_t* ids, const int32_t* mask, int B, int L, fl
   }
   const float* head = P + PRM_LAYER * BLAYERS;
   const float *WpT = head, *bp = WpT + (size_t)BH * BH, *WcT = bp + BH, *bc = WcT + (size_t)BH * 7;
-  hipLaunchKernelGGL(bert_head_kernel, dim3((B + HEAD_R - 1) / HEAD_R), dim3(256), 0, s, h32, B, L, WpT, bp, WcT,
-                     bc, cls, logits, probs);
+  // pooler: tanh(cls . Wp^T + bp) over the batch (also copies the CLS feature out)
+  hipLaunchKernelGGL((linear_rows_kernel<8, 768>), dim3((B + 7) / 8, BH / 64), dim3(256), 0, s, h32, (size_t)L * BH, B,
+                     BH, WpT, bp, BH, 64, pooled, BH, (int)BACT_TANH, cls, BH);
+  MEC_LAUNCH_CHECK();
+  hipLaunchKernelGGL((head_softmax_kernel<8, 768>), dim3((B + 7) / 8), dim3(256), 0, s, pooled, B, BH, WcT, bc,
+                     logits, probs);
   MEC_LAUNCH_CHECK();
   return 0;
 }

@@ -18,63 +18,65 @@ __device__ __forceinline__ float wave_max(float v) {
   return v;
 }
 
-// Y[r][n] = sum_k X[r][k] * Wt[k][n] + b[n] for r < R (R samples), n < N.
+enum BlockAct : int { BACT_NONE = 0, BACT_RELU = 1, BACT_TANH = 2 };
+
+__device__ __forceinline__ float block_act(float v, int act) {
+  return act == BACT_RELU ? fmaxf(v, 0.f) : (act == BACT_TANH ? tanhf(v) : v);
+}
+
+// Y[r][n] = act(sum_k X[r][k] * Wt[k*ldw + n] + b[n]) for r < R (R samples), n < N.
 // X: LDS (row stride ldx); Y: LDS or global (row stride ldy).
-// Threads own output columns; when N < blockDim the K loop is split over thread groups
-// and combined through LDS scratch `red` (needs R * blockDim floats).
+// Threads own output columns. When N < blockDim the K range is split into G = T/N
+// contiguous chunks (one per thread group) and the partial sums are combined through
+// LDS scratch `red` (>= R * blockDim floats). Weights are fetched 16 k-rows at a time so
+// 16 independent loads are in flight per thread (the loop is load-latency bound).
 template <int R>
-__device__ __noinline__ void block_linear(const float* X, int ldx, int K, const float* __restrict__ Wt,
-                             const float* __restrict__ b, int N, float* Y, int ldy, float* red) {
+__device__ __noinline__ void block_linear(const float* X, int ldx, int K, const float* __restrict__ Wt, int ldw,
+                                          const float* __restrict__ b, int N, float* Y, int ldy, float* red,
+                                          int act) {
   const int T = blockDim.x, tid = threadIdx.x;
-  if (N >= T / 2 || red == nullptr) {
-    for (int n = tid; n < N; n += T) {
+  const int G = (N >= T || red == nullptr) ? 1 : (T / N);
+  const int cols = (G == 1) ? T : N;
+  const int g = tid / cols, c = tid - g * cols;
+  const int kchunk = (K + G - 1) / G;
+  const int kb = g * kchunk, ke = min(K, kb + kchunk);
+  if (g < G) {
+    for (int n = c; n < N; n += cols) {
       float acc[R];
 #pragma unroll
       for (int r = 0; r < R; ++r) acc[r] = 0.f;
-      int k = 0;
-      for (; k + 4 <= K; k += 4) {
-        const float w0 = Wt[(size_t)(k + 0) * N + n], w1 = Wt[(size_t)(k + 1) * N + n];
-        const float w2 = Wt[(size_t)(k + 2) * N + n], w3 = Wt[(size_t)(k + 3) * N + n];
+      int k = kb;
+      for (; k + 16 <= ke; k += 16) {
+        float w[16];
 #pragma unroll
-        for (int r = 0; r < R; ++r) {
-          const float* x = X + r * ldx + k;
-          acc[r] = fmaf(x[0], w0, acc[r]);
-          acc[r] = fmaf(x[1], w1, acc[r]);
-          acc[r] = fmaf(x[2], w2, acc[r]);
-          acc[r] = fmaf(x[3], w3, acc[r]);
-        }
+        for (int q = 0; q < 16; ++q) w[q] = Wt[(size_t)(k + q) * ldw + n];
+#pragma unroll
+        for (int q = 0; q < 16; ++q)
+#pragma unroll
+          for (int r = 0; r < R; ++r) acc[r] = fmaf(X[r * ldx + k + q], w[q], acc[r]);
       }
-      for (; k < K; ++k) {
-        const float w = Wt[(size_t)k * N + n];
+      for (; k < ke; ++k) {
+        const float w = Wt[(size_t)k * ldw + n];
 #pragma unroll
         for (int r = 0; r < R; ++r) acc[r] = fmaf(X[r * ldx + k], w, acc[r]);
       }
-      const float bv = b ? b[n] : 0.f;
+      if (G == 1) {
+        const float bv = b ? b[n] : 0.f;
 #pragma unroll
-      for (int r = 0; r < R; ++r) Y[r * ldy + n] = acc[r] + bv;
-    }
-  } else {
-    // split-K: G groups of N threads; group g handles k = g, g+G, ...
-    const int G = T / N;
-    const int g = tid / N, n = tid - g * N;
-    if (g < G) {
-      float acc[R];
+        for (int r = 0; r < R; ++r) Y[r * ldy + n] = block_act(acc[r] + bv, act);
+      } else {
 #pragma unroll
-      for (int r = 0; r < R; ++r) acc[r] = 0.f;
-      for (int k = g; k < K; k += G) {
-        const float w = Wt[(size_t)k * N + n];
-#pragma unroll
-        for (int r = 0; r < R; ++r) acc[r] = fmaf(X[r * ldx + k], w, acc[r]);
+        for (int r = 0; r < R; ++r) red[(g * R + r) * N + n] = acc[r];
       }
-#pragma unroll
-      for (int r = 0; r < R; ++r) red[(r * G + g) * N + n] = acc[r];
     }
+  }
+  if (G > 1) {
     __syncthreads();
     for (int idx = tid; idx < R * N; idx += T) {
       const int r = idx / N, nn = idx - r * N;
       float s = 0.f;
-      for (int gg = 0; gg < G; ++gg) s += red[(r * G + gg) * N + nn];
-      Y[r * ldy + nn] = s + (b ? b[nn] : 0.f);
+      for (int gg = 0; gg < G; ++gg) s += red[(gg * R + r) * N + nn];
+      Y[r * ldy + nn] = block_act(s + (b ? b[nn] : 0.f), act);
     }
   }
   __syncthreads();
@@ -124,6 +126,62 @@ __device__ void block_softmax_small(float* X, int ldx, int N, float* out, int ld
     }
   }
   __syncthreads();
+}
+
+// Multi-block fp32 linear over a batch: grid (ceil(B/R), ceil(N/cols)), 256 threads.
+// Y[b, n] = act(X[b,:] . Wt[:, n] + bias[n]); optional copy of the X rows to Xcopy
+// (done by the blockIdx.y == 0 blocks).
+template <int R, int KMAX>
+__global__ __launch_bounds__(256) void linear_rows_kernel(const float* __restrict__ X, size_t ldx, int B, int K,
+                                                          const float* __restrict__ Wt, const float* __restrict__ bias,
+                                                          int N, int cols, float* __restrict__ Y, int ldy, int act,
+                                                          float* __restrict__ Xcopy, int ldxc) {
+  __shared__ float sX[R * KMAX];
+  __shared__ float sY[R * 256];
+  __shared__ float red[R * 256];
+  const int tid = threadIdx.x;
+  const int r0 = blockIdx.x * R, nr = min(R, B - r0);
+  const int col0 = blockIdx.y * cols, nc = min(cols, N - col0);
+  for (int idx = tid; idx < R * K; idx += blockDim.x) {
+    const int r = idx / K, k = idx - r * K;
+    const float v = r < nr ? X[(size_t)(r0 + r) * ldx + k] : 0.f;
+    sX[idx] = v;
+    if (Xcopy && blockIdx.y == 0 && r < nr) Xcopy[(size_t)(r0 + r) * ldxc + k] = v;
+  }
+  __syncthreads();
+  block_linear<R>(sX, K, K, Wt + col0, N, bias + col0, nc, sY, cols, red, act);
+  for (int idx = tid; idx < nr * nc; idx += blockDim.x) {
+    const int r = idx / nc, c = idx - r * nc;
+    Y[(size_t)(r0 + r) * ldy + col0 + c] = sY[r * cols + c];
+  }
+}
+
+// Classification head: logits = X . Wt + b (N = 7), probs = softmax(logits); R rows/block.
+template <int R, int KMAX>
+__global__ __launch_bounds__(256) void head_softmax_kernel(const float* __restrict__ X, int B, int K,
+                                                           const float* __restrict__ Wt, const float* __restrict__ b,
+                                                           float* __restrict__ logits, float* __restrict__ probs) {
+  __shared__ float sX[R * KMAX];
+  __shared__ float sY[R * 8];
+  __shared__ float red[R * 256];
+  const int tid = threadIdx.x;
+  const int r0 = blockIdx.x * R, nr = min(R, B - r0);
+  for (int idx = tid; idx < R * K; idx += blockDim.x) {
+    const int r = idx / K, k = idx - r * K;
+    sX[idx] = r < nr ? X[(size_t)(r0 + r) * K + k] : 0.f;
+  }
+  __syncthreads();
+  block_linear<R>(sX, K, K, Wt, 7, b, 7, sY, 8, red, BACT_NONE);
+  for (int idx = tid; idx < nr * 7; idx += blockDim.x) {
+    const int r = idx / 7, c = idx - r * 7;
+    logits[(size_t)(r0 + r) * 7 + c] = sY[r * 8 + c];
+  }
+  __syncthreads();
+  block_softmax_small<R>(sY, 8, 7, nullptr, 0);
+  for (int idx = tid; idx < nr * 7; idx += blockDim.x) {
+    const int r = idx / 7, c = idx - r * 7;
+    probs[(size_t)(r0 + r) * 7 + c] = sY[r * 8 + c];
+  }
 }
 
 }  // namespace mec

@@ -226,6 +226,9 @@ static int launch_mode(const GemmParams& p, hipStream_t s) {
   return 0;
 }
 
+int g_gemm_impl = 2;  // 1 = register-staged 128x128 kernel, 2 = glds pipelined (default)
+int g_gemm_bn = 0;    // 0 = auto tile width
+
 int launch_gemm(const GemmParams& p, hipStream_t s, Prof* prof, int tag) {
   MEC_REQUIRE(p.M > 0 && p.N > 0 && p.K > 0, "gemm: empty shape");
   MEC_REQUIRE(p.N % 64 == 0, "gemm: N % 64 != 0");
@@ -238,7 +241,11 @@ int launch_gemm(const GemmParams& p, hipStream_t s, Prof* prof, int tag) {
     MEC_REQUIRE(p.K == 128 && p.ks == 7, "stem: K must be 128 (49 taps + 49 flags, padded)");
   }
   if (prof) MEC_TRY(prof->begin(tag, s));
-  int rc = (p.N % 128 == 0) ? launch_mode<128, 128>(p, s) : launch_mode<128, 64>(p, s);
+  int rc;
+  if (p.amode != A_STEM && g_gemm_impl == 2)
+    rc = launch_gemm_glds(p, s, g_gemm_bn);
+  else
+    rc = (p.N % 128 == 0) ? launch_mode<128, 128>(p, s) : launch_mode<128, 64>(p, s);
   if (rc) return rc;
   if (prof) MEC_TRY(prof->end(tag, s));
   return 0;

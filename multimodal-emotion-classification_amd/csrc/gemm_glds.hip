@@ -1,0 +1,350 @@
+// Pipelined fp16 MFMA GEMM / implicit-GEMM conv for gfx950 (the main GEMM engine).
+//
+//   C[M,N] = epilogue( A'[M,K] . B[N,K]^T ),  A' = A (A_PLAIN) or im2col(NHWC) (A_CONV)
+//
+// * Tile BM=256 x BN (64/128/256) x BK=64, 512 threads = 8 waves (WM x WN), each wave a
+//   (BM/WM) x (BN/WN) block of v_mfma_f32_32x32x16_f16 accumulators.
+// * Operands move HBM/L2 -> LDS by global_load_lds_dwordx4 (no VGPR staging) into an
+//   NS-stage ring; a tile is waited for with a counted `s_waitcnt vmcnt` (later tiles
+//   stay in flight) and published with a raw s_barrier. LDS rows are 128 B with the
+//   chunk XOR swizzle kc ^ ((row>>1)&7) applied on the per-lane SOURCE address (the DMA
+//   destination is lane-linear), so the ds_read_b128 fragment reads are conflict-free.
+// * Conv padding / M-tail rows: the lane's source is redirected to a zero page, so the
+//   DMA itself writes the zeros (no predicated stores into the image).
+// * Epilogue: each wave stages 32-row slabs of its accumulators through LDS and writes
+//   them back row-contiguous: bias, residual (f16/f32), ReLU/GELU, f16 and/or f32 out
+//   with 16-byte loads/stores.
+// * XCD-aware bijective block remap: blocks that share an A panel share an L2.
+#include <map>
+#include <mutex>
+
+#include "mec_common.h"
+
+namespace mec {
+
+typedef __attribute__((address_space(3))) void* lds_vptr;
+
+__device__ __attribute__((aligned(64))) uint4 g_zero_page[16];
+
+__device__ __forceinline__ int sw(int row, int kc) { return kc ^ ((row >> 1) & 7); }
+
+__device__ __forceinline__ float gelu_erf2(float x) {
+  return x * 0.5f * (1.0f + erff(x * 0.70710678118654752440f));
+}
+
+template <int N>
+__device__ __forceinline__ void wait_vm() {
+  asm volatile("s_waitcnt vmcnt(%0)" ::"n"(N) : "memory");
+}
+
+template <int BM, int BN, int WM, int WN, int NS, int AM>
+__global__ __launch_bounds__(512, 1) void gemm_glds_kernel(const GemmParams p) {
+  constexpr int BK = 64;
+  constexpr int NW = WM * WN;
+  static_assert(NW == 8, "8 waves");
+  constexpr int TM = BM / WM, TN = BN / WN;    // wave tile
+  constexpr int TI = TM / 32, TJ = TN / 32;    // 32x32 MFMA tiles per wave
+  constexpr int AI = BM / 8 / NW;              // glds wave-instructions per stage (A)
+  constexpr int BI = BN / 8 / NW;              // (B)
+  static_assert(BI >= 1 && AI >= 1, "tile too small for 8 waves");
+  constexpr int LPT = AI + BI;
+  constexpr int STAGE = (BM + BN) * BK;        // halfs per stage
+  constexpr int EPI_LD = TN + 4;               // f32 staging row (padded)
+  constexpr int EPI = NW * 32 * EPI_LD;        // floats for the epilogue staging
+  constexpr int SMEM_H = (NS * STAGE > EPI * 2) ? NS * STAGE : EPI * 2;
+  __shared__ __attribute__((aligned(16))) f16 smem[SMEM_H];
+
+  const int tid = threadIdx.x, lane = tid & 63;
+  const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int wm = wave / WN, wn = wave - (wave / WN) * WN;
+  const int M = p.M, N = p.N, K = p.K;
+  const int nbn = N / BN;
+  const int nbm = (M + BM - 1) / BM;
+  const int nwg = nbm * nbn;
+  int bid = blockIdx.x;
+  {
+    const int xcd = bid & 7, q = nwg >> 3, r = nwg & 7;
+    bid = (xcd < r ? xcd * (q + 1) : r * (q + 1) + (xcd - r) * q) + (bid >> 3);
+  }
+  const int bm = bid / nbn, bn = bid - (bid / nbn) * nbn;
+  const int m0 = bm * BM, n0 = bn * BN;
+
+  // ---- per-lane DMA sources: lane -> (row in its 8-row group, physical chunk)
+  const int lrow = lane >> 3, pchunk = lane & 7;
+  const f16* a_src[AI];
+  int a_ih0[AI], a_iw0[AI];
+  bool a_ok[AI];
+#pragma unroll
+  for (int i = 0; i < AI; ++i) {
+    const int r = (wave * AI + i) * 8 + lrow;  // row within tile
+    const int m = m0 + r;
+    a_ok[i] = m < M;
+    const int mc = a_ok[i] ? m : 0;
+    const int kc = pchunk ^ ((r >> 1) & 7);
+    if constexpr (AM == A_PLAIN) {
+      a_src[i] = reinterpret_cast<const f16*>(p.A) + (size_t)mc * K + kc * 8;
+    } else {
+      const int ohw = p.OH * p.OW;
+      const int n = mc / ohw;
+      const int rem = mc - n * ohw;
+      const int oh = rem / p.OW;
+      const int ow = rem - oh * p.OW;
+      a_ih0[i] = oh * p.stride - p.pad;
+      a_iw0[i] = ow * p.stride - p.pad;
+      a_src[i] = reinterpret_cast<const f16*>(p.A) + (size_t)n * p.H * p.W * p.C + kc * 8;
+    }
+  }
+  const f16* b_src[BI];
+#pragma unroll
+  for (int j = 0; j < BI; ++j) {
+    const int r = (wave * BI + j) * 8 + lrow;
+    const int kc = pchunk ^ ((r >> 1) & 7);
+    b_src[j] = p.B + (size_t)(n0 + r) * K + kc * 8;
+  }
+  const f16* zero = reinterpret_cast<const f16*>(g_zero_page);
+
+  auto issue = [&](int stage, int kt) {
+    const int k0 = kt * BK;
+    f16* sA = smem + stage * STAGE;
+    f16* sB = sA + BM * BK;
+    if constexpr (AM == A_PLAIN) {
+#pragma unroll
+      for (int i = 0; i < AI; ++i) {
+        const f16* src = a_ok[i] ? a_src[i] + k0 : zero;
+        __builtin_amdgcn_global_load_lds((const void*)src, (lds_vptr)(sA + (wave * AI + i) * 8 * BK), 16, 0, 0);
+      }
+    } else {
+      const int tap = k0 / p.C;
+      const int c0 = k0 - tap * p.C;
+      const int kh = tap / p.ks;
+      const int kw = tap - kh * p.ks;
+#pragma unroll
+      for (int i = 0; i < AI; ++i) {
+        const int ih = a_ih0[i] + kh, iw = a_iw0[i] + kw;
+        const bool ok = a_ok[i] && ih >= 0 && ih < p.H && iw >= 0 && iw < p.W;
+        const f16* src = ok ? a_src[i] + ((size_t)ih * p.W + iw) * p.C + c0 : zero;
+        __builtin_amdgcn_global_load_lds((const void*)src, (lds_vptr)(sA + (wave * AI + i) * 8 * BK), 16, 0, 0);
+      }
+    }
+#pragma unroll
+    for (int j = 0; j < BI; ++j)
+      __builtin_amdgcn_global_load_lds((const void*)(b_src[j] + k0), (lds_vptr)(sB + (wave * BI + j) * 8 * BK), 16,
+                                       0, 0);
+  };
+
+  floatx16 acc[TI][TJ];
+#pragma unroll
+  for (int i = 0; i < TI; ++i)
+#pragma unroll
+    for (int j = 0; j < TJ; ++j)
+#pragma unroll
+      for (int e = 0; e < 16; ++e) acc[i][j][e] = 0.f;
+
+  const int nk = K / BK;
+#pragma unroll
+  for (int s = 0; s < NS - 1; ++s)
+    if (s < nk) issue(s, s);
+
+  const int lr = lane & 31, lh = lane >> 5;
+  for (int t = 0; t < nk; ++t) {
+    // tile t must have landed; tiles t+1..t+NS-2 (if issued) may stay in flight
+    const int ahead = min(nk - 1 - t, NS - 2);
+    if constexpr (NS >= 3) {
+      if (ahead >= 1) wait_vm<LPT * (NS - 2)>();
+      else wait_vm<0>();
+    } else {
+      wait_vm<0>();
+    }
+    (void)ahead;
+    __builtin_amdgcn_s_barrier();
+    asm volatile("" ::: "memory");
+    if (t + NS - 1 < nk) issue((t + NS - 1) % NS, t + NS - 1);
+    const f16* sA = smem + (t % NS) * STAGE;
+    const f16* sB = sA + BM * BK;
+#pragma unroll
+    for (int s = 0; s < 4; ++s) {
+      const int kcs = 2 * s + lh;
+      half8 af[TI], bf[TJ];
+#pragma unroll
+      for (int i = 0; i < TI; ++i) {
+        const int r = wm * TM + i * 32 + lr;
+        af[i] = *reinterpret_cast<const half8*>(sA + r * BK + sw(r, kcs) * 8);
+      }
+#pragma unroll
+      for (int j = 0; j < TJ; ++j) {
+        const int r = wn * TN + j * 32 + lr;
+        bf[j] = *reinterpret_cast<const half8*>(sB + r * BK + sw(r, kcs) * 8);
+      }
+#pragma unroll
+      for (int i = 0; i < TI; ++i)
+#pragma unroll
+        for (int j = 0; j < TJ; ++j)
+          acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_f16(af[i], bf[j], acc[i][j], 0, 0, 0);
+    }
+  }
+  asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)" ::: "memory");
+  __builtin_amdgcn_s_barrier();
+  asm volatile("" ::: "memory");
+
+  // ---- epilogue: per wave, 32-row slabs staged through LDS (f32), written row-contiguous
+  float* stg = reinterpret_cast<float*>(smem) + wave * 32 * EPI_LD;
+  constexpr int CPL = TN / 2;  // columns per lane (2 lanes per row)
+  const int er = lane >> 1, ec = (lane & 1) * CPL;
+  const int col0 = n0 + wn * TN + ec;
+#pragma unroll 1
+  for (int i = 0; i < TI; ++i) {
+#pragma unroll
+    for (int j = 0; j < TJ; ++j)
+#pragma unroll
+      for (int e = 0; e < 16; ++e) {
+        const int rr = (e & 3) + 8 * (e >> 2) + 4 * lh;
+        float val = 0.f;
+#pragma unroll
+        for (int ii = 0; ii < TI; ++ii)
+          if (ii == i) val = acc[ii][j][e];
+        stg[rr * EPI_LD + j * 32 + lr] = val;
+      }
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+    const int row = m0 + wm * TM + i * 32 + er;
+    if (row < M) {
+      const size_t base = (size_t)row * N + col0;
+#pragma unroll
+      for (int c = 0; c < CPL; c += 8) {
+        float v[8];
+        const float4 x0 = *reinterpret_cast<const float4*>(stg + er * EPI_LD + ec + c);
+        const float4 x1 = *reinterpret_cast<const float4*>(stg + er * EPI_LD + ec + c + 4);
+        v[0] = x0.x; v[1] = x0.y; v[2] = x0.z; v[3] = x0.w; v[4] = x1.x; v[5] = x1.y; v[6] = x1.z; v[7] = x1.w;
+        if (p.bias) {
+          const float4 b0 = *reinterpret_cast<const float4*>(p.bias + col0 + c);
+          const float4 b1 = *reinterpret_cast<const float4*>(p.bias + col0 + c + 4);
+          v[0] += b0.x; v[1] += b0.y; v[2] += b0.z; v[3] += b0.w; v[4] += b1.x; v[5] += b1.y; v[6] += b1.z; v[7] += b1.w;
+        }
+        if (p.R) {
+          if (p.r_f32) {
+            const float* R = reinterpret_cast<const float*>(p.R) + base + c;
+            const float4 r0 = *reinterpret_cast<const float4*>(R);
+            const float4 r1 = *reinterpret_cast<const float4*>(R + 4);
+            v[0] += r0.x; v[1] += r0.y; v[2] += r0.z; v[3] += r0.w; v[4] += r1.x; v[5] += r1.y; v[6] += r1.z; v[7] += r1.w;
+          } else {
+            const half8 r8 = *reinterpret_cast<const half8*>(reinterpret_cast<const f16*>(p.R) + base + c);
+#pragma unroll
+            for (int q = 0; q < 8; ++q) v[q] += (float)r8[q];
+          }
+        }
+        if (p.act == ACT_RELU) {
+#pragma unroll
+          for (int q = 0; q < 8; ++q) v[q] = fmaxf(v[q], 0.f);
+        } else if (p.act == ACT_GELU) {
+#pragma unroll
+          for (int q = 0; q < 8; ++q) v[q] = gelu_erf2(v[q]);
+        }
+        if (p.C16) {
+          half8 h;
+#pragma unroll
+          for (int q = 0; q < 8; ++q) h[q] = (f16)v[q];
+          *reinterpret_cast<half8*>(p.C16 + base + c) = h;
+        }
+        if (p.C32) {
+          *reinterpret_cast<float4*>(p.C32 + base + c) = make_float4(v[0], v[1], v[2], v[3]);
+          *reinterpret_cast<float4*>(p.C32 + base + c + 4) = make_float4(v[4], v[5], v[6], v[7]);
+        }
+      }
+    }
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+  }
+}
+
+// BM=256 tiles: (BN, WM, WN, NS)
+template <int BN, int WM, int WN, int NS>
+static int launch_cfg(const GemmParams& p, hipStream_t s) {
+  const int nwg = ((p.M + 255) / 256) * (p.N / BN);
+  if (p.amode == A_PLAIN)
+    hipLaunchKernelGGL((gemm_glds_kernel<256, BN, WM, WN, NS, A_PLAIN>), dim3(nwg), dim3(512), 0, s, p);
+  else
+    hipLaunchKernelGGL((gemm_glds_kernel<256, BN, WM, WN, NS, A_CONV>), dim3(nwg), dim3(512), 0, s, p);
+  MEC_LAUNCH_CHECK();
+  return 0;
+}
+
+// Tile-width choice. Every BN computes each output with the same k-ordered MFMA chain, so
+// the choice changes speed only, never results. The first launch of each distinct shape
+// times every legal width on the caller's stream (hipEvents; skipped while the stream is
+// being captured into a graph) and caches the fastest; `gemm_bn` forces a width.
+struct GemmKey {
+  int amode, M, N, K, H, W, C, ks, stride, pad;
+  bool operator<(const GemmKey& o) const {
+    const int a[10] = {amode, M, N, K, H, W, C, ks, stride, pad};
+    const int b[10] = {o.amode, o.M, o.N, o.K, o.H, o.W, o.C, o.ks, o.stride, o.pad};
+    for (int i = 0; i < 10; ++i)
+      if (a[i] != b[i]) return a[i] < b[i];
+    return false;
+  }
+};
+static std::map<GemmKey, int> g_tuned;
+static std::mutex g_tuned_mu;
+int g_gemm_autotune = 1;
+
+static int launch_bn(const GemmParams& p, hipStream_t s, int bn) {
+  switch (bn) {
+    case 256: return launch_cfg<256, 2, 4, 2>(p, s);
+    case 128: return launch_cfg<128, 4, 2, 3>(p, s);
+    case 64: return launch_cfg<64, 4, 2, 3>(p, s);
+    default: set_error("gemm_glds: unsupported BN"); return -1;
+  }
+}
+
+static int heuristic_bn(const GemmParams& p) {
+  const long nbm = (p.M + 255) / 256;
+  if (p.N % 256 == 0 && nbm * (p.N / 256) >= 4 * 256 && p.K >= 768) return 256;
+  if (p.N % 128 == 0 && p.K >= 1024) return 128;
+  if (p.N % 128 == 0 && p.K <= 64) return 128;
+  return 64;
+}
+
+static int tune_bn(const GemmParams& p, hipStream_t s, int* out_bn) {
+  const int cands[3] = {64, 128, 256};
+  hipEvent_t e0, e1;
+  MEC_HIP(hipEventCreate(&e0));
+  MEC_HIP(hipEventCreate(&e1));
+  float best = 1e30f;
+  int best_bn = heuristic_bn(p);
+  for (int bn : cands) {
+    if (p.N % bn) continue;
+    MEC_TRY(launch_bn(p, s, bn));  // warm
+    MEC_HIP(hipEventRecord(e0, s));
+    for (int r = 0; r < 2; ++r) MEC_TRY(launch_bn(p, s, bn));
+    MEC_HIP(hipEventRecord(e1, s));
+    MEC_HIP(hipEventSynchronize(e1));
+    float ms = 0.f;
+    MEC_HIP(hipEventElapsedTime(&ms, e0, e1));
+    if (ms < best) { best = ms; best_bn = bn; }
+  }
+  (void)hipEventDestroy(e0);
+  (void)hipEventDestroy(e1);
+  *out_bn = best_bn;
+  return 0;
+}
+
+int launch_gemm_glds(const GemmParams& p, hipStream_t s, int force_bn) {
+  if (force_bn) return launch_bn(p, s, force_bn);
+  const GemmKey key{p.amode, p.M, p.N, p.K, p.H, p.W, p.C, p.ks, p.stride, p.pad};
+  int bn = 0;
+  {
+    std::lock_guard<std::mutex> lk(g_tuned_mu);
+    auto it = g_tuned.find(key);
+    if (it != g_tuned.end()) bn = it->second;
+  }
+  if (!bn) {
+    hipStreamCaptureStatus cs = hipStreamCaptureStatusNone;
+    if (g_gemm_autotune && hipStreamIsCapturing(s, &cs) == hipSuccess && cs == hipStreamCaptureStatusNone) {
+      MEC_TRY(tune_bn(p, s, &bn));
+    } else {
+      bn = heuristic_bn(p);
+    }
+    std::lock_guard<std::mutex> lk(g_tuned_mu);
+    g_tuned[key] = bn;
+  }
+  return launch_bn(p, s, bn);
+}
+
+}  // namespace mec

@@ -117,5 +117,9 @@ struct GemmParams {
 };
 
 int launch_gemm(const GemmParams& p, hipStream_t s, Prof* prof, int tag);
+int launch_gemm_glds(const GemmParams& p, hipStream_t s, int force_bn);
+extern int g_gemm_impl;
+extern int g_gemm_bn;
+extern int g_gemm_autotune;
 
 }  // namespace mec

@@ -137,48 +137,15 @@ __global__ __launch_bounds__(256) void maxpool3s2_kernel(const f16* __restrict__
   *reinterpret_cast<half8*>(y + (((size_t)n * OH + oh) * OW + ow) * C + cc * 8) = o;
 }
 
-// ----------------------------------------------------------------------------- head
-constexpr int IHEAD_R = 8;
-__global__ __launch_bounds__(256) void resnet_head_kernel(const f16* __restrict__ x, int B, int HW,
-                                                          const float* __restrict__ W1T, const float* __restrict__ b1,
-                                                          const float* __restrict__ W2T, const float* __restrict__ b2,
-                                                          float* feat, float* logits, float* probs) {
-  constexpr int R = IHEAD_R, C = 2048;
-  __shared__ float X[R * C];
-  __shared__ float Y[R * 512];
-  __shared__ float red[R * 256];
-  const int tid = threadIdx.x;
-  const int r0 = blockIdx.x * R, nr = min(R, B - r0);
-  // AdaptiveAvgPool2d(1): mean over the HW positions
-  for (int idx = tid; idx < R * C; idx += 256) {
-    const int r = idx / C, c = idx - r * C;
-    float s = 0.f;
-    if (r < nr) {
-      const f16* p = x + (size_t)(r0 + r) * HW * C + c;
-      for (int q = 0; q < HW; ++q) s += (float)p[(size_t)q * C];
-    }
-    X[idx] = s / (float)HW;
-  }
-  __syncthreads();
-  block_linear<R>(X, C, C, W1T, b1, 512, Y, 512, red);
-  for (int idx = tid; idx < R * 512; idx += 256) {
-    const int r = idx >> 9, n = idx & 511;
-    const float v = fmaxf(Y[idx], 0.f);
-    Y[idx] = v;
-    if (r < nr) feat[(size_t)(r0 + r) * 512 + n] = v;  // fc[2] ReLU output (extract_features)
-  }
-  __syncthreads();
-  block_linear<R>(Y, 512, 512, W2T, b2, 7, X, C, red);
-  for (int idx = tid; idx < nr * 7; idx += 256) {
-    const int r = idx / 7, c = idx - r * 7;
-    logits[(size_t)(r0 + r) * 7 + c] = X[r * C + c];
-  }
-  __syncthreads();
-  block_softmax_small<R>(X, C, 7, nullptr, 0);
-  for (int idx = tid; idx < nr * 7; idx += 256) {
-    const int r = idx / 7, c = idx - r * 7;
-    probs[(size_t)(r0 + r) * 7 + c] = X[r * C + c];
-  }
+// ----------------------------------------------------------------------------- avgpool
+// AdaptiveAvgPool2d(1) on NHWC f16 -> f32 [B, C]: one thread per (sample, channel).
+__global__ __launch_bounds__(256) void avgpool_kernel(const f16* __restrict__ x, int HW, int C, float* __restrict__ y) {
+  const int b = blockIdx.x, c = blockIdx.y * 256 + threadIdx.x;
+  if (c >= C) return;
+  const f16* p = x + (size_t)b * HW * C + c;
+  float s = 0.f;
+  for (int q = 0; q < HW; ++q) s += (float)p[(size_t)q * C];
+  y[(size_t)b * C + c] = s / (float)HW;
 }
 
 // ----------------------------------------------------------------------------- model
@@ -289,7 +256,7 @@ int ImageModel::forward(const uint8_t* gray, int B, float* feat, float* logits, 
   MEC_REQUIRE(gray && feat && logits && probs, "image: null pointer");
   const size_t per_img_big = (size_t)56 * 56 * 256;  // largest NHWC activation (elements)
   const size_t per_t1 = (size_t)56 * 56 * 128, per_t2 = (size_t)56 * 56 * 64;
-  const size_t per_img = 224 * 224 + (3 * per_img_big + per_t1 + per_t2) * sizeof(f16) + 256;
+  const size_t per_img = 224 * 224 + (3 * per_img_big + per_t1 + per_t2) * sizeof(f16) + 256 + 2048 * sizeof(float);
   if (B > ws_batch) {
     MEC_TRY(ws.ensure(per_img * (size_t)B + 4096));
     ws_batch = B;
@@ -302,6 +269,8 @@ int ImageModel::forward(const uint8_t* gray, int B, float* feat, float* logits, 
   f16* DS = reinterpret_cast<f16*>(p); p += (size_t)B * per_img_big * sizeof(f16);
   f16* T1 = reinterpret_cast<f16*>(p); p += (size_t)B * per_t1 * sizeof(f16);
   f16* T2 = reinterpret_cast<f16*>(p);
+  p += (size_t)B * per_t2 * sizeof(f16);
+  float* pooled = reinterpret_cast<float*>(p);  // [B,2048]
 
   const f16* Wt = wts.as<f16>();
   const float* P = prm.as<float>();
@@ -352,8 +321,14 @@ int ImageModel::forward(const uint8_t* gray, int B, float* feat, float* logits, 
     std::swap(cur, other);
     H = OH;
   }
-  hipLaunchKernelGGL(resnet_head_kernel, dim3((B + IHEAD_R - 1) / IHEAD_R), dim3(256), 0, s, cur, B, H * H,
-                     P + fc1_off, P + fc1b_off, P + fc2_off, P + fc2b_off, feat, logits, probs);
+  hipLaunchKernelGGL(avgpool_kernel, dim3(B, 2048 / 256), dim3(256), 0, s, cur, H * H, 2048, pooled);
+  MEC_LAUNCH_CHECK();
+  // fc[1] Linear(2048,512) + fc[2] ReLU -> the 512-d feature (extract_features)
+  hipLaunchKernelGGL((linear_rows_kernel<8, 2048>), dim3((B + 7) / 8, 512 / 64), dim3(256), 0, s, pooled, (size_t)2048,
+                     B, 2048, P + fc1_off, P + fc1b_off, 512, 64, feat, 512, (int)BACT_RELU, (float*)nullptr, 0);
+  MEC_LAUNCH_CHECK();
+  hipLaunchKernelGGL((head_softmax_kernel<8, 768>), dim3((B + 7) / 8), dim3(256), 0, s, feat, B, 512, P + fc2_off,
+                     P + fc2b_off, logits, probs);
   MEC_LAUNCH_CHECK();
   return 0;
 }

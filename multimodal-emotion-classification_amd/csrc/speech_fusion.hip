@@ -22,13 +22,14 @@ struct SpeechW {
   const float* shift[5];
 };
 
-constexpr int SPEECH_R = 8;
+constexpr int SPEECH_R = 4;
+constexpr int SF_THREADS = 512;
 __constant__ int kSpeechDims[6] = {56, 512, 512, 256, 128, 64};
 
-__global__ __launch_bounds__(256) void speech_kernel(SpeechW w, const float* __restrict__ x, int B,
+__global__ __launch_bounds__(512) void speech_kernel(SpeechW w, const float* __restrict__ x, int B,
                                                      float* feat, float* logits, float* probs) {
   constexpr int R = SPEECH_R, LD = 512;
-  __shared__ float bufA[R * LD], bufB[R * LD], red[R * 256];
+  __shared__ float bufA[R * LD], bufB[R * LD], red[R * SF_THREADS];
   const int tid = threadIdx.x;
   const int r0 = blockIdx.x * R;
   const int nr = min(R, B - r0);
@@ -42,7 +43,7 @@ __global__ __launch_bounds__(256) void speech_kernel(SpeechW w, const float* __r
   float* out = bufB;
   for (int l = 0; l < 5; ++l) {
     const int K = kSpeechDims[l], N = kSpeechDims[l + 1];
-    block_linear<R>(in, LD, K, w.W[l], w.b[l], N, out, LD, red);
+    block_linear<R>(in, LD, K, w.W[l], N, w.b[l], N, out, LD, red, BACT_NONE);
     for (int idx = tid; idx < R * N; idx += blockDim.x) {
       const int r = idx / N, n = idx - r * N;
       // tf.nn.batch_normalization: x * inv + (beta - mean * inv), inv = rsqrt(var+eps)*gamma
@@ -56,7 +57,7 @@ __global__ __launch_bounds__(256) void speech_kernel(SpeechW w, const float* __r
     const int r = idx / 64, n = idx - r * 64;
     feat[(size_t)(r0 + r) * 64 + n] = in[r * LD + n];
   }
-  block_linear<R>(in, LD, 64, w.W[5], w.b[5], 7, out, LD, red);
+  block_linear<R>(in, LD, 64, w.W[5], 7, w.b[5], 7, out, LD, red, BACT_NONE);
   for (int idx = tid; idx < nr * 7; idx += blockDim.x) {
     const int r = idx / 7, n = idx - r * 7;
     logits[(size_t)(r0 + r) * 7 + n] = out[r * LD + n];
@@ -113,7 +114,7 @@ int SpeechModel::forward(const float* x, int B, float* feat, float* logits, floa
   for (int l = 0; l < 6; ++l) { p.W[l] = base + off_W[l]; p.b[l] = base + off_b[l]; }
   for (int l = 0; l < 5; ++l) { p.inv[l] = base + off_inv[l]; p.shift[l] = base + off_shift[l]; }
   MEC_TRY(prof.begin(TAG_SPEECH, s));
-  hipLaunchKernelGGL(speech_kernel, dim3((B + SPEECH_R - 1) / SPEECH_R), dim3(256), 0, s, p, x, B, feat,
+  hipLaunchKernelGGL(speech_kernel, dim3((B + SPEECH_R - 1) / SPEECH_R), dim3(SF_THREADS), 0, s, p, x, B, feat,
                      logits, probs);
   MEC_LAUNCH_CHECK();
   MEC_TRY(prof.end(TAG_SPEECH, s));
@@ -129,7 +130,7 @@ int SpeechModel::forward(const float* x, int B, float* feat, float* logits, floa
 constexpr int FUSION_NP = 70;
 struct FusionW { const float* p[FUSION_NP]; };
 
-constexpr int FUSION_R = 4;
+constexpr int FUSION_R = 2;
 constexpr int F_LDIN = 1368, F_LDP = 768, F_LDT = 1280;
 
 __device__ void cross_attention_rows(float* T, int ldt, int nr) {
@@ -160,13 +161,13 @@ __device__ void cross_attention_rows(float* T, int ldt, int nr) {
   __syncthreads();
 }
 
-__global__ __launch_bounds__(256) void fusion_kernel(FusionW w, const float* __restrict__ sf,
+__global__ __launch_bounds__(512) void fusion_kernel(FusionW w, const float* __restrict__ sf,
                                                      const float* __restrict__ tf, const float* __restrict__ imf,
                                                      const float* __restrict__ sp, const float* __restrict__ tp,
                                                      const float* __restrict__ ip, int B, float* logits,
                                                      float* probs, float* attn_w, float* dec_w) {
   constexpr int R = FUSION_R;
-  __shared__ float IN[R * F_LDIN], P[R * F_LDP], E[R * F_LDP], T[R * F_LDT], red[R * 256];
+  __shared__ float IN[R * F_LDIN], P[R * F_LDP], E[R * F_LDP], T[R * F_LDT], red[R * SF_THREADS];
   const int tid = threadIdx.x, T_ = blockDim.x;
   const int r0 = blockIdx.x * R;
   const int nr = min(R, B - r0);
@@ -188,20 +189,20 @@ __global__ __launch_bounds__(256) void fusion_kernel(FusionW w, const float* __r
   const int in_off[3] = {0, 64, 832}, in_dim[3] = {64, 768, 512};
   // modality projections: ReLU(LN(Linear)) (multimodal_fusion.py:113-130, :157-159)
   for (int m = 0; m < 3; ++m) {
-    block_linear<R>(IN + in_off[m], F_LDIN, in_dim[m], w.p[4 * m], w.p[4 * m + 1], 256, P + 256 * m, F_LDP, red);
+    block_linear<R>(IN + in_off[m], F_LDIN, in_dim[m], w.p[4 * m], 256, w.p[4 * m + 1], 256, P + 256 * m, F_LDP, red, BACT_NONE);
     block_layernorm<R>(P + 256 * m, F_LDP, 256, w.p[4 * m + 2], w.p[4 * m + 3], 1e-5f, true);
   }
   // cross-modal attention (:161-167): query m attends to the other two (in order)
   const int others[3][2] = {{1, 2}, {0, 2}, {0, 1}};
   for (int m = 0; m < 3; ++m) {
     const float* const* c = w.p + 12 + 10 * m;
-    block_linear<R>(P + 256 * m, F_LDP, 256, c[0], c[1], 256, T + 0, F_LDT, red);
-    block_linear<R>(P + 256 * others[m][0], F_LDP, 256, c[2], c[3], 256, T + 256, F_LDT, red);
-    block_linear<R>(P + 256 * others[m][1], F_LDP, 256, c[2], c[3], 256, T + 512, F_LDT, red);
-    block_linear<R>(P + 256 * others[m][0], F_LDP, 256, c[4], c[5], 256, T + 768, F_LDT, red);
-    block_linear<R>(P + 256 * others[m][1], F_LDP, 256, c[4], c[5], 256, T + 1024, F_LDT, red);
+    block_linear<R>(P + 256 * m, F_LDP, 256, c[0], 256, c[1], 256, T + 0, F_LDT, red, BACT_NONE);
+    block_linear<R>(P + 256 * others[m][0], F_LDP, 256, c[2], 256, c[3], 256, T + 256, F_LDT, red, BACT_NONE);
+    block_linear<R>(P + 256 * others[m][1], F_LDP, 256, c[2], 256, c[3], 256, T + 512, F_LDT, red, BACT_NONE);
+    block_linear<R>(P + 256 * others[m][0], F_LDP, 256, c[4], 256, c[5], 256, T + 768, F_LDT, red, BACT_NONE);
+    block_linear<R>(P + 256 * others[m][1], F_LDP, 256, c[4], 256, c[5], 256, T + 1024, F_LDT, red, BACT_NONE);
     cross_attention_rows(T, F_LDT, nr);
-    block_linear<R>(T, F_LDT, 256, c[6], c[7], 256, E + 256 * m, F_LDP, red);
+    block_linear<R>(T, F_LDT, 256, c[6], 256, c[7], 256, E + 256 * m, F_LDP, red, BACT_NONE);
     for (int idx = tid; idx < R * 256; idx += T_) {
       const int r = idx >> 8, n = idx & 255;
       E[r * F_LDP + 256 * m + n] = P[r * F_LDP + 256 * m + n] + E[r * F_LDP + 256 * m + n];
@@ -211,16 +212,11 @@ __global__ __launch_bounds__(256) void fusion_kernel(FusionW w, const float* __r
   }
   // AttentionFusion (:79-106): per-modality projection, attention over the 768 concat
   for (int j = 0; j < 3; ++j) {
-    block_linear<R>(E + 256 * j, F_LDP, 256, w.p[42 + 4 * j], w.p[43 + 4 * j], 256, T + 256 * j, F_LDT, red);
+    block_linear<R>(E + 256 * j, F_LDP, 256, w.p[42 + 4 * j], 256, w.p[43 + 4 * j], 256, T + 256 * j, F_LDT, red, BACT_NONE);
     block_layernorm<R>(T + 256 * j, F_LDT, 256, w.p[44 + 4 * j], w.p[45 + 4 * j], 1e-5f, true);
   }
-  block_linear<R>(T, F_LDT, 768, w.p[54], w.p[55], 256, T + 768, F_LDT, red);
-  for (int idx = tid; idx < R * 256; idx += T_) {
-    const int r = idx >> 8, n = idx & 255;
-    T[r * F_LDT + 768 + n] = tanhf(T[r * F_LDT + 768 + n]);
-  }
-  __syncthreads();
-  block_linear<R>(T + 768, F_LDT, 256, w.p[56], w.p[57], 3, P, F_LDP, red);
+  block_linear<R>(T, F_LDT, 768, w.p[54], 256, w.p[55], 256, T + 768, F_LDT, red, BACT_TANH);
+  block_linear<R>(T + 768, F_LDT, 256, w.p[56], 3, w.p[57], 3, P, F_LDP, red, BACT_NONE);
   block_softmax_small<R>(P, F_LDP, 3, nullptr, 0);
   for (int idx = tid; idx < R * 256; idx += T_) {  // fused = sum_j w_j * proj_j
     const int r = idx >> 8, n = idx & 255;
@@ -234,13 +230,8 @@ __global__ __launch_bounds__(256) void fusion_kernel(FusionW w, const float* __r
   }
   __syncthreads();
   // decision weights over the 21-d concat of softmax outputs (:138-143, :171-175)
-  block_linear<R>(IN + 1344, F_LDIN, 21, w.p[58], w.p[59], 64, P + 256, F_LDP, red);
-  for (int idx = tid; idx < R * 64; idx += T_) {
-    const int r = idx >> 6, n = idx & 63;
-    P[r * F_LDP + 256 + n] = fmaxf(P[r * F_LDP + 256 + n], 0.f);
-  }
-  __syncthreads();
-  block_linear<R>(P + 256, F_LDP, 64, w.p[60], w.p[61], 3, P + 384, F_LDP, red);
+  block_linear<R>(IN + 1344, F_LDIN, 21, w.p[58], 64, w.p[59], 64, P + 256, F_LDP, red, BACT_RELU);
+  block_linear<R>(P + 256, F_LDP, 64, w.p[60], 3, w.p[61], 3, P + 384, F_LDP, red, BACT_NONE);
   block_softmax_small<R>(P + 384, F_LDP, 3, nullptr, 0);
   for (int idx = tid; idx < R * 7; idx += T_) {
     const int r = idx / 7, c = idx - r * 7;
@@ -254,15 +245,10 @@ __global__ __launch_bounds__(256) void fusion_kernel(FusionW w, const float* __r
   }
   __syncthreads();
   // classifier on [fused, weighted_preds] (:145-154, :177-178)
-  block_linear<R>(E, F_LDP, 263, w.p[62], w.p[63], 256, T, F_LDT, red);
+  block_linear<R>(E, F_LDP, 263, w.p[62], 256, w.p[63], 256, T, F_LDT, red, BACT_NONE);
   block_layernorm<R>(T, F_LDT, 256, w.p[64], w.p[65], 1e-5f, true);
-  block_linear<R>(T, F_LDT, 256, w.p[66], w.p[67], 128, T + 256, F_LDT, red);
-  for (int idx = tid; idx < R * 128; idx += T_) {
-    const int r = idx >> 7, n = idx & 127;
-    T[r * F_LDT + 256 + n] = fmaxf(T[r * F_LDT + 256 + n], 0.f);
-  }
-  __syncthreads();
-  block_linear<R>(T + 256, F_LDT, 128, w.p[68], w.p[69], 7, T + 384, F_LDT, red);
+  block_linear<R>(T, F_LDT, 256, w.p[66], 128, w.p[67], 128, T + 256, F_LDT, red, BACT_RELU);
+  block_linear<R>(T + 256, F_LDT, 128, w.p[68], 7, w.p[69], 7, T + 384, F_LDT, red, BACT_NONE);
   for (int idx = tid; idx < nr * 7; idx += T_) {
     const int r = idx / 7, c = idx - r * 7;
     logits[(size_t)(r0 + r) * 7 + c] = T[r * F_LDT + 384 + c];
@@ -336,7 +322,7 @@ int FusionModel::forward(const float* sf, const float* tf, const float* imf, con
   const float* base = w.as<float>();
   for (int i = 0; i < FUSION_NP; ++i) p.p[i] = base + off[i];
   MEC_TRY(prof.begin(TAG_FUSION, s));
-  hipLaunchKernelGGL(fusion_kernel, dim3((B + FUSION_R - 1) / FUSION_R), dim3(256), 0, s, p, sf, tf, imf, sp,
+  hipLaunchKernelGGL(fusion_kernel, dim3((B + FUSION_R - 1) / FUSION_R), dim3(SF_THREADS), 0, s, p, sf, tf, imf, sp,
                      tp, ip, B, logits, probs, attn_w, dec_w);
   MEC_LAUNCH_CHECK();
   MEC_TRY(prof.end(TAG_FUSION, s));
