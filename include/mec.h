@@ -64,6 +64,14 @@ int mec_text_fwd(mec_model* m, const int32_t* ids, const int32_t* mask, int B, i
 int mec_image_fwd(mec_model* m, const uint8_t* gray, int B, float* feat, float* logits, float* probs,
                   void* stream);
 
+/* Generic image entry: img u8[B,H,W,C] in one of
+ *   (48,48,1)    FER2013 gray, resized on the GPU (same as mec_image_fwd),
+ *   (224,224,1)  gray already resized by PIL on the host (any input size),
+ *   (224,224,3)  RGB already resized by PIL on the host (colour inputs).
+ * Replaces ImageInference.predict for arbitrary image files (image_inference.py:112-113). */
+int mec_image_fwd_u8(mec_model* m, const uint8_t* img, int B, int H, int W, int C, float* feat, float* logits,
+                     float* probs, void* stream);
+
 /* Attention-MLP fusion. Outputs logits/probs f32[B,7], attn_w/dec_w f32[B,3].
  * Replaces MultimodalFusion.fuse_with_attention  inference/multimodal_fusion.py:201-239. */
 int mec_fusion_fwd(mec_model* m, const float* s_feat, const float* t_feat, const float* i_feat,
@@ -74,6 +82,10 @@ int mec_fusion_fwd(mec_model* m, const float* s_feat, const float* t_feat, const
  * Replaces MultimodalFusion.fuse_predictions  inference/multimodal_fusion.py:184-199. */
 int mec_fuse_weighted(const float* s_probs, const float* t_probs, const float* i_probs, int B,
                       double* out, void* stream);
+
+/* Same with float64 inputs (per-request dicts carry Python floats, e.g. heuristic 0.1/6). */
+int mec_fuse_weighted_f64(const double* s_probs, const double* t_probs, const double* i_probs, int B,
+                          double* out, void* stream);
 
 /* Kernel-level entry points (parity tests / microbenchmarks). */
 int mec_resize_u8(const uint8_t* in, int B, int H, int W, uint8_t* out, int OH, int OW, void* stream);

@@ -149,6 +149,15 @@ int mec_image_fwd(mec_model* m, const uint8_t* gray, int B, float* feat, float* 
   })
 }
 
+int mec_image_fwd_u8(mec_model* m, const uint8_t* img, int B, int H, int W, int C, float* feat, float* logits,
+                     float* probs, void* stream) {
+  API_GUARD({
+    auto* p = as<ImageModel>(m, KIND_IMAGE);
+    if (!p) return -1;
+    return p->forward_u8(img, B, H, W, C, feat, logits, probs, S(stream));
+  })
+}
+
 int mec_fusion_fwd(mec_model* m, const float* s_feat, const float* t_feat, const float* i_feat, const float* s_pred,
                    const float* t_pred, const float* i_pred, int B, float* logits, float* probs, float* attn_w,
                    float* dec_w, void* stream) {
@@ -161,6 +170,10 @@ int mec_fusion_fwd(mec_model* m, const float* s_feat, const float* t_feat, const
 
 int mec_fuse_weighted(const float* s, const float* t, const float* i, int B, double* out, void* stream) {
   API_GUARD({ return fuse_weighted(s, t, i, B, out, S(stream)); })
+}
+
+int mec_fuse_weighted_f64(const double* s, const double* t, const double* i, int B, double* out, void* stream) {
+  API_GUARD({ return fuse_weighted_f64(s, t, i, B, out, S(stream)); })
 }
 
 int mec_resize_u8(const uint8_t* in, int B, int H, int W, uint8_t* out, int OH, int OW, void* stream) {

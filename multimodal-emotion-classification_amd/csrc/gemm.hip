@@ -3,8 +3,9 @@
 //   A_CONV   implicit im2col of an NHWC f16 tensor (ResNet 3x3 convs, strided 1x1
 //            downsample convs); K ordered (kh, kw, c), C % 64 == 0 so a 64-deep K tile
 //            never straddles two filter taps
-//   A_STEM   the ResNet stem on the u8 resized image: K = 128 = 49 pixel taps | 15 zeros |
-//            49 "tap in bounds" flags | 15 zeros. The RGB-replicate + ToTensor + Normalize
+//   A_STEM   the ResNet stem on a u8 224x224 image with C = 1 (gray, RGB-replicated) or 3
+//            channels: K = 64*(C+1) = per channel 49 pixel taps | 15 zeros, then 49
+//            "tap in bounds" flags | 15 zeros. The RGB-replicate + ToTensor + Normalize
 //            of inference/image_inference.py:28-32 is folded into the stem weights (the
 //            flag half carries the -mean/std term, so zero padding stays exact).
 // B is the weight matrix [N,K] (K contiguous = torch Linear layout). Epilogue fuses
@@ -73,7 +74,7 @@ __global__ __launch_bounds__(256, 2) void gemm_f16_kernel(const GemmParams p) {
       const int ow = rem - oh * p.OW;
       a_ih0[i] = oh * p.stride - p.pad;
       a_iw0[i] = ow * p.stride - p.pad;
-      a_img[i] = (size_t)n * p.H * p.W * (AM == A_CONV ? p.C : 1);
+      a_img[i] = (size_t)n * p.H * p.W * p.C;
     }
   }
   const f16* b_src[BI];
@@ -117,8 +118,8 @@ __global__ __launch_bounds__(256, 2) void gemm_f16_kernel(const GemmParams p) {
             const int kh = t / 7, kw = t - (t / 7) * 7;
             const int ih = a_ih0[i] + kh, iw = a_iw0[i] + kw;
             const bool ok = a_in[i] && ih >= 0 && ih < p.H && iw >= 0 && iw < p.W;
-            if (kt == 0) val = ok ? (float)X[a_img[i] + (size_t)ih * p.W + iw] : 0.f;
-            else val = ok ? 1.f : 0.f;
+            if (kt < p.C) val = ok ? (float)X[a_img[i] + ((size_t)ih * p.W + iw) * p.C + kt] : 0.f;
+            else val = ok ? 1.f : 0.f;  // "tap in bounds" flag (carries the -mean/std term)
           }
           h[e] = (f16)val;
         }
@@ -238,7 +239,8 @@ int launch_gemm(const GemmParams& p, hipStream_t s, Prof* prof, int tag) {
   if (p.amode == A_CONV) {
     MEC_REQUIRE(p.C % 64 == 0 && p.K == p.ks * p.ks * p.C, "conv: C % 64 != 0 or K != ks*ks*C");
   } else if (p.amode == A_STEM) {
-    MEC_REQUIRE(p.K == 128 && p.ks == 7, "stem: K must be 128 (49 taps + 49 flags, padded)");
+    MEC_REQUIRE((p.C == 1 || p.C == 3) && p.K == 64 * (p.C + 1) && p.ks == 7,
+                "stem: K must be 64*(C+1) (49 taps per channel + 49 flags, each padded to 64)");
   }
   if (prof) MEC_TRY(prof->begin(tag, s));
   int rc;

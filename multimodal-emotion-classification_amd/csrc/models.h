@@ -36,6 +36,7 @@ struct FusionModel : Model {
 };
 
 int fuse_weighted(const float* s, const float* t, const float* i, int B, double* out, hipStream_t st);
+int fuse_weighted_f64(const double* s, const double* t, const double* i, int B, double* out, hipStream_t st);
 
 // ---------------------------------------------------------------- BERT-base
 struct TextModel : Model {
@@ -64,11 +65,15 @@ struct ImageModel : Model {
   DevBuf prm;   // fp32 biases, stem weights, head
   DevBuf ws;    // workspace
   int ws_batch = 0;
-  ConvLayer stem;
+  ConvLayer stem;      // gray input (channels folded): K = 128
+  ConvLayer stem_rgb;  // RGB input: K = 256
   std::vector<Bottleneck> blocks;
   size_t fc1_off = 0, fc1b_off = 0, fc2_off = 0, fc2b_off = 0;
   int create(const float* blob, size_t n);
   int forward(const uint8_t* gray, int B, float* feat, float* logits, float* probs, hipStream_t s);
+  // img u8 [B,H,W,C]: (48,48,1) gray FER2013 (GPU resize), (224,224,1) gray, (224,224,3) RGB
+  int forward_u8(const uint8_t* img, int B, int H, int W, int C, float* feat, float* logits, float* probs,
+                 hipStream_t s);
 };
 
 int resize_u8(const uint8_t* in, int B, int H, int W, uint8_t* out, int OH, int OW, hipStream_t s);

@@ -186,15 +186,20 @@ int ImageModel::create(const float* blob, size_t n) {
                 (f16)((double)src[(((size_t)o * cin + c) * ks + kh) * ks + kw] * scale[o]);
     return L;
   };
-  // stem: fold RGB replication + ToTensor(/255) + Normalize + BN scale into K=128 rows
+  // stem: fold ToTensor(/255) + Normalize + BN scale into the K rows (see gemm.hip A_STEM):
+  // gray input folds the three replicated channels into one (K=128); RGB keeps them (K=256).
   {
     const float* src = rd.take((size_t)64 * 3 * 49);
     std::vector<float> scale;
     stem.b_off = bn_fold(64, scale);
-    stem.w_off = w.size();
     stem.cin = 1; stem.cout = 64; stem.ks = 7; stem.stride = 2; stem.pad = 3;
-    const double mean[3] = {0.485, 0.456, 0.406}, stdv[3] = {0.229, 0.224, 0.225};
+    stem_rgb = stem;
+    stem_rgb.cin = 3;
+    stem.w_off = w.size();
     w.resize(w.size() + 64 * 128, (f16)0.f);
+    stem_rgb.w_off = w.size();
+    w.resize(w.size() + 64 * 256, (f16)0.f);
+    const double mean[3] = {0.485, 0.456, 0.406}, stdv[3] = {0.229, 0.224, 0.225};
     if (rd.ok) {
       for (int o = 0; o < 64; ++o)
         for (int t = 0; t < 49; ++t) {
@@ -204,9 +209,11 @@ int ImageModel::create(const float* blob, size_t n) {
             const double mf = (double)(float)mean[c], sf = (double)(float)stdv[c];
             a += wv / (255.0 * sf);
             c0 -= wv * mf / sf;
+            w[stem_rgb.w_off + (size_t)o * 256 + 64 * c + t] = (f16)(wv / (255.0 * sf) * scale[o]);
           }
           w[stem.w_off + (size_t)o * 128 + t] = (f16)(a * scale[o]);
           w[stem.w_off + (size_t)o * 128 + 64 + t] = (f16)(c0 * scale[o]);
+          w[stem_rgb.w_off + (size_t)o * 256 + 192 + t] = (f16)(c0 * scale[o]);
         }
     }
   }
@@ -251,9 +258,17 @@ int ImageModel::create(const float* blob, size_t n) {
 }
 
 int ImageModel::forward(const uint8_t* gray, int B, float* feat, float* logits, float* probs, hipStream_t s) {
+  return forward_u8(gray, B, 48, 48, 1, feat, logits, probs, s);
+}
+
+int ImageModel::forward_u8(const uint8_t* img, int B, int H, int W, int C, float* feat, float* logits, float* probs,
+                           hipStream_t s) {
   MEC_REQUIRE(B >= 0, "image: B < 0");
   if (B == 0) return 0;
-  MEC_REQUIRE(gray && feat && logits && probs, "image: null pointer");
+  MEC_REQUIRE(img && feat && logits && probs, "image: null pointer");
+  const bool fer = (H == 48 && W == 48 && C == 1);
+  MEC_REQUIRE(fer || (H == 224 && W == 224 && (C == 1 || C == 3)),
+              "image: input must be u8 [B,48,48,1] (GPU resize) or [B,224,224,{1,3}] (already resized)");
   const size_t per_img_big = (size_t)56 * 56 * 256;  // largest NHWC activation (elements)
   const size_t per_t1 = (size_t)56 * 56 * 128, per_t2 = (size_t)56 * 56 * 64;
   const size_t per_img = 224 * 224 + (3 * per_img_big + per_t1 + per_t2) * sizeof(f16) + 256 + 2048 * sizeof(float);
@@ -274,12 +289,17 @@ int ImageModel::forward(const uint8_t* gray, int B, float* feat, float* logits, 
 
   const f16* Wt = wts.as<f16>();
   const float* P = prm.as<float>();
-  MEC_TRY(resize_u8(gray, B, 48, 48, resized, 224, 224, s));
+  const uint8_t* stem_in = img;
+  if (fer) {
+    MEC_TRY(resize_u8(img, B, 48, 48, resized, 224, 224, s));
+    stem_in = resized;
+  }
   {  // stem conv 7x7/2 + BN + ReLU -> Y [B,112,112,64]
+    const ConvLayer& st = C == 3 ? stem_rgb : stem;
     GemmParams g;
-    g.amode = A_STEM; g.A = resized; g.B = Wt + stem.w_off; g.bias = P + stem.b_off; g.act = ACT_RELU;
-    g.C16 = Y; g.M = B * 112 * 112; g.N = 64; g.K = 128;
-    g.H = 224; g.W = 224; g.C = 1; g.OH = 112; g.OW = 112; g.ks = 7; g.stride = 2; g.pad = 3;
+    g.amode = A_STEM; g.A = stem_in; g.B = Wt + st.w_off; g.bias = P + st.b_off; g.act = ACT_RELU;
+    g.C16 = Y; g.M = B * 112 * 112; g.N = 64; g.K = 64 * (C + 1);
+    g.H = 224; g.W = 224; g.C = C; g.OH = 112; g.OW = 112; g.ks = 7; g.stride = 2; g.pad = 3;
     MEC_TRY(launch_gemm(g, s, &prof, TAG_RESNET_STEM));
   }
   {  // maxpool -> X [B,56,56,64]
@@ -290,7 +310,7 @@ int ImageModel::forward(const uint8_t* gray, int B, float* feat, float* logits, 
   }
   f16* cur = X;
   f16* other = Y;
-  int H = 56;
+  H = 56;
   for (const Bottleneck& bk : blocks) {
     const int wd = bk.c1.cout, cin = bk.c1.cin, st = bk.c2.stride;
     const int OH = (H + 2 - 3) / st + 1;

@@ -330,7 +330,8 @@ int FusionModel::forward(const float* sf, const float* tf, const float* imf, con
 }
 
 // =============================================================== weighted average
-__global__ void fuse_weighted_kernel(const float* s, const float* t, const float* i, int B, double* out) {
+template <class T>
+__global__ void fuse_weighted_kernel(const T* s, const T* t, const T* i, int B, double* out) {
   const int b = blockIdx.x * blockDim.x + threadIdx.x;
   if (b >= B) return;
   double w[7];
@@ -338,19 +339,28 @@ __global__ void fuse_weighted_kernel(const float* s, const float* t, const float
     const double vs = s ? (double)s[b * 7 + c] : 0.0;
     const double vt = t ? (double)t[b * 7 + c] : 0.0;
     const double vi = i ? (double)i[b * 7 + c] : 0.0;
-    w[c] = 0.3 * vs + 0.35 * vt + 0.35 * vi;
+    w[c] = 0.3 * vs + 0.35 * vt + 0.35 * vi;  // weights [0.3, 0.35, 0.35] (multimodal_fusion.py:23)
   }
   double sum = 0.0;
   for (int c = 0; c < 7; ++c) sum += w[c];
   for (int c = 0; c < 7; ++c) out[b * 7 + c] = sum > 0.0 ? w[c] / sum : w[c];
 }
 
-int fuse_weighted(const float* s, const float* t, const float* i, int B, double* out, hipStream_t st) {
+template <class T>
+static int fuse_weighted_t(const T* s, const T* t, const T* i, int B, double* out, hipStream_t st) {
   MEC_REQUIRE(B >= 0 && (B == 0 || out), "fuse_weighted: bad args");
   if (B == 0) return 0;
-  hipLaunchKernelGGL(fuse_weighted_kernel, dim3((B + 255) / 256), dim3(256), 0, st, s, t, i, B, out);
+  hipLaunchKernelGGL((fuse_weighted_kernel<T>), dim3((B + 255) / 256), dim3(256), 0, st, s, t, i, B, out);
   MEC_LAUNCH_CHECK();
   return 0;
+}
+
+int fuse_weighted(const float* s, const float* t, const float* i, int B, double* out, hipStream_t st) {
+  return fuse_weighted_t<float>(s, t, i, B, out, st);
+}
+
+int fuse_weighted_f64(const double* s, const double* t, const double* i, int B, double* out, hipStream_t st) {
+  return fuse_weighted_t<double>(s, t, i, B, out, st);
 }
 
 }  // namespace mec

@@ -25,8 +25,10 @@ SIGNATURES = {
     'mec_speech_fwd': (c_int, [c_vp, c_vp, c_int, c_vp, c_vp, c_vp, c_vp]),
     'mec_text_fwd': (c_int, [c_vp, c_vp, c_vp, c_int, c_int, c_vp, c_vp, c_vp, c_vp]),
     'mec_image_fwd': (c_int, [c_vp, c_vp, c_int, c_vp, c_vp, c_vp, c_vp]),
+    'mec_image_fwd_u8': (c_int, [c_vp, c_vp, c_int, c_int, c_int, c_int, c_vp, c_vp, c_vp, c_vp]),
     'mec_fusion_fwd': (c_int, [c_vp, c_vp, c_vp, c_vp, c_vp, c_vp, c_vp, c_int, c_vp, c_vp, c_vp, c_vp, c_vp]),
     'mec_fuse_weighted': (c_int, [c_vp, c_vp, c_vp, c_int, c_vp, c_vp]),
+    'mec_fuse_weighted_f64': (c_int, [c_vp, c_vp, c_vp, c_int, c_vp, c_vp]),
     'mec_resize_u8': (c_int, [c_vp, c_int, c_int, c_int, c_vp, c_int, c_int, c_vp]),
     'mec_gemm_f16': (c_int, [c_vp, c_vp, c_vp, c_vp, c_int, c_vp, c_vp, c_int, c_int, c_int, c_int, c_vp]),
     'mec_conv_f16': (c_int, [c_vp, c_vp, c_vp, c_vp, c_vp, c_int, c_int, c_int, c_int, c_int, c_int, c_int,

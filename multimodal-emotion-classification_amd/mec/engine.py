@@ -143,6 +143,20 @@ class ImageEncoder(HipModel):
                                               _stream(self.device)), 'mec_image_fwd')
         return feat, logits, probs
 
+    def forward_u8(self, img: torch.Tensor):
+        """img u8 [B,H,W,C] with (H,W,C) in {(48,48,1), (224,224,1), (224,224,3)}."""
+        if img.dim() == 3:
+            img = img.unsqueeze(-1)
+        if img.dim() != 4 or tuple(img.shape[1:]) not in ((48, 48, 1), (224, 224, 1), (224, 224, 3)):
+            raise ValueError(f'img: shape {tuple(img.shape)} not in [B,48,48,1] / [B,224,224,1] / [B,224,224,3]')
+        B, H, W, C = img.shape
+        _check_tensor('img', img, torch.uint8, (B, H, W, C), self.device)
+        feat, logits, probs = self._empty(B, 512), self._empty(B, 7), self._empty(B, 7)
+        with self._lock:
+            _lib.check(self.lib.mec_image_fwd_u8(self.handle, _ptr(img), B, H, W, C, _ptr(feat), _ptr(logits),
+                                                 _ptr(probs), _stream(self.device)), 'mec_image_fwd_u8')
+        return feat, logits, probs
+
 
 class FusionHead(HipModel):
     kind = 'fusion'
@@ -172,6 +186,21 @@ def fuse_weighted(s=None, t=None, i=None, device=None) -> torch.Tensor:
             _check_tensor(n, x, torch.float32, (B, 7), dev)
     out = torch.empty((B, 7), dtype=torch.float64, device=dev)
     _lib.check(lib.mec_fuse_weighted(_ptr(s), _ptr(t), _ptr(i), B, _ptr(out), _stream(dev)), 'mec_fuse_weighted')
+    return out
+
+
+def fuse_weighted_f64(s=None, t=None, i=None, device=None) -> torch.Tensor:
+    """Same as fuse_weighted with float64 [B,7] inputs (per-request Python floats)."""
+    present = [x for x in (s, t, i) if x is not None]
+    lib = _lib.load()
+    dev = present[0].device if present else require_gpu(device)
+    B = present[0].shape[0] if present else 1
+    for n, x in (('s', s), ('t', t), ('i', i)):
+        if x is not None:
+            _check_tensor(n, x, torch.float64, (B, 7), dev)
+    out = torch.empty((B, 7), dtype=torch.float64, device=dev)
+    _lib.check(lib.mec_fuse_weighted_f64(_ptr(s), _ptr(t), _ptr(i), B, _ptr(out), _stream(dev)),
+               'mec_fuse_weighted_f64')
     return out
 
 

@@ -42,15 +42,36 @@ def backbone(w, x: torch.Tensor) -> torch.Tensor:
     return torch.flatten(F.adaptive_avg_pool2d(x, 1), 1)
 
 
+def normalized_from_resized(resized_u8: np.ndarray) -> np.ndarray:
+    """u8 [B,224,224] (gray) or [B,224,224,3] (RGB), already PIL-resized -> ToTensor +
+    Normalize float32 [B,3,224,224] (image_inference.py:30-31)."""
+    a = np.asarray(resized_u8, np.uint8)
+    if a.ndim == 3:
+        return to_normalized_tensor(a)
+    mean = np.array([0.485, 0.456, 0.406], np.float32)
+    std = np.array([0.229, 0.224, 0.225], np.float32)
+    x = a.astype(np.float32).transpose(0, 3, 1, 2) / np.float32(255.0)
+    return ((x - mean[None, :, None, None]) / std[None, :, None, None]).astype(np.float32)
+
+
+@torch.no_grad()
+def head(w, pooled: torch.Tensor):
+    g = lambda n: torch.from_numpy(np.asarray(w[n], np.float32))
+    feat = F.relu(F.linear(pooled, g('base.fc.1.weight'), g('base.fc.1.bias')))
+    logits = F.linear(feat, g('base.fc.4.weight'), g('base.fc.4.bias'))
+    return feat.numpy().copy(), logits.numpy().copy(), torch.softmax(logits, dim=-1).numpy().copy()
+
+
+@torch.no_grad()
+def forward_resized(w, resized_u8: np.ndarray):
+    """Already-resized u8 image(s) -> (feat512, logits, probs)."""
+    return head(w, backbone(w, torch.from_numpy(normalized_from_resized(resized_u8))))
+
+
 @torch.no_grad()
 def forward(w, gray_u8: np.ndarray, return_resized: bool = False):
     """gray u8 [B,48,48] -> (feat512 [B,512], logits [B,7], probs [B,7]) float32 numpy."""
     resized = resize_bilinear_u8(gray_u8)
     x = torch.from_numpy(to_normalized_tensor(resized))
-    pooled = backbone(w, x)
-    g = lambda n: torch.from_numpy(np.asarray(w[n], np.float32))
-    feat = F.relu(F.linear(pooled, g('base.fc.1.weight'), g('base.fc.1.bias')))
-    logits = F.linear(feat, g('base.fc.4.weight'), g('base.fc.4.bias'))
-    probs = torch.softmax(logits, dim=-1)
-    out = (feat.numpy().copy(), logits.numpy().copy(), probs.numpy().copy())
+    out = head(w, backbone(w, x))
     return out + (resized,) if return_resized else out

