@@ -101,6 +101,9 @@ int mec_conv_f16(const void* x, const void* w, const float* bias, const void* R,
  * "gemm_autotune" 0|1 (time each GEMM tile width on the first launch of a shape; default 1). */
 int mec_set_option(const char* key, int value);
 
+/* Tile width the autotuner chose for a plain (amode 0) or conv (amode 1) GEMM shape; 0 = not yet seen. */
+int mec_gemm_query(int amode, int M, int N, int K);
+
 /* hipEvent timing hook: time every launch of kernel class `tag`. */
 int mec_prof_enable(mec_model* m, int tag);
 int mec_prof_read(mec_model* m, double* total_ms, int* count);

@@ -212,6 +212,8 @@ int mec_set_option(const char* key, int value) {
   return -1;
 }
 
+int mec_gemm_query(int amode, int M, int N, int K) { return gemm_tuned_bn(amode, M, N, K); }
+
 int mec_prof_enable(mec_model* m, int tag) {
   if (!m || !m->impl) { set_error("null model handle"); return -1; }
   m->impl->prof.tag = tag;

@@ -325,6 +325,13 @@ static int tune_bn(const GemmParams& p, hipStream_t s, int* out_bn) {
   return 0;
 }
 
+int gemm_tuned_bn(int amode, int M, int N, int K) {
+  std::lock_guard<std::mutex> lk(g_tuned_mu);
+  for (const auto& kv : g_tuned)
+    if (kv.first.amode == amode && kv.first.M == M && kv.first.N == N && kv.first.K == K) return kv.second;
+  return 0;
+}
+
 int launch_gemm_glds(const GemmParams& p, hipStream_t s, int force_bn) {
   if (force_bn) return launch_bn(p, s, force_bn);
   const GemmKey key{p.amode, p.M, p.N, p.K, p.H, p.W, p.C, p.ks, p.stride, p.pad};

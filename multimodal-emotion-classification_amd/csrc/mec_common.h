@@ -121,5 +121,6 @@ int launch_gemm_glds(const GemmParams& p, hipStream_t s, int force_bn);
 extern int g_gemm_impl;
 extern int g_gemm_bn;
 extern int g_gemm_autotune;
+int gemm_tuned_bn(int amode, int M, int N, int K);
 
 }  // namespace mec

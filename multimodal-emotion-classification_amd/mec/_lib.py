@@ -34,6 +34,7 @@ SIGNATURES = {
     'mec_conv_f16': (c_int, [c_vp, c_vp, c_vp, c_vp, c_vp, c_int, c_int, c_int, c_int, c_int, c_int, c_int,
                              c_int, c_int, c_vp]),
     'mec_set_option': (c_int, [ctypes.c_char_p, c_int]),
+    'mec_gemm_query': (c_int, [c_int, c_int, c_int, c_int]),
     'mec_prof_enable': (c_int, [c_vp, c_int]),
     'mec_prof_read': (c_int, [c_vp, c_dp, ctypes.POINTER(c_int)]),
 }
