@@ -206,8 +206,12 @@ int mec_conv_f16(const void* x, const void* w, const float* bias, const void* R,
 int mec_set_option(const char* key, int value) {
   const std::string k = key ? key : "";
   if (k == "gemm_impl" && (value == 1 || value == 2)) { g_gemm_impl = value; return 0; }
+  if (k == "gemm_debug" && value >= 0 && value <= 2) { g_gemm_debug = value; return 0; }
   if (k == "gemm_autotune" && (value == 0 || value == 1)) { g_gemm_autotune = value; return 0; }
-  if (k == "gemm_bn" && (value == 0 || value == 64 || value == 128 || value == 256)) { g_gemm_bn = value; return 0; }
+  if (k == "gemm_bn" && (value == 0 || value == 64 || value == 128 || value == 256 || value == 1064 || value == 1128)) {
+    g_gemm_bn = value;
+    return 0;
+  }
   set_error("mec_set_option: unknown key or bad value: " + k);
   return -1;
 }

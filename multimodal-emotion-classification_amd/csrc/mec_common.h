@@ -121,6 +121,7 @@ int launch_gemm_glds(const GemmParams& p, hipStream_t s, int force_bn);
 extern int g_gemm_impl;
 extern int g_gemm_bn;
 extern int g_gemm_autotune;
+extern int g_gemm_debug;
 int gemm_tuned_bn(int amode, int M, int N, int K);
 
 }  // namespace mec

@@ -48,6 +48,7 @@ def main():
     ap.add_argument('--bn', type=int, nargs='+', default=[0])
     ap.add_argument('--iters', type=int, default=20)
     ap.add_argument('--only', nargs='*')
+    ap.add_argument('--debug', type=int, nargs='+', default=[0])
     a = ap.parse_args()
     lib = _lib.load()
     dev = torch.device('cuda', 0)
@@ -84,8 +85,9 @@ def main():
             def run():
                 _lib.check(lib.mec_conv_f16(p(x), p(w), p(bias), None, p(y), n, H, H, C, Co, ks, s, pd, 1, st), name)
             ref = None
-        for impl in a.impl:
-            for bn in (a.bn if impl == 2 else [0]):
+        for impl, bn, dbg in [(i, b, d) for i in a.impl for b in (a.bn if i == 2 else [0]) for d in a.debug]:
+            if True:
+                lib.mec_set_option(b'gemm_debug', dbg)
                 lib.mec_set_option(b'gemm_impl', impl)
                 lib.mec_set_option(b'gemm_bn', bn)
                 try:
@@ -101,8 +103,8 @@ def main():
                 e1.record()
                 torch.cuda.synchronize()
                 ms = e0.elapsed_time(e1) / a.iters
-                r = {'shape': name, 'impl': impl, 'bn': bn, 'us': round(ms * 1e3, 1), 'tflops': round(flop / ms / 1e9, 1)}
-                if ref is not None:
+                r = {'shape': name, 'impl': impl, 'bn': bn, 'dbg': dbg, 'us': round(ms * 1e3, 1), 'tflops': round(flop / ms / 1e9, 1)}
+                if ref is not None and dbg == 0:
                     rr = ref()
                     if act == 1:
                         rr = torch.relu(rr + (R[:512].float() if R is not None else 0))
@@ -114,6 +116,7 @@ def main():
                 res.append(r)
                 print(json.dumps(r), flush=True)
     lib.mec_set_option(b'gemm_impl', 2)
+    lib.mec_set_option(b'gemm_debug', 0)
     lib.mec_set_option(b'gemm_bn', 0)
 
 

@@ -1,21 +1,36 @@
-"""Summarise a rocprofv3 rocpd database (or kernel_stats.csv) into a per-kernel table.
-usage: python tools/prof_summary.py gpurun_out/prof/run_results.db [--steps N]"""
+"""Summarise a rocprofv3 rocpd database into per-kernel tables.
+usage: python tools/prof_summary.py DB [--by-grid] [--skip-first-steps N --launches-per-step L]
+--by-grid splits a kernel name by launch grid (tells GEMM shapes apart)."""
+import argparse
 import sqlite3
-import sys
 
 
-def main(path, steps=None):
-    c = sqlite3.connect(path)
-    cols = [r[1] for r in c.execute("pragma table_info(kernels)")]
-    name_col = 'kernel_name' if 'kernel_name' in cols else 'name'
-    rows = c.execute(f"select {name_col}, count(*), sum(end-start), avg(end-start), min(end-start), max(end-start) "
-                     f"from kernels group by {name_col} order by sum(end-start) desc").fetchall()
-    tot = sum(r[2] for r in rows)
-    print(f"{'kernel':90s} {'calls':>6s} {'total_ms':>10s} {'avg_us':>9s} {'min_us':>9s} {'max_us':>9s} {'pct':>6s}")
-    for n, cnt, s, a, mn, mx in rows:
-        print(f"{n[:90]:90s} {cnt:6d} {s/1e6:10.3f} {a/1e3:9.1f} {mn/1e3:9.1f} {mx/1e3:9.1f} {100*s/tot:6.2f}")
-    print(f"total kernel time {tot/1e6:.3f} ms")
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument('db')
+    ap.add_argument('--by-grid', action='store_true')
+    ap.add_argument('--match', default=None, help='substring filter on the kernel name')
+    a = ap.parse_args()
+    c = sqlite3.connect(a.db)
+    q = "select name, grid_x, workgroup_x, end-start from kernels order by start"
+    rows = c.execute(q).fetchall()
+    agg = {}
+    for name, gx, wx, d in rows:
+        if a.match and a.match not in name:
+            continue
+        key = (name, gx // max(wx, 1)) if a.by_grid else (name, None)
+        s = agg.setdefault(key, [0, 0, 1e18, 0])
+        s[0] += 1
+        s[1] += d
+        s[2] = min(s[2], d)
+        s[3] = max(s[3], d)
+    tot = sum(v[1] for v in agg.values())
+    print(f"{'kernel':88s} {'blocks':>7s} {'calls':>6s} {'total_ms':>10s} {'avg_us':>9s} {'min_us':>9s} {'max_us':>9s} {'pct':>6s}")
+    for (n, g), (cnt, s, mn, mx) in sorted(agg.items(), key=lambda kv: -kv[1][1]):
+        gs = '' if g is None else str(g)
+        print(f"{n[:88]:88s} {gs:>7s} {cnt:6d} {s/1e6:10.3f} {s/cnt/1e3:9.1f} {mn/1e3:9.1f} {mx/1e3:9.1f} {100*s/tot:6.2f}")
+    print(f"total kernel time {tot/1e6:.3f} ms over {sum(v[0] for v in agg.values())} dispatches")
 
 
 if __name__ == '__main__':
-    main(sys.argv[1])
+    main()
