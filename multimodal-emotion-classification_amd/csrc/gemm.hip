@@ -1,13 +1,10 @@
-// fp16-operand / fp32-accumulate MFMA GEMM for gfx950, with three A-operand views:
+// fp16-operand / fp32-accumulate MFMA GEMM for gfx950 — the first, register-staged engine
+// (128x128 tiles), kept selectable (mec_set_option("gemm_impl", 1)) as the A/B baseline of
+// gemm_glds.hip, which is the default. Two A-operand views:
 //   A_PLAIN  A[M,K] row-major (BERT projections/FFN, ResNet 1x1 stride-1 convs)
 //   A_CONV   implicit im2col of an NHWC f16 tensor (ResNet 3x3 convs, strided 1x1
 //            downsample convs); K ordered (kh, kw, c), C % 64 == 0 so a 64-deep K tile
 //            never straddles two filter taps
-//   A_STEM   the ResNet stem on a u8 224x224 image with C = 1 (gray, RGB-replicated) or 3
-//            channels: K = 64*(C+1) = per channel 49 pixel taps | 15 zeros, then 49
-//            "tap in bounds" flags | 15 zeros. The RGB-replicate + ToTensor + Normalize
-//            of inference/image_inference.py:28-32 is folded into the stem weights (the
-//            flag half carries the -mean/std term, so zero padding stays exact).
 // B is the weight matrix [N,K] (K contiguous = torch Linear layout). Epilogue fuses
 // bias (folded BN shift), residual add, ReLU/GELU(erf), f16 and/or f32 stores.
 //
@@ -105,26 +102,6 @@ __global__ __launch_bounds__(256, 2) void gemm_f16_kernel(const GemmParams p) {
         uint4 v = *reinterpret_cast<const uint4*>(src);
         ra[i] = ok ? v : make_uint4(0, 0, 0, 0);
       }
-    } else {  // A_STEM: u8 image, 7x7 taps
-      const uint8_t* X = reinterpret_cast<const uint8_t*>(p.A);
-#pragma unroll
-      for (int i = 0; i < AI; ++i) {
-        half8 h;
-#pragma unroll
-        for (int e = 0; e < 8; ++e) {
-          const int t = kc * 8 + e;
-          float val = 0.f;
-          if (t < 49) {
-            const int kh = t / 7, kw = t - (t / 7) * 7;
-            const int ih = a_ih0[i] + kh, iw = a_iw0[i] + kw;
-            const bool ok = a_in[i] && ih >= 0 && ih < p.H && iw >= 0 && iw < p.W;
-            if (kt < p.C) val = ok ? (float)X[a_img[i] + ((size_t)ih * p.W + iw) * p.C + kt] : 0.f;
-            else val = ok ? 1.f : 0.f;  // "tap in bounds" flag (carries the -mean/std term)
-          }
-          h[e] = (f16)val;
-        }
-        ra[i] = *reinterpret_cast<uint4*>(&h);
-      }
     }
 #pragma unroll
     for (int j = 0; j < BI; ++j) rb[j] = *reinterpret_cast<const uint4*>(b_src[j] + k0);
@@ -220,7 +197,6 @@ static int launch_mode(const GemmParams& p, hipStream_t s) {
   switch (p.amode) {
     case A_PLAIN: hipLaunchKernelGGL((gemm_f16_kernel<BM, BN, A_PLAIN>), grid, block, 0, s, p); break;
     case A_CONV: hipLaunchKernelGGL((gemm_f16_kernel<BM, BN, A_CONV>), grid, block, 0, s, p); break;
-    case A_STEM: hipLaunchKernelGGL((gemm_f16_kernel<BM, BN, A_STEM>), grid, block, 0, s, p); break;
     default: set_error("bad amode"); return -1;
   }
   MEC_LAUNCH_CHECK();
@@ -238,13 +214,12 @@ int launch_gemm(const GemmParams& p, hipStream_t s, Prof* prof, int tag) {
   MEC_REQUIRE(p.C16 || p.C32, "gemm: no output");
   if (p.amode == A_CONV) {
     MEC_REQUIRE(p.C % 64 == 0 && p.K == p.ks * p.ks * p.C, "conv: C % 64 != 0 or K != ks*ks*C");
-  } else if (p.amode == A_STEM) {
-    MEC_REQUIRE((p.C == 1 || p.C == 3) && p.K == 64 * (p.C + 1) && p.ks == 7,
-                "stem: K must be 64*(C+1) (49 taps per channel + 49 flags, each padded to 64)");
+  } else {
+    MEC_REQUIRE(p.amode == A_PLAIN, "gemm: unknown A mode");
   }
   if (prof) MEC_TRY(prof->begin(tag, s));
   int rc;
-  if (p.amode != A_STEM && g_gemm_impl == 2)
+  if (g_gemm_impl == 2)
     rc = launch_gemm_glds(p, s, g_gemm_bn);
   else
     rc = (p.N % 128 == 0) ? launch_mode<128, 128>(p, s) : launch_mode<128, 64>(p, s);

@@ -15,6 +15,7 @@
 //   them back row-contiguous: bias, residual (f16/f32), ReLU/GELU, f16 and/or f32 out
 //   with 16-byte loads/stores.
 // * XCD-aware bijective block remap: blocks that share an A panel share an L2.
+#include <algorithm>
 #include <map>
 #include <mutex>
 
@@ -360,25 +361,27 @@ static int heuristic_bn(const GemmParams& p) {
 }
 
 static int tune_bn(const GemmParams& p, hipStream_t s, int* out_bn) {
+  constexpr int REPS = 5;
   const int cands[5] = {64, 128, 256, 1128, 1064};
-  hipEvent_t e0, e1;
-  MEC_HIP(hipEventCreate(&e0));
-  MEC_HIP(hipEventCreate(&e1));
+  hipEvent_t ev[REPS + 1];
+  for (auto& e : ev) MEC_HIP(hipEventCreate(&e));
   float best = 1e30f;
   int best_bn = heuristic_bn(p);
   for (int bn : cands) {
     if (p.N % tile_bn(bn)) continue;
     MEC_TRY(launch_bn(p, s, bn));  // warm
-    MEC_HIP(hipEventRecord(e0, s));
-    for (int r = 0; r < 2; ++r) MEC_TRY(launch_bn(p, s, bn));
-    MEC_HIP(hipEventRecord(e1, s));
-    MEC_HIP(hipEventSynchronize(e1));
-    float ms = 0.f;
-    MEC_HIP(hipEventElapsedTime(&ms, e0, e1));
-    if (ms < best) { best = ms; best_bn = bn; }
+    MEC_HIP(hipEventRecord(ev[0], s));
+    for (int r = 0; r < REPS; ++r) {
+      MEC_TRY(launch_bn(p, s, bn));
+      MEC_HIP(hipEventRecord(ev[r + 1], s));
+    }
+    MEC_HIP(hipEventSynchronize(ev[REPS]));
+    float t[REPS];
+    for (int r = 0; r < REPS; ++r) MEC_HIP(hipEventElapsedTime(&t[r], ev[r], ev[r + 1]));
+    std::sort(t, t + REPS);
+    if (t[REPS / 2] < best) { best = t[REPS / 2]; best_bn = bn; }  // median launch
   }
-  (void)hipEventDestroy(e0);
-  (void)hipEventDestroy(e1);
+  for (auto& e : ev) (void)hipEventDestroy(e);
   *out_bn = best_bn;
   return 0;
 }

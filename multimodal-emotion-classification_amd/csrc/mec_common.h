@@ -97,12 +97,12 @@ struct BlobReader {
 
 // fp16 MFMA GEMM / implicit-GEMM convolution ------------------------------------------
 // C[M,N] = epilogue( A'[M,K] . B[N,K]^T ), A' = A (plain) or the im2col view of an NHWC
-// tensor (conv), or the folded single-channel stem view of a u8 image (stem).
-enum AMode : int { A_PLAIN = 0, A_CONV = 1, A_STEM = 2 };
+// tensor (conv).
+enum AMode : int { A_PLAIN = 0, A_CONV = 1 };
 enum Act : int { ACT_NONE = 0, ACT_RELU = 1, ACT_GELU = 2 };
 
 struct GemmParams {
-  const void* A = nullptr;   // f16 [M,K] | f16 NHWC [n,H,W,C] | u8 [n,H,W]
+  const void* A = nullptr;   // f16 [M,K] | f16 NHWC [n,H,W,C]
   const f16* B = nullptr;    // f16 [N,K], K contiguous
   const float* bias = nullptr;  // [N]
   const void* R = nullptr;      // residual [M,N] (f16 or f32) or null
@@ -112,7 +112,7 @@ struct GemmParams {
   int M = 0, N = 0, K = 0;
   int act = ACT_NONE;
   int amode = A_PLAIN;
-  // conv / stem geometry (NHWC input)
+  // conv geometry (NHWC input)
   int H = 1, W = 1, C = 0, OH = 1, OW = 1, ks = 1, stride = 1, pad = 0;
 };
 

@@ -65,8 +65,9 @@ struct ImageModel : Model {
   DevBuf prm;   // fp32 biases, stem weights, head
   DevBuf ws;    // workspace
   int ws_batch = 0;
-  ConvLayer stem;      // gray input (channels folded): K = 128
-  ConvLayer stem_rgb;  // RGB input: K = 256
+  ConvLayer stem;      // gray input (channels folded): f16 [64][64] pixel taps
+  ConvLayer stem_rgb;  // RGB input: f16 [64][3*64]
+  size_t stem_corr_off = 0;  // f32 [16 border classes][64] -mean/std term
   std::vector<Bottleneck> blocks;
   size_t fc1_off = 0, fc1b_off = 0, fc2_off = 0, fc2b_off = 0;
   int create(const float* blob, size_t n);

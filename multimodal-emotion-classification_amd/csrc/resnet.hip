@@ -103,38 +103,163 @@ int resize_u8(const uint8_t* in, int B, int H, int W, uint8_t* out, int OH, int 
   return 0;
 }
 
-// ----------------------------------------------------------------------------- maxpool
-// 3x3 / stride 2 / pad 1 on NHWC f16 (torch max_pool2d pads with -inf).
-__global__ __launch_bounds__(256) void maxpool3s2_kernel(const f16* __restrict__ x, f16* __restrict__ y, int B,
-                                                         int H, int W, int C, int OH, int OW) {
-  const int c8 = C / 8;
-  const size_t total = (size_t)B * OH * OW * c8;
-  const size_t i = (size_t)blockIdx.x * 256 + threadIdx.x;
-  if (i >= total) return;
-  const int cc = (int)(i % c8);
-  size_t r = i / c8;
-  const int ow = (int)(r % OW); r /= OW;
-  const int oh = (int)(r % OH);
-  const int n = (int)(r / OH);
-  float m[8];
+// ----------------------------------------------------------------------------- stem + maxpool
+// Fused conv7x7/2 + BN + ReLU (MFMA) + maxpool3x3/2 on the u8 224x224 image.
+// One workgroup = an 8x8 tile of pooled outputs = a 17x17 region of stem outputs (with the
+// pool's halo). The u8 39x39 input patch is converted once to f16 in LDS; each thread then
+// gathers a whole im2col row (49 taps at compile-time offsets from the row's patch base)
+// into a swizzled [320 x 64] f16 tile per channel, and the 7x7 conv runs on MFMA.
+// ToTensor/Normalize is folded into the weights; the -mean/std term summed over the
+// in-image taps depends only on the border class of the stem pixel (rows/cols 0, 1, 111
+// have out-of-image taps), so it is a [16 classes][64] table added in the epilogue.
+// Stem pixels outside the 112x112 image become 0: outputs are post-ReLU (>= 0) and every
+// pool window holds a valid pixel, so this equals torch's -inf padding. Pooling f16 values
+// is exact (max commutes with monotone rounding).
+constexpr int SP_T = 8;              // pooled tile
+constexpr int SP_S = 2 * SP_T + 1;   // 17 stem rows/cols
+constexpr int SP_M = 320;            // 289 padded to 10 x 32
+constexpr int SP_P = 4 * SP_T + 7;   // 39 patch rows/cols
+constexpr int SO_LD = 72;            // stem-output row (f16), padded: 144 B
+
+__device__ __forceinline__ int sp_swz(int row, int kc) { return kc ^ ((row >> 1) & 7); }
+
+// border class of a stem coordinate: 0 -> 0, 1 -> 1, 111 -> 3, else 2 (interior)
+__device__ __forceinline__ int sp_cls(int o) { return o == 0 ? 0 : (o == 1 ? 1 : (o == 111 ? 3 : 2)); }
+
+__global__ __launch_bounds__(256) void stem_pool_kernel(const uint8_t* __restrict__ img, int C,
+                                                        const f16* __restrict__ Wst, const float* __restrict__ bias,
+                                                        const float* __restrict__ corr, f16* __restrict__ out) {
+  __shared__ __attribute__((aligned(16))) f16 sA[SP_M * SO_LD];  // im2col tile, later stem outputs
+  __shared__ __attribute__((aligned(16))) f16 sB[64 * 64];
+  __shared__ f16 sP[3 * SP_P * SP_P + 64];
+  __shared__ float sCorr[16 * 64];
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int b = blockIdx.x / 49, t = blockIdx.x - b * 49;
+  const int ph0 = (t / 7) * SP_T, pw0 = (t - (t / 7) * 7) * SP_T;
+  const int sr0 = 2 * ph0 - 1, sc0 = 2 * pw0 - 1;       // first stem row/col of the region
+  const int ir0 = 2 * sr0 - 3, ic0 = 2 * sc0 - 3;       // first image row/col of the patch
+  const uint8_t* im = img + (size_t)b * 224 * 224 * C;
+  {  // issue every prologue load before any use: patch bytes, border-class table
+    constexpr int PER = (3 * SP_P * SP_P + 255) / 256;  // 18
+    uint32_t px[PER];
 #pragma unroll
-  for (int e = 0; e < 8; ++e) m[e] = -INFINITY;
-  for (int kh = 0; kh < 3; ++kh) {
-    const int ih = oh * 2 - 1 + kh;
-    if (ih < 0 || ih >= H) continue;
-    for (int kw = 0; kw < 3; ++kw) {
-      const int iw = ow * 2 - 1 + kw;
-      if (iw < 0 || iw >= W) continue;
-      const uint4 v = *reinterpret_cast<const uint4*>(x + (((size_t)n * H + ih) * W + iw) * C + cc * 8);
-      const f16* hv = reinterpret_cast<const f16*>(&v);
+    for (int j = 0; j < PER; ++j) {
+      const int i = tid + 256 * j;
+      px[j] = 0;
+      if (i < C * SP_P * SP_P) {
+        const int c = i / (SP_P * SP_P), rem = i - c * SP_P * SP_P;
+        const int pr = rem / SP_P, pc = rem - (rem / SP_P) * SP_P;
+        const int y = ir0 + pr, x = ic0 + pc;
+        if (y >= 0 && y < 224 && x >= 0 && x < 224) px[j] = im[((size_t)y * 224 + x) * C + c];
+      }
+    }
+    float cr[4];
 #pragma unroll
-      for (int e = 0; e < 8; ++e) m[e] = fmaxf(m[e], (float)hv[e]);
+    for (int j = 0; j < 4; ++j) cr[j] = corr[tid + 256 * j];
+#pragma unroll
+    for (int j = 0; j < PER; ++j) {
+      const int i = tid + 256 * j;
+      if (i < C * SP_P * SP_P) sP[i] = (f16)(float)px[j];
+    }
+#pragma unroll
+    for (int j = 0; j < 4; ++j) sCorr[tid + 256 * j] = cr[j];
+  }
+  const int lr = lane & 31, lh = lane >> 5;
+  const int jt = wave & 1;          // N tile (32 of the 64 channels)
+  const int it0 = wave >> 1;        // row tiles it0, it0+2, ..., it0+8
+  floatx16 acc[5];
+#pragma unroll
+  for (int q = 0; q < 5; ++q)
+#pragma unroll
+    for (int e = 0; e < 16; ++e) acc[q][e] = 0.f;
+  for (int ch = 0; ch < C; ++ch) {
+    __syncthreads();  // patch ready / previous chunk consumed
+    for (int i = tid; i < 64 * 8; i += 256) {  // weights (channel ch) -> sB, swizzled rows
+      const int n = i >> 3, kc = i & 7;
+      *reinterpret_cast<uint4*>(sB + n * 64 + sp_swz(n, kc) * 8) =
+          *reinterpret_cast<const uint4*>(Wst + (size_t)n * 64 * C + ch * 64 + kc * 8);
+    }
+    for (int m = tid; m < SP_M; m += 256) {  // one im2col row per thread
+      const int lrow = m / SP_S, lcol = m - (m / SP_S) * SP_S;
+      const bool valid = m < SP_S * SP_S;
+      const f16* src = sP + ch * SP_P * SP_P + (2 * lrow) * SP_P + 2 * lcol;
+#pragma unroll
+      for (int kc = 0; kc < 8; ++kc) {
+        half8 h;
+#pragma unroll
+        for (int e = 0; e < 8; ++e) {
+          const int k = kc * 8 + e;  // compile-time tap -> patch offset kh*39 + kw
+          h[e] = (k < 49 && valid) ? src[(k / 7) * SP_P + (k % 7)] : (f16)0.f;
+        }
+        *reinterpret_cast<half8*>(sA + m * 64 + sp_swz(m, kc) * 8) = h;
+      }
+    }
+    __syncthreads();
+#pragma unroll
+    for (int s = 0; s < 4; ++s) {
+      const int kcs = 2 * s + lh;
+      const int rb = 32 * jt + lr;
+      const half8 bf = *reinterpret_cast<const half8*>(sB + rb * 64 + sp_swz(rb, kcs) * 8);
+#pragma unroll
+      for (int q = 0; q < 5; ++q) {
+        const int ra = 32 * (it0 + 2 * q) + lr;
+        const half8 af = *reinterpret_cast<const half8*>(sA + ra * 64 + sp_swz(ra, kcs) * 8);
+        acc[q] = __builtin_amdgcn_mfma_f32_32x32x16_f16(af, bf, acc[q], 0, 0, 0);
+      }
     }
   }
-  half8 o;
+  __syncthreads();  // all MFMA reads of sA done before it is reused for stem outputs
+  {  // raw conv + (bias + interior correction) -> sO [m][SO_LD] f16 (padded rows: no conflicts)
+    const int col = 32 * jt + lr;
+    const float bv = bias[col] + sCorr[(2 * 4 + 2) * 64 + col];
+    f16* sO = sA;
 #pragma unroll
-  for (int e = 0; e < 8; ++e) o[e] = (f16)m[e];
-  *reinterpret_cast<half8*>(y + (((size_t)n * OH + oh) * OW + ow) * C + cc * 8) = o;
+    for (int q = 0; q < 5; ++q)
+#pragma unroll
+      for (int e = 0; e < 16; ++e) {
+        const int m = 32 * (it0 + 2 * q) + (e & 3) + 8 * (e >> 2) + 4 * lh;
+        sO[m * SO_LD + col] = (f16)(acc[q][e] + bv);
+      }
+  }
+  __syncthreads();
+  {  // ReLU + border correction + 3x3/2 max; thread -> (pooled pixel, 16 channels)
+    const f16* sO = sA;
+    const int px = tid >> 2, c0 = (tid & 3) * 16;
+    const int py = px >> 3, pxx = px & 7;
+    const bool border = ph0 == 0 || pw0 == 0 || ph0 + SP_T == 56 || pw0 + SP_T == 56;
+    float m[16];
+#pragma unroll
+    for (int c = 0; c < 16; ++c) m[c] = 0.f;  // post-ReLU values are >= 0
+#pragma unroll
+    for (int dy = 0; dy < 3; ++dy)
+#pragma unroll
+      for (int dx = 0; dx < 3; ++dx) {
+        const int oh = sr0 + 2 * py + dy, ow = sc0 + 2 * pxx + dx;
+        const int mm = (2 * py + dy) * SP_S + 2 * pxx + dx;
+        const half8 a0 = *reinterpret_cast<const half8*>(sO + mm * SO_LD + c0);
+        const half8 a1 = *reinterpret_cast<const half8*>(sO + mm * SO_LD + c0 + 8);
+        float v[16];
+#pragma unroll
+        for (int c = 0; c < 8; ++c) { v[c] = (float)a0[c]; v[8 + c] = (float)a1[c]; }
+        if (border) {
+          const bool ok = oh >= 0 && oh < 112 && ow >= 0 && ow < 112;
+          const int cls = sp_cls(oh) * 4 + sp_cls(ow);
+#pragma unroll
+          for (int c = 0; c < 16; ++c) {
+            const float d = sCorr[cls * 64 + c0 + c] - sCorr[(2 * 4 + 2) * 64 + c0 + c];
+            v[c] = ok ? v[c] + d : 0.f;
+          }
+        }
+#pragma unroll
+        for (int c = 0; c < 16; ++c) m[c] = fmaxf(m[c], v[c]);
+      }
+    half8 o0, o1;
+#pragma unroll
+    for (int c = 0; c < 8; ++c) { o0[c] = (f16)m[c]; o1[c] = (f16)m[8 + c]; }
+    f16* o = out + (((size_t)b * 56 + ph0 + py) * 56 + pw0 + pxx) * 64 + c0;
+    *reinterpret_cast<half8*>(o) = o0;
+    *reinterpret_cast<half8*>(o + 8) = o1;
+  }
 }
 
 // ----------------------------------------------------------------------------- avgpool
@@ -186,8 +311,9 @@ int ImageModel::create(const float* blob, size_t n) {
                 (f16)((double)src[(((size_t)o * cin + c) * ks + kh) * ks + kw] * scale[o]);
     return L;
   };
-  // stem: fold ToTensor(/255) + Normalize + BN scale into the K rows (see gemm.hip A_STEM):
-  // gray input folds the three replicated channels into one (K=128); RGB keeps them (K=256).
+  // stem (stem_pool_kernel): ToTensor(/255) + Normalize + BN scale folded into per-channel
+  // pixel weights (gray: the three replicated channels summed into one); the -mean/std
+  // term summed over in-image taps goes to a [16 border classes][64] table.
   {
     const float* src = rd.take((size_t)64 * 3 * 49);
     std::vector<float> scale;
@@ -196,25 +322,40 @@ int ImageModel::create(const float* blob, size_t n) {
     stem_rgb = stem;
     stem_rgb.cin = 3;
     stem.w_off = w.size();
-    w.resize(w.size() + 64 * 128, (f16)0.f);
+    w.resize(w.size() + 64 * 64, (f16)0.f);
     stem_rgb.w_off = w.size();
-    w.resize(w.size() + 64 * 256, (f16)0.f);
+    w.resize(w.size() + 64 * 192, (f16)0.f);
+    stem_corr_off = pr.size();
+    pr.resize(pr.size() + 16 * 64, 0.f);
     const double mean[3] = {0.485, 0.456, 0.406}, stdv[3] = {0.229, 0.224, 0.225};
     if (rd.ok) {
+      std::vector<double> c0(64 * 49);
       for (int o = 0; o < 64; ++o)
         for (int t = 0; t < 49; ++t) {
-          double a = 0.0, c0 = 0.0;
+          double a = 0.0, cc = 0.0;
           for (int c = 0; c < 3; ++c) {
             const double wv = src[((size_t)o * 3 + c) * 49 + t];
             const double mf = (double)(float)mean[c], sf = (double)(float)stdv[c];
             a += wv / (255.0 * sf);
-            c0 -= wv * mf / sf;
-            w[stem_rgb.w_off + (size_t)o * 256 + 64 * c + t] = (f16)(wv / (255.0 * sf) * scale[o]);
+            cc -= wv * mf / sf;
+            w[stem_rgb.w_off + (size_t)o * 192 + 64 * c + t] = (f16)(wv / (255.0 * sf) * scale[o]);
           }
-          w[stem.w_off + (size_t)o * 128 + t] = (f16)(a * scale[o]);
-          w[stem.w_off + (size_t)o * 128 + 64 + t] = (f16)(c0 * scale[o]);
-          w[stem_rgb.w_off + (size_t)o * 256 + 192 + t] = (f16)(c0 * scale[o]);
+          w[stem.w_off + (size_t)o * 64 + t] = (f16)(a * scale[o]);
+          c0[o * 49 + t] = cc * scale[o];
         }
+      // border classes of a stem coordinate: 0, 1, interior, 111 (see sp_cls)
+      const int rep[4] = {0, 1, 50, 111};
+      for (int rc = 0; rc < 4; ++rc)
+        for (int cc = 0; cc < 4; ++cc)
+          for (int o = 0; o < 64; ++o) {
+            double sum = 0.0;
+            for (int kh = 0; kh < 7; ++kh)
+              for (int kw = 0; kw < 7; ++kw) {
+                const int ih = 2 * rep[rc] - 3 + kh, iw = 2 * rep[cc] - 3 + kw;
+                if (ih >= 0 && ih < 224 && iw >= 0 && iw < 224) sum += c0[o * 49 + kh * 7 + kw];
+              }
+            pr[stem_corr_off + (rc * 4 + cc) * 64 + o] = (float)sum;
+          }
     }
   }
   blocks.clear();
@@ -294,19 +435,13 @@ int ImageModel::forward_u8(const uint8_t* img, int B, int H, int W, int C, float
     MEC_TRY(resize_u8(img, B, 48, 48, resized, 224, 224, s));
     stem_in = resized;
   }
-  {  // stem conv 7x7/2 + BN + ReLU -> Y [B,112,112,64]
+  {  // fused stem conv 7x7/2 + BN + ReLU + maxpool 3x3/2 -> X [B,56,56,64]
     const ConvLayer& st = C == 3 ? stem_rgb : stem;
-    GemmParams g;
-    g.amode = A_STEM; g.A = stem_in; g.B = Wt + st.w_off; g.bias = P + st.b_off; g.act = ACT_RELU;
-    g.C16 = Y; g.M = B * 112 * 112; g.N = 64; g.K = 64 * (C + 1);
-    g.H = 224; g.W = 224; g.C = C; g.OH = 112; g.OW = 112; g.ks = 7; g.stride = 2; g.pad = 3;
-    MEC_TRY(launch_gemm(g, s, &prof, TAG_RESNET_STEM));
-  }
-  {  // maxpool -> X [B,56,56,64]
-    const size_t total = (size_t)B * 56 * 56 * 8;
-    hipLaunchKernelGGL(maxpool3s2_kernel, dim3((unsigned)((total + 255) / 256)), dim3(256), 0, s, Y, X, B, 112, 112,
-                       64, 56, 56);
+    MEC_TRY(prof.begin(TAG_RESNET_STEM, s));
+    hipLaunchKernelGGL(stem_pool_kernel, dim3(B * 49), dim3(256), 0, s, stem_in, C, Wt + st.w_off, P + st.b_off,
+                       P + stem_corr_off, X);
     MEC_LAUNCH_CHECK();
+    MEC_TRY(prof.end(TAG_RESNET_STEM, s));
   }
   f16* cur = X;
   f16* other = Y;

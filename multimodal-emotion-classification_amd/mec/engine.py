@@ -210,20 +210,44 @@ ROW = 34
 
 
 class FusedPipeline:
-    """The whole tri-modal path: speech + text + image encoders, then the fusion model."""
+    """The whole tri-modal path: speech + text + image encoders, then the fusion model.
 
-    def __init__(self, seed: int = 1234, device=None, weights=None):
+    BERT runs on the caller's stream; speech and ResNet50 run concurrently on a second HIP
+    stream (their kernels fill the CUs that BERT's GEMM tails and its LayerNorm/attention
+    kernels leave idle); the fusion waits for both. The first call runs everything
+    serially so each GEMM shape is autotuned in isolation.
+    """
+
+    def __init__(self, seed: int = 1234, device=None, weights=None, concurrent: bool = True):
         weights = weights or {}
         self.speech = SpeechEncoder(weights.get('speech'), seed, device)
         self.text = TextEncoder(weights.get('text'), seed, device)
         self.image = ImageEncoder(weights.get('image'), seed, device)
         self.fusion = FusionHead(weights.get('fusion'), seed, device)
         self.device = self.speech.device
+        self.concurrent = concurrent
+        self._side = torch.cuda.Stream(device=self.device) if concurrent else None
+        self._tuned = False
 
     def forward(self, x_speech, ids, mask, gray):
-        sf, sl, sp = self.speech.forward(x_speech)
-        tf, tl, tp = self.text.forward(ids, mask)
-        imf, il, ip = self.image.forward(gray)
+        if not self.concurrent or not self._tuned:
+            sf, sl, sp = self.speech.forward(x_speech)
+            tf, tl, tp = self.text.forward(ids, mask)
+            imf, il, ip = self.image.forward(gray)
+            self._tuned = True
+        else:
+            main = torch.cuda.current_stream(self.device)
+            side = self._side
+            side.wait_stream(main)  # inputs were produced on the main stream
+            with torch.cuda.stream(side):
+                sf, sl, sp = self.speech.forward(x_speech)
+                imf, il, ip = self.image.forward(gray)
+            tf, tl, tp = self.text.forward(ids, mask)
+            main.wait_stream(side)
+            for t in (sf, sl, sp, imf, il, ip):
+                t.record_stream(main)
+            for t in (x_speech, gray):
+                t.record_stream(side)
         fl, fp, aw, dw = self.fusion.forward(sf, tf, imf, sp, tp, ip)
         return {'speech': (sf, sl, sp), 'text': (tf, tl, tp), 'image': (imf, il, ip),
                 'fusion': (fl, fp, aw, dw)}
