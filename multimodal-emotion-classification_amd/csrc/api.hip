@@ -208,7 +208,8 @@ int mec_set_option(const char* key, int value) {
   if (k == "gemm_impl" && (value == 1 || value == 2)) { g_gemm_impl = value; return 0; }
   if (k == "gemm_debug" && value >= 0 && value <= 2) { g_gemm_debug = value; return 0; }
   if (k == "gemm_autotune" && (value == 0 || value == 1)) { g_gemm_autotune = value; return 0; }
-  if (k == "gemm_bn" && (value == 0 || value == 64 || value == 128 || value == 256 || value == 1064 || value == 1128)) {
+  const int v = value % 10000;
+  if (k == "gemm_bn" && (value == 0 || v == 64 || v == 128 || v == 256 || v == 1064 || v == 1128)) {
     g_gemm_bn = value;
     return 0;
   }

@@ -49,14 +49,17 @@ __device__ __forceinline__ void wait_vm() {
   asm volatile("s_waitcnt vmcnt(%0)" ::"n"(N) : "memory");
 }
 
-template <int BM, int BN, int WM, int WN, int NS, int AM, int DBG = 0>
+template <int BM, int BN, int WM, int WN, int NS, int AM, int DBG = 0, int MF = 32>
 __global__ __launch_bounds__(64 * WM * WN) void gemm_glds_kernel(const GemmParams p) {
+  // MF: 32 = v_mfma_f32_32x32x16_f16 tiles, 16 = v_mfma_f32_16x16x32_f16 tiles
   // DBG (probe builds only): 1 = no operand loads inside the K loop, 2 = no epilogue
   constexpr int BK = 64;
   constexpr int NW = WM * WN;
   static_assert(NW == 8 || NW == 4, "4 or 8 waves");
   constexpr int TM = BM / WM, TN = BN / WN;    // wave tile
-  constexpr int TI = TM / 32, TJ = TN / 32;    // 32x32 MFMA tiles per wave
+  constexpr int TI = TM / MF, TJ = TN / MF;    // MFxMF MFMA tiles per wave
+  typedef float accv __attribute__((ext_vector_type(MF == 32 ? 16 : 4)));
+  constexpr int NACC = MF == 32 ? 16 : 4;
   constexpr int AI = BM / 8 / NW;              // glds wave-instructions per stage (A)
   constexpr int BI = BN / 8 / NW;              // (B)
   static_assert(BI >= 1 && AI >= 1, "tile too small for 8 waves");
@@ -145,13 +148,13 @@ __global__ __launch_bounds__(64 * WM * WN) void gemm_glds_kernel(const GemmParam
                                        0, 0);
   };
 
-  floatx16 acc[TI][TJ];
+  accv acc[TI][TJ];
 #pragma unroll
   for (int i = 0; i < TI; ++i)
 #pragma unroll
     for (int j = 0; j < TJ; ++j)
 #pragma unroll
-      for (int e = 0; e < 16; ++e) acc[i][j][e] = 0.f;
+      for (int e = 0; e < NACC; ++e) acc[i][j][e] = 0.f;
 
   const int nk = K / BK;
 #pragma unroll
@@ -174,25 +177,50 @@ __global__ __launch_bounds__(64 * WM * WN) void gemm_glds_kernel(const GemmParam
     if (DBG != 1 && t + NS - 1 < nk) issue((t + NS - 1) % NS, t + NS - 1);
     const f16* sA = smem + ((DBG == 1 ? 0 : t) % NS) * STAGE;
     const f16* sB = sA + BM * BK;
+    if constexpr (MF == 32) {
 #pragma unroll
-    for (int s = 0; s < 4; ++s) {
-      const int kcs = 2 * s + lh;
-      half8 af[TI], bf[TJ];
+      for (int s = 0; s < 4; ++s) {
+        const int kcs = 2 * s + lh;
+        half8 af[TI], bf[TJ];
 #pragma unroll
-      for (int i = 0; i < TI; ++i) {
-        const int r = wm * TM + i * 32 + lr;
-        af[i] = *reinterpret_cast<const half8*>(sA + r * BK + sw(r, kcs) * 8);
+        for (int i = 0; i < TI; ++i) {
+          const int r = wm * TM + i * 32 + lr;
+          af[i] = *reinterpret_cast<const half8*>(sA + r * BK + sw(r, kcs) * 8);
+        }
+#pragma unroll
+        for (int j = 0; j < TJ; ++j) {
+          const int r = wn * TN + j * 32 + lr;
+          bf[j] = *reinterpret_cast<const half8*>(sB + r * BK + sw(r, kcs) * 8);
+        }
+#pragma unroll
+        for (int i = 0; i < TI; ++i)
+#pragma unroll
+          for (int j = 0; j < TJ; ++j)
+            acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_f16(af[i], bf[j], acc[i][j], 0, 0, 0);
       }
+    } else {
+      // 16x16x32: lane l holds A[row l&15][k 8(l>>4)..+7] of each 32-deep k step
+      const int l16 = lane & 15, lq = lane >> 4;
 #pragma unroll
-      for (int j = 0; j < TJ; ++j) {
-        const int r = wn * TN + j * 32 + lr;
-        bf[j] = *reinterpret_cast<const half8*>(sB + r * BK + sw(r, kcs) * 8);
+      for (int s = 0; s < 2; ++s) {
+        const int kcs = 4 * s + lq;
+        half8 af[TI], bf[TJ];
+#pragma unroll
+        for (int i = 0; i < TI; ++i) {
+          const int r = wm * TM + i * 16 + l16;
+          af[i] = *reinterpret_cast<const half8*>(sA + r * BK + sw(r, kcs) * 8);
+        }
+#pragma unroll
+        for (int j = 0; j < TJ; ++j) {
+          const int r = wn * TN + j * 16 + l16;
+          bf[j] = *reinterpret_cast<const half8*>(sB + r * BK + sw(r, kcs) * 8);
+        }
+#pragma unroll
+        for (int i = 0; i < TI; ++i)
+#pragma unroll
+          for (int j = 0; j < TJ; ++j)
+            acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_f16(af[i], bf[j], acc[i][j], 0, 0, 0);
       }
-#pragma unroll
-      for (int i = 0; i < TI; ++i)
-#pragma unroll
-        for (int j = 0; j < TJ; ++j)
-          acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_f16(af[i], bf[j], acc[i][j], 0, 0, 0);
     }
   }
   asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)" ::: "memory");
@@ -206,7 +234,7 @@ __global__ __launch_bounds__(64 * WM * WN) void gemm_glds_kernel(const GemmParam
 #pragma unroll
       for (int j = 0; j < TJ; ++j)
 #pragma unroll
-        for (int e = 0; e < 16; ++e) s += acc[i][j][e];
+        for (int e = 0; e < NACC; ++e) s += acc[i][j][e];
     if (s == 12345.678f) p.C32[0] = s;  // keeps the accumulators live
     return;
   }
@@ -227,15 +255,26 @@ __global__ __launch_bounds__(64 * WM * WN) void gemm_glds_kernel(const GemmParam
     bias[0] = b0.x; bias[1] = b0.y; bias[2] = b0.z; bias[3] = b0.w;
     bias[4] = b1.x; bias[5] = b1.y; bias[6] = b1.z; bias[7] = b1.w;
   }
+  constexpr int SLABS = TM / 32;
 #pragma unroll
-  for (int i = 0; i < TI; ++i) {
+  for (int i = 0; i < SLABS; ++i) {
+    if constexpr (MF == 32) {
 #pragma unroll
-    for (int j = 0; j < TJ; ++j)
+      for (int j = 0; j < TJ; ++j)
 #pragma unroll
-      for (int e = 0; e < 16; ++e) {
-        const int rr = (e & 3) + 8 * (e >> 2) + 4 * lh;
-        stg[rr * EPI_LD + j * 32 + lr] = acc[i][j][e];
-      }
+        for (int e = 0; e < 16; ++e) {
+          const int rr = (e & 3) + 8 * (e >> 2) + 4 * lh;
+          stg[rr * EPI_LD + j * 32 + lr] = acc[i][j][e];
+        }
+    } else {  // 16x16 D layout: col = lane&15, row = 4(lane>>4) + e
+#pragma unroll
+      for (int a = 0; a < 2; ++a)
+#pragma unroll
+        for (int j = 0; j < TJ; ++j)
+#pragma unroll
+          for (int e = 0; e < 4; ++e)
+            stg[(16 * a + 4 * (lane >> 4) + e) * EPI_LD + j * 16 + (lane & 15)] = acc[2 * i + a][j][e];
+    }
     asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
     constexpr int NPS = 32 / RPP;
     float rv[NPS][8];
@@ -301,7 +340,7 @@ __global__ __launch_bounds__(64 * WM * WN) void gemm_glds_kernel(const GemmParam
 // BM=256 tiles: (BN, WM, WN, NS)
 int g_gemm_debug = 0;
 
-template <int BM, int BN, int WM, int WN, int NS>
+template <int BM, int BN, int WM, int WN, int NS, int MF = 32>
 static int launch_cfg(const GemmParams& p, hipStream_t s) {
   const int nwg = ((p.M + BM - 1) / BM) * (p.N / BN);
   const dim3 blk(64 * WM * WN);
@@ -311,9 +350,9 @@ static int launch_cfg(const GemmParams& p, hipStream_t s) {
     else
       hipLaunchKernelGGL((gemm_glds_kernel<BM, BN, WM, WN, NS, A_PLAIN, 2>), dim3(nwg), blk, 0, s, p);
   } else if (p.amode == A_PLAIN)
-    hipLaunchKernelGGL((gemm_glds_kernel<BM, BN, WM, WN, NS, A_PLAIN>), dim3(nwg), blk, 0, s, p);
+    hipLaunchKernelGGL((gemm_glds_kernel<BM, BN, WM, WN, NS, A_PLAIN, 0, MF>), dim3(nwg), blk, 0, s, p);
   else
-    hipLaunchKernelGGL((gemm_glds_kernel<BM, BN, WM, WN, NS, A_CONV>), dim3(nwg), blk, 0, s, p);
+    hipLaunchKernelGGL((gemm_glds_kernel<BM, BN, WM, WN, NS, A_CONV, 0, MF>), dim3(nwg), blk, 0, s, p);
   MEC_LAUNCH_CHECK();
   return 0;
 }
@@ -339,7 +378,11 @@ int g_gemm_autotune = 1;
 // Tile configs (id): 256 / 128 / 64 = 256 x BN with 8 waves; 1128 / 1064 = 128 x BN with
 // 4 waves (64 / 48 KB of LDS, so two blocks share a CU and one block's epilogue overlaps
 // the other's MFMA loop).
-static int tile_bn(int id) { return id > 1000 ? id - 1000 : id; }
+// +10000: the same tile on v_mfma_f32_16x16x32_f16.
+static int tile_bn(int id) {
+  id %= 10000;
+  return id > 1000 ? id - 1000 : id;
+}
 
 static int launch_bn(const GemmParams& p, hipStream_t s, int id) {
   switch (id) {
@@ -348,6 +391,11 @@ static int launch_bn(const GemmParams& p, hipStream_t s, int id) {
     case 64: return launch_cfg<256, 64, 4, 2, 3>(p, s);
     case 1128: return launch_cfg<128, 128, 2, 2, 2>(p, s);
     case 1064: return launch_cfg<128, 64, 2, 2, 2>(p, s);
+    case 10256: return launch_cfg<256, 256, 2, 4, 2, 16>(p, s);
+    case 10128: return launch_cfg<256, 128, 4, 2, 3, 16>(p, s);
+    case 10064: return launch_cfg<256, 64, 4, 2, 3, 16>(p, s);
+    case 11128: return launch_cfg<128, 128, 2, 2, 2, 16>(p, s);
+    case 11064: return launch_cfg<128, 64, 2, 2, 2, 16>(p, s);
     default: set_error("gemm_glds: unsupported tile id"); return -1;
   }
 }
@@ -362,7 +410,7 @@ static int heuristic_bn(const GemmParams& p) {
 
 static int tune_bn(const GemmParams& p, hipStream_t s, int* out_bn) {
   constexpr int REPS = 5;
-  const int cands[5] = {64, 128, 256, 1128, 1064};
+  const int cands[10] = {64, 128, 256, 1128, 1064, 10064, 10128, 10256, 11128, 11064};
   hipEvent_t ev[REPS + 1];
   for (auto& e : ev) MEC_HIP(hipEventCreate(&e));
   float best = 1e30f;
