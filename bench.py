@@ -111,6 +111,12 @@ def main():
     torch.cuda.synchronize()
     el = time.perf_counter() - t0
     ffn_ms, ffn_n = pipe.text.prof_read()
+    # the same kernel with BERT alone on the GPU (no concurrent image stream), untimed region
+    pipe.text.prof_enable('bert_ffn1')
+    for _ in range(2):
+        pipe.text.forward(ids, mask)
+    torch.cuda.synchronize()
+    iso_ms, iso_n = pipe.text.prof_read()
     pipe.text.prof_enable(0)
     t = torch.tensor([el], device=dev, dtype=torch.float64)
     if world > 1:
@@ -122,13 +128,30 @@ def main():
         ffn_flop = 2.0 * M * 3072 * 768
         avg_s = (ffn_ms / max(ffn_n, 1)) / 1e3
         achieved = ffn_flop / avg_s / 1e12 if ffn_n else None
-        bn = pipe.text.lib.mec_gemm_query(0, M, 3072, 768)
-        kname = (f'gemm_glds_kernel<256,{bn},...,A_PLAIN> grid={((M + 255) // 256) * (3072 // bn)} '
+        tile = pipe.text.lib.mec_gemm_query(0, M, 3072, 768)
+        bm, bnw = (128, tile % 10000 - 1000) if tile % 10000 > 1000 else (256, tile % 10000)
+        mf = 16 if tile >= 10000 else 32
+        grid = ((M + bm - 1) // bm) * (3072 // bnw)
+        kname = (f'gemm_glds_kernel<{bm},{bnw},...,A_PLAIN,mfma{mf}x{mf}> grid={grid} '
                  f'(BERT FFN1 + GELU epilogue, M={M} N=3072 K=768)')
+        iso = ffn_flop / ((iso_ms / max(iso_n, 1)) / 1e3) / 1e12 if iso_n else None
+        traffic, tsrc = None, None
+        tf = os.path.join(ROOT, 'profiles', 'ffn1_traffic.json')
+        if os.path.exists(tf):  # PMC passes (tools/pmc.sh), FETCH_SIZE x2 per MI355X_MICROARCH gfx950 note
+            with open(tf) as fh:
+                t = json.load(fh)
+            if t.get('tile') == tile and t.get('M') == M:
+                traffic, tsrc = t['bytes_per_launch'], t['source']
         roof = {'bound': 'mfma', 'kernel': kname,
                 'achieved': achieved, 'peak': MI355X_F16_DENSE_TFLOPS, 'unit': 'TFLOP/s',
-                'frac': (achieved / MI355X_F16_DENSE_TFLOPS) if achieved else None, 'traffic': None,
-                'avg_launch_ms': avg_s * 1e3, 'launches': ffn_n}
+                'frac': (achieved / MI355X_F16_DENSE_TFLOPS) if achieved else None, 'traffic': traffic,
+                'traffic_source': tsrc, 'algorithmic_flop_per_launch': ffn_flop,
+                'algorithmic_bytes_per_launch': 2 * (M * 768 + 3072 * 768 + M * 3072),
+                'avg_launch_ms': avg_s * 1e3, 'launches': ffn_n,
+                'note': 'achieved = live, inside the timed region, sharing CUs with the concurrent image '
+                        'stream; achieved_isolated = same kernel with BERT alone',
+                'achieved_isolated': iso,
+                'frac_isolated': (iso / MI355X_F16_DENSE_TFLOPS) if iso else None}
         total = world * B * a.steps
         flop = sum(FLOP_PER_SAMPLE.values()) * total
         res = {

@@ -30,16 +30,22 @@ __device__ __forceinline__ float block_act(float v, int act) {
 // contiguous chunks (one per thread group) and the partial sums are combined through
 // LDS scratch `red` (>= R * blockDim floats). Weights are fetched 16 k-rows at a time so
 // 16 independent loads are in flight per thread (the loop is load-latency bound).
+typedef __attribute__((address_space(3))) const float lds_cf;
+
 template <int R>
-__device__ __noinline__ void block_linear(const float* X, int ldx, int K, const float* __restrict__ Wt, int ldw,
+__device__ __noinline__ void block_linear(const float* Xg, int ldx, int K, const float* __restrict__ Wt, int ldw,
                                           const float* __restrict__ b, int N, float* Y, int ldy, float* red,
                                           int act) {
+  // X always lives in LDS: address it as such (ds_read, broadcast across the wave) rather
+  // than through a generic pointer (flat loads wait on both vmcnt and lgkmcnt).
+  lds_cf* X = (lds_cf*)Xg;
   const int T = blockDim.x, tid = threadIdx.x;
   const int G = (N >= T || red == nullptr) ? 1 : (T / N);
   const int cols = (G == 1) ? T : N;
   const int g = tid / cols, c = tid - g * cols;
-  const int kchunk = (K + G - 1) / G;
+  const int kchunk = ((K + G - 1) / G + 3) & ~3;  // multiple of 4: float4 reads of X stay aligned
   const int kb = g * kchunk, ke = min(K, kb + kchunk);
+  const bool x4 = (ldx & 3) == 0;
   if (g < G) {
     for (int n = c; n < N; n += cols) {
       float acc[R];
@@ -50,10 +56,26 @@ __device__ __noinline__ void block_linear(const float* X, int ldx, int K, const 
         float w[16];
 #pragma unroll
         for (int q = 0; q < 16; ++q) w[q] = Wt[(size_t)(k + q) * ldw + n];
+        if (x4) {
 #pragma unroll
-        for (int q = 0; q < 16; ++q)
+          for (int r = 0; r < R; ++r) {
 #pragma unroll
-          for (int r = 0; r < R; ++r) acc[r] = fmaf(X[r * ldx + k + q], w[q], acc[r]);
+            for (int q4 = 0; q4 < 4; ++q4) {
+              const __attribute__((address_space(3))) floatx4* p4 =
+                  (const __attribute__((address_space(3))) floatx4*)(X + r * ldx + k + 4 * q4);
+              const floatx4 xv = *p4;
+              acc[r] = fmaf(xv.x, w[4 * q4 + 0], acc[r]);
+              acc[r] = fmaf(xv.y, w[4 * q4 + 1], acc[r]);
+              acc[r] = fmaf(xv.z, w[4 * q4 + 2], acc[r]);
+              acc[r] = fmaf(xv.w, w[4 * q4 + 3], acc[r]);
+            }
+          }
+        } else {
+#pragma unroll
+          for (int q = 0; q < 16; ++q)
+#pragma unroll
+            for (int r = 0; r < R; ++r) acc[r] = fmaf(X[r * ldx + k + q], w[q], acc[r]);
+        }
       }
       for (; k < ke; ++k) {
         const float w = Wt[(size_t)k * ldw + n];
@@ -136,9 +158,9 @@ __global__ __launch_bounds__(256) void linear_rows_kernel(const float* __restric
                                                           const float* __restrict__ Wt, const float* __restrict__ bias,
                                                           int N, int cols, float* __restrict__ Y, int ldy, int act,
                                                           float* __restrict__ Xcopy, int ldxc) {
-  __shared__ float sX[R * KMAX];
-  __shared__ float sY[R * 256];
-  __shared__ float red[R * 256];
+  __shared__ __attribute__((aligned(16))) float sX[R * KMAX];
+  __shared__ __attribute__((aligned(16))) float sY[R * 256];
+  __shared__ __attribute__((aligned(16))) float red[R * 256];
   const int tid = threadIdx.x;
   const int r0 = blockIdx.x * R, nr = min(R, B - r0);
   const int col0 = blockIdx.y * cols, nc = min(cols, N - col0);
@@ -161,9 +183,9 @@ template <int R, int KMAX>
 __global__ __launch_bounds__(256) void head_softmax_kernel(const float* __restrict__ X, int B, int K,
                                                            const float* __restrict__ Wt, const float* __restrict__ b,
                                                            float* __restrict__ logits, float* __restrict__ probs) {
-  __shared__ float sX[R * KMAX];
-  __shared__ float sY[R * 8];
-  __shared__ float red[R * 256];
+  __shared__ __attribute__((aligned(16))) float sX[R * KMAX];
+  __shared__ __attribute__((aligned(16))) float sY[R * 8];
+  __shared__ __attribute__((aligned(16))) float red[R * 256];
   const int tid = threadIdx.x;
   const int r0 = blockIdx.x * R, nr = min(R, B - r0);
   for (int idx = tid; idx < R * K; idx += blockDim.x) {

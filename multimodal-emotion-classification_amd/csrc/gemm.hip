@@ -214,6 +214,10 @@ int launch_gemm(const GemmParams& p, hipStream_t s, Prof* prof, int tag) {
   MEC_REQUIRE(p.C16 || p.C32, "gemm: no output");
   if (p.amode == A_CONV) {
     MEC_REQUIRE(p.C % 64 == 0 && p.K == p.ks * p.ks * p.C, "conv: C % 64 != 0 or K != ks*ks*C");
+  } else if (p.amode == A_DUAL) {
+    MEC_REQUIRE(p.A2 && p.K1 > 0 && p.K1 % 64 == 0 && p.C % 64 == 0 && p.K == p.K1 + p.C && p.ks == 1 && p.pad == 0,
+                "dual gemm: need K = K1 + C, K1 % 64 == 0, C % 64 == 0, 1x1 unpadded second source");
+    MEC_REQUIRE(g_gemm_impl == 2, "dual gemm needs the glds engine");
   } else {
     MEC_REQUIRE(p.amode == A_PLAIN, "gemm: unknown A mode");
   }

@@ -1,6 +1,8 @@
 // Pipelined fp16 MFMA GEMM / implicit-GEMM conv for gfx950 (the main GEMM engine).
 //
 //   C[M,N] = epilogue( A'[M,K] . B[N,K]^T ),  A' = A (A_PLAIN) or im2col(NHWC) (A_CONV)
+//   or [A | 1x1/stride-s view of A2] concatenated along K (A_DUAL: a ResNet bottleneck's
+//   conv3 and its downsample projection as one GEMM)
 //
 // * Tile BM=256 x BN (64/128/256) x BK=64, 512 threads = 8 waves (WM x WN), each wave a
 //   (BM/WM) x (BN/WN) block of v_mfma_f32_32x32x16_f16 accumulators.
@@ -88,6 +90,7 @@ __global__ __launch_bounds__(64 * WM * WN) void gemm_glds_kernel(const GemmParam
   // ---- per-lane DMA sources: lane -> (row in its 8-row group, physical chunk)
   const int lrow = lane >> 3, pchunk = lane & 7;
   const f16* a_src[AI];
+  const f16* a2_src[AI];  // A_DUAL: second source (1x1 / stride-s view of an NHWC tensor)
   int a_ih0[AI], a_iw0[AI];
   bool a_ok[AI];
 #pragma unroll
@@ -99,6 +102,15 @@ __global__ __launch_bounds__(64 * WM * WN) void gemm_glds_kernel(const GemmParam
     const int kc = pchunk ^ ((r >> 1) & 7);
     if constexpr (AM == A_PLAIN) {
       a_src[i] = reinterpret_cast<const f16*>(p.A) + (size_t)mc * K + kc * 8;
+    } else if constexpr (AM == A_DUAL) {
+      a_src[i] = reinterpret_cast<const f16*>(p.A) + (size_t)mc * p.K1 + kc * 8;
+      const int ohw = p.OH * p.OW;
+      const int n = mc / ohw;
+      const int rem = mc - n * ohw;
+      const int oh = rem / p.OW;
+      const int ow = rem - oh * p.OW;
+      a2_src[i] = reinterpret_cast<const f16*>(p.A2) +
+                  (((size_t)n * p.H + oh * p.stride) * p.W + ow * p.stride) * p.C + kc * 8;
     } else {
       const int ohw = p.OH * p.OW;
       const int n = mc / ohw;
@@ -127,6 +139,13 @@ __global__ __launch_bounds__(64 * WM * WN) void gemm_glds_kernel(const GemmParam
 #pragma unroll
       for (int i = 0; i < AI; ++i) {
         const f16* src = a_ok[i] ? a_src[i] + k0 : zero;
+        __builtin_amdgcn_global_load_lds((const void*)src, (lds_vptr)(sA + (wave * AI + i) * 8 * BK), 16, 0, 0);
+      }
+    } else if constexpr (AM == A_DUAL) {
+      const bool first = k0 < p.K1;
+#pragma unroll
+      for (int i = 0; i < AI; ++i) {
+        const f16* src = !a_ok[i] ? zero : (first ? a_src[i] + k0 : a2_src[i] + (k0 - p.K1));
         __builtin_amdgcn_global_load_lds((const void*)src, (lds_vptr)(sA + (wave * AI + i) * 8 * BK), 16, 0, 0);
       }
     } else {
@@ -199,28 +218,33 @@ __global__ __launch_bounds__(64 * WM * WN) void gemm_glds_kernel(const GemmParam
             acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_f16(af[i], bf[j], acc[i][j], 0, 0, 0);
       }
     } else {
-      // 16x16x32: lane l holds A[row l&15][k 8(l>>4)..+7] of each 32-deep k step
+      // 16x16x32: lane l holds A[row l&15][k 8(l>>4)..+7] of each 32-deep k step. Both
+      // k steps' fragments are requested up front, so the second step's LDS reads are in
+      // flight under the first step's MFMAs (counted lgkmcnt instead of a drain per group).
       const int l16 = lane & 15, lq = lane >> 4;
+      half8 af[2][TI], bf[2][TJ];
 #pragma unroll
       for (int s = 0; s < 2; ++s) {
         const int kcs = 4 * s + lq;
-        half8 af[TI], bf[TJ];
 #pragma unroll
         for (int i = 0; i < TI; ++i) {
           const int r = wm * TM + i * 16 + l16;
-          af[i] = *reinterpret_cast<const half8*>(sA + r * BK + sw(r, kcs) * 8);
+          af[s][i] = *reinterpret_cast<const half8*>(sA + r * BK + sw(r, kcs) * 8);
         }
 #pragma unroll
         for (int j = 0; j < TJ; ++j) {
           const int r = wn * TN + j * 16 + l16;
-          bf[j] = *reinterpret_cast<const half8*>(sB + r * BK + sw(r, kcs) * 8);
+          bf[s][j] = *reinterpret_cast<const half8*>(sB + r * BK + sw(r, kcs) * 8);
         }
+      }
+      __builtin_amdgcn_sched_barrier(0);  // keep all fragment reads ahead of the MFMAs
+#pragma unroll
+      for (int s = 0; s < 2; ++s)
 #pragma unroll
         for (int i = 0; i < TI; ++i)
 #pragma unroll
           for (int j = 0; j < TJ; ++j)
-            acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_f16(af[i], bf[j], acc[i][j], 0, 0, 0);
-      }
+            acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_f16(af[s][i], bf[s][j], acc[i][j], 0, 0, 0);
     }
   }
   asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)" ::: "memory");
@@ -351,6 +375,8 @@ static int launch_cfg(const GemmParams& p, hipStream_t s) {
       hipLaunchKernelGGL((gemm_glds_kernel<BM, BN, WM, WN, NS, A_PLAIN, 2>), dim3(nwg), blk, 0, s, p);
   } else if (p.amode == A_PLAIN)
     hipLaunchKernelGGL((gemm_glds_kernel<BM, BN, WM, WN, NS, A_PLAIN, 0, MF>), dim3(nwg), blk, 0, s, p);
+  else if (p.amode == A_DUAL)
+    hipLaunchKernelGGL((gemm_glds_kernel<BM, BN, WM, WN, NS, A_DUAL, 0, MF>), dim3(nwg), blk, 0, s, p);
   else
     hipLaunchKernelGGL((gemm_glds_kernel<BM, BN, WM, WN, NS, A_CONV, 0, MF>), dim3(nwg), blk, 0, s, p);
   MEC_LAUNCH_CHECK();

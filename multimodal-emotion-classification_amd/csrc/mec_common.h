@@ -98,7 +98,7 @@ struct BlobReader {
 // fp16 MFMA GEMM / implicit-GEMM convolution ------------------------------------------
 // C[M,N] = epilogue( A'[M,K] . B[N,K]^T ), A' = A (plain) or the im2col view of an NHWC
 // tensor (conv).
-enum AMode : int { A_PLAIN = 0, A_CONV = 1 };
+enum AMode : int { A_PLAIN = 0, A_CONV = 1, A_DUAL = 2 };
 enum Act : int { ACT_NONE = 0, ACT_RELU = 1, ACT_GELU = 2 };
 
 struct GemmParams {
@@ -112,6 +112,8 @@ struct GemmParams {
   int M = 0, N = 0, K = 0;
   int act = ACT_NONE;
   int amode = A_PLAIN;
+  const void* A2 = nullptr;  // A_DUAL second source (NHWC, geometry below), K1 = columns of A
+  int K1 = 0;
   // conv geometry (NHWC input)
   int H = 1, W = 1, C = 0, OH = 1, OW = 1, ks = 1, stride = 1, pad = 0;
 };

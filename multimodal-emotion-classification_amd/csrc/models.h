@@ -59,6 +59,7 @@ struct ConvLayer {
 struct Bottleneck {
   ConvLayer c1, c2, c3, ds;
   bool has_ds = false;
+  size_t c3ds_w_off = 0, c3ds_b_off = 0;  // block 0: [conv3 | downsample] weights [4w][w+cin], summed bias
 };
 struct ImageModel : Model {
   DevBuf wts;   // f16 conv weights

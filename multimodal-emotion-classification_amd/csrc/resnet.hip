@@ -371,6 +371,17 @@ int ImageModel::create(const float* blob, size_t n) {
       if (b == 0) {
         bk.has_ds = true;
         bk.ds = conv(4 * wd, cin, 1, s, 0);
+        // conv3 and the downsample projection as one GEMM over K = [w | cin] (A_DUAL):
+        // bn3(conv3(t)) + bn_ds(conv_ds(x)) = [t | x] . [W3' | Wds']^T + (b3 + bds)
+        bk.c3ds_w_off = w.size();
+        const int K3 = wd, K2 = cin, Kt = wd + cin;
+        w.resize(w.size() + (size_t)4 * wd * Kt);
+        for (int o = 0; o < 4 * wd; ++o) {
+          for (int k = 0; k < K3; ++k) w[bk.c3ds_w_off + (size_t)o * Kt + k] = w[bk.c3.w_off + (size_t)o * K3 + k];
+          for (int k = 0; k < K2; ++k) w[bk.c3ds_w_off + (size_t)o * Kt + K3 + k] = w[bk.ds.w_off + (size_t)o * K2 + k];
+        }
+        bk.c3ds_b_off = pr.size();
+        for (int o = 0; o < 4 * wd; ++o) pr.push_back(pr[bk.c3.b_off + o] + pr[bk.ds.b_off + o]);
       }
       blocks.push_back(bk);
       cin = 4 * wd;
@@ -412,7 +423,7 @@ int ImageModel::forward_u8(const uint8_t* img, int B, int H, int W, int C, float
               "image: input must be u8 [B,48,48,1] (GPU resize) or [B,224,224,{1,3}] (already resized)");
   const size_t per_img_big = (size_t)56 * 56 * 256;  // largest NHWC activation (elements)
   const size_t per_t1 = (size_t)56 * 56 * 128, per_t2 = (size_t)56 * 56 * 64;
-  const size_t per_img = 224 * 224 + (3 * per_img_big + per_t1 + per_t2) * sizeof(f16) + 256 + 2048 * sizeof(float);
+  const size_t per_img = 224 * 224 + (2 * per_img_big + per_t1 + per_t2) * sizeof(f16) + 256 + 2048 * sizeof(float);
   if (B > ws_batch) {
     MEC_TRY(ws.ensure(per_img * (size_t)B + 4096));
     ws_batch = B;
@@ -422,7 +433,6 @@ int ImageModel::forward_u8(const uint8_t* img, int B, int H, int W, int C, float
   p += ((size_t)B * 224 * 224 + 255) / 256 * 256;
   f16* X = reinterpret_cast<f16*>(p); p += (size_t)B * per_img_big * sizeof(f16);
   f16* Y = reinterpret_cast<f16*>(p); p += (size_t)B * per_img_big * sizeof(f16);
-  f16* DS = reinterpret_cast<f16*>(p); p += (size_t)B * per_img_big * sizeof(f16);
   f16* T1 = reinterpret_cast<f16*>(p); p += (size_t)B * per_t1 * sizeof(f16);
   f16* T2 = reinterpret_cast<f16*>(p);
   p += (size_t)B * per_t2 * sizeof(f16);
@@ -458,21 +468,18 @@ int ImageModel::forward_u8(const uint8_t* img, int B, int H, int W, int C, float
     g.M = B * OH * OH; g.N = wd; g.K = 9 * wd;
     g.H = H; g.W = H; g.C = wd; g.OH = OH; g.OW = OH; g.ks = 3; g.stride = st; g.pad = 1;
     MEC_TRY(launch_gemm(g, s, &prof, TAG_RESNET_CONV3X3));
-    const f16* res = cur;
-    if (bk.has_ds) {
+    if (bk.has_ds) {  // conv3 + downsample + add + ReLU in one dual-source GEMM
       g = GemmParams();
-      g.B = Wt + bk.ds.w_off; g.bias = P + bk.ds.b_off; g.C16 = DS; g.A = cur;
-      g.M = B * OH * OH; g.N = 4 * wd; g.K = cin;
-      if (st != 1) {
-        g.amode = A_CONV; g.H = H; g.W = H; g.C = cin; g.OH = OH; g.OW = OH; g.ks = 1; g.stride = st; g.pad = 0;
-      }
+      g.amode = A_DUAL; g.A = T2; g.K1 = wd; g.A2 = cur; g.B = Wt + bk.c3ds_w_off; g.bias = P + bk.c3ds_b_off;
+      g.act = ACT_RELU; g.C16 = other; g.M = B * OH * OH; g.N = 4 * wd; g.K = wd + cin;
+      g.H = H; g.W = H; g.C = cin; g.OH = OH; g.OW = OH; g.ks = 1; g.stride = st; g.pad = 0;
       MEC_TRY(launch_gemm(g, s, &prof, TAG_RESNET_CONV1X1));
-      res = DS;
+    } else {
+      g = GemmParams();
+      g.A = T2; g.B = Wt + bk.c3.w_off; g.bias = P + bk.c3.b_off; g.R = cur; g.act = ACT_RELU; g.C16 = other;
+      g.M = B * OH * OH; g.N = 4 * wd; g.K = wd;
+      MEC_TRY(launch_gemm(g, s, &prof, TAG_RESNET_CONV1X1));
     }
-    g = GemmParams();
-    g.A = T2; g.B = Wt + bk.c3.w_off; g.bias = P + bk.c3.b_off; g.R = res; g.act = ACT_RELU; g.C16 = other;
-    g.M = B * OH * OH; g.N = 4 * wd; g.K = wd;
-    MEC_TRY(launch_gemm(g, s, &prof, TAG_RESNET_CONV1X1));
     std::swap(cur, other);
     H = OH;
   }

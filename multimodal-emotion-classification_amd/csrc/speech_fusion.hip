@@ -29,7 +29,7 @@ __constant__ int kSpeechDims[6] = {56, 512, 512, 256, 128, 64};
 __global__ __launch_bounds__(512) void speech_kernel(SpeechW w, const float* __restrict__ x, int B,
                                                      float* feat, float* logits, float* probs) {
   constexpr int R = SPEECH_R, LD = 512;
-  __shared__ float bufA[R * LD], bufB[R * LD], red[R * SF_THREADS];
+  __shared__ __attribute__((aligned(16))) float bufA[R * LD], bufB[R * LD], red[R * SF_THREADS];
   const int tid = threadIdx.x;
   const int r0 = blockIdx.x * R;
   const int nr = min(R, B - r0);
@@ -167,7 +167,7 @@ __global__ __launch_bounds__(512) void fusion_kernel(FusionW w, const float* __r
                                                      const float* __restrict__ ip, int B, float* logits,
                                                      float* probs, float* attn_w, float* dec_w) {
   constexpr int R = FUSION_R;
-  __shared__ float IN[R * F_LDIN], P[R * F_LDP], E[R * F_LDP], T[R * F_LDT], red[R * SF_THREADS];
+  __shared__ __attribute__((aligned(16))) float IN[R * F_LDIN], P[R * F_LDP], E[R * F_LDP], T[R * F_LDT], red[R * SF_THREADS];
   const int tid = threadIdx.x, T_ = blockDim.x;
   const int r0 = blockIdx.x * R;
   const int nr = min(R, B - r0);
