@@ -26,10 +26,11 @@ __device__ __forceinline__ float block_act(float v, int act) {
 
 // Y[r][n] = act(sum_k X[r][k] * Wt[k*ldw + n] + b[n]) for r < R (R samples), n < N.
 // X: LDS (row stride ldx); Y: LDS or global (row stride ldy).
-// Threads own output columns. When N < blockDim the K range is split into G = T/N
-// contiguous chunks (one per thread group) and the partial sums are combined through
-// LDS scratch `red` (>= R * blockDim floats). Weights are fetched 16 k-rows at a time so
-// 16 independent loads are in flight per thread (the loop is load-latency bound).
+// Quad path (N % 4 == 0, N >= 64): each thread owns 4 consecutive output columns and a
+// contiguous K chunk, weights are fetched as 16-B vectors 8 k-rows deep (the loop is bound
+// by bytes in flight from L2/MALL), partial sums are combined through LDS scratch `red`
+// (>= 4 * R * blockDim floats). Otherwise threads own single columns (K split into
+// G = T/N groups when N < T, `red` >= R * blockDim floats).
 typedef __attribute__((address_space(3))) const float lds_cf;
 
 template <int R>
@@ -46,6 +47,62 @@ __device__ __noinline__ void block_linear(const float* Xg, int ldx, int K, const
   const int kchunk = ((K + G - 1) / G + 3) & ~3;  // multiple of 4: float4 reads of X stay aligned
   const int kb = g * kchunk, ke = min(K, kb + kchunk);
   const bool x4 = (ldx & 3) == 0;
+  // quad path: N % 4 == 0, 16-B aligned rows, enough columns, room in `red` (R*4*T floats)
+  const int QCOLS = N / 4;
+  const bool quad = red != nullptr && x4 && (N & 3) == 0 && (ldw & 3) == 0 && QCOLS >= 16 && QCOLS <= T;
+  const int QG = quad ? T / QCOLS : 1;
+  const int qg = quad ? tid / QCOLS : 0, qc = quad ? tid - qg * QCOLS : 0;
+  const int qchunk = ((K + QG - 1) / QG + 7) & ~7;
+  const int qkb = qg * qchunk, qke = min(K, qkb + qchunk);
+  if (quad) {
+    // 4 consecutive output columns per thread (16-B weight loads: 4x the bytes in flight),
+    // K split over QG thread groups, partial sums combined through `red`.
+    if (qg < QG) {
+      const int n = 4 * qc;
+      float acc[R][4];
+#pragma unroll
+      for (int r = 0; r < R; ++r)
+#pragma unroll
+        for (int j = 0; j < 4; ++j) acc[r][j] = 0.f;
+      int k = qkb;
+      for (; k + 8 <= qke; k += 8) {
+        floatx4 w[8];
+#pragma unroll
+        for (int q = 0; q < 8; ++q) w[q] = *reinterpret_cast<const floatx4*>(Wt + (size_t)(k + q) * ldw + n);
+#pragma unroll
+        for (int r = 0; r < R; ++r) {
+#pragma unroll
+          for (int h = 0; h < 2; ++h) {
+            const floatx4 xv = *(const __attribute__((address_space(3))) floatx4*)(X + r * ldx + k + 4 * h);
+#pragma unroll
+            for (int q = 0; q < 4; ++q)
+#pragma unroll
+              for (int j = 0; j < 4; ++j) acc[r][j] = fmaf(xv[q], w[4 * h + q][j], acc[r][j]);
+          }
+        }
+      }
+      for (; k < qke; ++k) {
+        const floatx4 wv = *reinterpret_cast<const floatx4*>(Wt + (size_t)k * ldw + n);
+#pragma unroll
+        for (int r = 0; r < R; ++r)
+#pragma unroll
+          for (int j = 0; j < 4; ++j) acc[r][j] = fmaf(X[r * ldx + k], wv[j], acc[r][j]);
+      }
+#pragma unroll
+      for (int r = 0; r < R; ++r)
+#pragma unroll
+        for (int j = 0; j < 4; ++j) red[(qg * R + r) * N + n + j] = acc[r][j];
+    }
+    __syncthreads();
+    for (int idx = tid; idx < R * N; idx += T) {
+      const int r = idx / N, nn = idx - r * N;
+      float sum = 0.f;
+      for (int gg = 0; gg < QG; ++gg) sum += red[(gg * R + r) * N + nn];
+      Y[r * ldy + nn] = block_act(sum + (b ? b[nn] : 0.f), act);
+    }
+    __syncthreads();
+    return;
+  }
   if (g < G) {
     for (int n = c; n < N; n += cols) {
       float acc[R];
@@ -160,7 +217,7 @@ __global__ __launch_bounds__(256) void linear_rows_kernel(const float* __restric
                                                           float* __restrict__ Xcopy, int ldxc) {
   __shared__ __attribute__((aligned(16))) float sX[R * KMAX];
   __shared__ __attribute__((aligned(16))) float sY[R * 256];
-  __shared__ __attribute__((aligned(16))) float red[R * 256];
+  __shared__ __attribute__((aligned(16))) float red[R * 4 * 256];
   const int tid = threadIdx.x;
   const int r0 = blockIdx.x * R, nr = min(R, B - r0);
   const int col0 = blockIdx.y * cols, nc = min(cols, N - col0);

@@ -29,7 +29,7 @@ __constant__ int kSpeechDims[6] = {56, 512, 512, 256, 128, 64};
 __global__ __launch_bounds__(512) void speech_kernel(SpeechW w, const float* __restrict__ x, int B,
                                                      float* feat, float* logits, float* probs) {
   constexpr int R = SPEECH_R, LD = 512;
-  __shared__ __attribute__((aligned(16))) float bufA[R * LD], bufB[R * LD], red[R * SF_THREADS];
+  __shared__ __attribute__((aligned(16))) float bufA[R * LD], bufB[R * LD], red[4 * R * SF_THREADS];
   const int tid = threadIdx.x;
   const int r0 = blockIdx.x * R;
   const int nr = min(R, B - r0);
@@ -130,9 +130,10 @@ int SpeechModel::forward(const float* x, int B, float* feat, float* logits, floa
 constexpr int FUSION_NP = 70;
 struct FusionW { const float* p[FUSION_NP]; };
 
-constexpr int FUSION_R = 2;
+int g_fusion_r = 2;  // samples per workgroup (mec_set_option "fusion_r": 1, 2, 4, 8)
 constexpr int F_LDIN = 1368, F_LDP = 768, F_LDT = 1280;
 
+template <int FUSION_R>
 __device__ void cross_attention_rows(float* T, int ldt, int nr) {
   // T[r][0:256]=q, [256]=k0, [512]=k1, [768]=v0, [1024]=v1; writes o into T[r][0:256].
   const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
@@ -161,13 +162,14 @@ __device__ void cross_attention_rows(float* T, int ldt, int nr) {
   __syncthreads();
 }
 
+template <int FUSION_R>
 __global__ __launch_bounds__(512) void fusion_kernel(FusionW w, const float* __restrict__ sf,
                                                      const float* __restrict__ tf, const float* __restrict__ imf,
                                                      const float* __restrict__ sp, const float* __restrict__ tp,
                                                      const float* __restrict__ ip, int B, float* logits,
                                                      float* probs, float* attn_w, float* dec_w) {
   constexpr int R = FUSION_R;
-  __shared__ __attribute__((aligned(16))) float IN[R * F_LDIN], P[R * F_LDP], E[R * F_LDP], T[R * F_LDT], red[R * SF_THREADS];
+  __shared__ __attribute__((aligned(16))) float IN[R * F_LDIN], P[R * F_LDP], E[R * F_LDP], T[R * F_LDT], red[4 * R * SF_THREADS];
   const int tid = threadIdx.x, T_ = blockDim.x;
   const int r0 = blockIdx.x * R;
   const int nr = min(R, B - r0);
@@ -201,7 +203,7 @@ __global__ __launch_bounds__(512) void fusion_kernel(FusionW w, const float* __r
     block_linear<R>(P + 256 * others[m][1], F_LDP, 256, c[2], 256, c[3], 256, T + 512, F_LDT, red, BACT_NONE);
     block_linear<R>(P + 256 * others[m][0], F_LDP, 256, c[4], 256, c[5], 256, T + 768, F_LDT, red, BACT_NONE);
     block_linear<R>(P + 256 * others[m][1], F_LDP, 256, c[4], 256, c[5], 256, T + 1024, F_LDT, red, BACT_NONE);
-    cross_attention_rows(T, F_LDT, nr);
+    cross_attention_rows<FUSION_R>(T, F_LDT, nr);
     block_linear<R>(T, F_LDT, 256, c[6], 256, c[7], 256, E + 256 * m, F_LDP, red, BACT_NONE);
     for (int idx = tid; idx < R * 256; idx += T_) {
       const int r = idx >> 8, n = idx & 255;
@@ -322,8 +324,13 @@ int FusionModel::forward(const float* sf, const float* tf, const float* imf, con
   const float* base = w.as<float>();
   for (int i = 0; i < FUSION_NP; ++i) p.p[i] = base + off[i];
   MEC_TRY(prof.begin(TAG_FUSION, s));
-  hipLaunchKernelGGL(fusion_kernel, dim3((B + FUSION_R - 1) / FUSION_R), dim3(SF_THREADS), 0, s, p, sf, tf, imf, sp,
-                     tp, ip, B, logits, probs, attn_w, dec_w);
+  const int R = g_fusion_r;
+  const dim3 grid((B + R - 1) / R), blk(SF_THREADS);
+  switch (R) {
+    case 1: hipLaunchKernelGGL((fusion_kernel<1>), grid, blk, 0, s, p, sf, tf, imf, sp, tp, ip, B, logits, probs, attn_w, dec_w); break;
+    case 4: hipLaunchKernelGGL((fusion_kernel<4>), grid, blk, 0, s, p, sf, tf, imf, sp, tp, ip, B, logits, probs, attn_w, dec_w); break;
+    default: hipLaunchKernelGGL((fusion_kernel<2>), grid, blk, 0, s, p, sf, tf, imf, sp, tp, ip, B, logits, probs, attn_w, dec_w); break;
+  }
   MEC_LAUNCH_CHECK();
   MEC_TRY(prof.end(TAG_FUSION, s));
   return 0;

@@ -1,0 +1,24 @@
+"""Microbenchmark of the fp32 block kernels (fusion, speech) at B=256 across options."""
+import sys, os, ctypes
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, os.path.join(ROOT, 'multimodal-emotion-classification_amd'))
+import torch
+from mec import engine, synthetic as syn, _lib
+dev = torch.device('cuda', 0)
+B = 256
+fu = engine.FusionHead(device=dev)
+sp = engine.SpeechEncoder(device=dev)
+args = [torch.rand(B, d, device=dev) for d in (64, 768, 512, 7, 7, 7)]
+x = engine.to_device(syn.speech_inputs(B, seed=1), dev)
+lib = _lib.load()
+def t(fn, it=20):
+    fn(); torch.cuda.synchronize()
+    e0, e1 = torch.cuda.Event(True), torch.cuda.Event(True)
+    e0.record()
+    for _ in range(it): fn()
+    e1.record(); torch.cuda.synchronize(); return e0.elapsed_time(e1) / it * 1e3
+for r in (1, 2, 4):
+    lib.mec_set_option(b'fusion_r', r)
+    print('fusion R=%d  %.1f us' % (r, t(lambda: fu.forward(*args))))
+lib.mec_set_option(b'fusion_r', 2)
+print('speech %.1f us' % t(lambda: sp.forward(x)))
