@@ -31,19 +31,24 @@ __device__ __attribute__((aligned(64))) uint4 g_zero_page[16];
 
 __device__ __forceinline__ int sw(int row, int kc) { return kc ^ ((row >> 1) & 7); }
 
-// GELU(x) = x/2 (1 + erf(x/sqrt2)) (HF "gelu"). erf by Abramowitz-Stegun 7.1.26:
-// |err| <= 1.5e-7 absolute (checked over [-12, 12]), i.e. far below the f16 rounding of
-// the FFN1 output; one v_rcp + one v_exp instead of ocml's branchy erff.
-__device__ __forceinline__ float gelu_erf2(float x) {
-  const float z = x * 0.70710678118654752440f;
-  const float az = fabsf(z);
-  const float t = __frcp_rn(fmaf(0.3275911f, az, 1.0f));
-  float poly = fmaf(1.061405429f, t, -1.453152027f);
-  poly = fmaf(poly, t, 1.421413741f);
-  poly = fmaf(poly, t, -0.284496736f);
-  poly = fmaf(poly, t, 0.254829592f);
-  const float e = 1.0f - poly * t * __expf(-az * az);
-  return 0.5f * x * (1.0f + copysignf(e, z));
+// GELU(x) = x/2 (1 + erf(x/sqrt2)) (HF "gelu"), erf by Abramowitz-Stegun 7.1.26
+// (|err| <= 1.5e-7 absolute over [-12, 12], far below the f16 rounding of FFN1's output).
+// With z = |x|/sqrt2: erf(z) = 1 - t P(t) exp(-z^2), t = 1/(1 + p z), so
+//   GELU(x) = 0.5 (x + |x| (1 - t P(t) exp2(-x^2 log2(e)/2)))      (no sign select)
+// evaluated on pairs with packed f32 math; v_rcp / v_exp are the raw instructions.
+typedef float f32x2 __attribute__((ext_vector_type(2)));
+__device__ __forceinline__ f32x2 gelu_erf_x2(f32x2 x) {
+  const f32x2 ax = {fabsf(x.x), fabsf(x.y)};
+  const f32x2 d = ax * 0.23164189f + 1.0f;                 // 1 + (0.3275911/sqrt2) |x|
+  const f32x2 t = {__builtin_amdgcn_rcpf(d.x), __builtin_amdgcn_rcpf(d.y)};
+  const f32x2 a = (x * x) * -0.72134752f;                  // -x^2 log2(e) / 2
+  const f32x2 e = {__builtin_amdgcn_exp2f(a.x), __builtin_amdgcn_exp2f(a.y)};
+  f32x2 p = t * 1.061405429f - 1.453152027f;
+  p = p * t + 1.421413741f;
+  p = p * t - 0.284496736f;
+  p = p * t + 0.254829592f;
+  const f32x2 q = 1.0f - (p * t) * e;
+  return (ax * q + x) * 0.5f;
 }
 
 template <int N>
@@ -341,7 +346,11 @@ __global__ __launch_bounds__(64 * WM * WN) void gemm_glds_kernel(const GemmParam
         for (int q = 0; q < 8; ++q) v[q] = fmaxf(v[q], 0.f);
       } else if (p.act == ACT_GELU) {
 #pragma unroll
-        for (int q = 0; q < 8; ++q) v[q] = gelu_erf2(v[q]);
+        for (int q = 0; q < 8; q += 2) {
+          const f32x2 r = gelu_erf_x2(f32x2{v[q], v[q + 1]});
+          v[q] = r.x;
+          v[q + 1] = r.y;
+        }
       }
       if (row < M) {
         const size_t base = (size_t)row * N + col0;
@@ -368,11 +377,11 @@ template <int BM, int BN, int WM, int WN, int NS, int MF = 32>
 static int launch_cfg(const GemmParams& p, hipStream_t s) {
   const int nwg = ((p.M + BM - 1) / BM) * (p.N / BN);
   const dim3 blk(64 * WM * WN);
-  if (g_gemm_debug && BN == 256 && p.amode == A_PLAIN) {
+  if (g_gemm_debug && BN == 256 && BM == 256 && p.amode == A_PLAIN) {
     if (g_gemm_debug == 1)
-      hipLaunchKernelGGL((gemm_glds_kernel<BM, BN, WM, WN, NS, A_PLAIN, 1>), dim3(nwg), blk, 0, s, p);
+      hipLaunchKernelGGL((gemm_glds_kernel<BM, BN, WM, WN, NS, A_PLAIN, 1, MF>), dim3(nwg), blk, 0, s, p);
     else
-      hipLaunchKernelGGL((gemm_glds_kernel<BM, BN, WM, WN, NS, A_PLAIN, 2>), dim3(nwg), blk, 0, s, p);
+      hipLaunchKernelGGL((gemm_glds_kernel<BM, BN, WM, WN, NS, A_PLAIN, 2, MF>), dim3(nwg), blk, 0, s, p);
   } else if (p.amode == A_PLAIN)
     hipLaunchKernelGGL((gemm_glds_kernel<BM, BN, WM, WN, NS, A_PLAIN, 0, MF>), dim3(nwg), blk, 0, s, p);
   else if (p.amode == A_DUAL)

@@ -24,6 +24,7 @@ SHAPES = [
     ('bert_oproj', 'gemm', B * 128, 768, 768, 0, 1),
     ('bert_ffn1', 'gemm', B * 128, 3072, 768, 2, 0),
     ('bert_ffn2', 'gemm', B * 128, 768, 3072, 0, 1),
+    ('bert_ffn1_noact', 'gemm', B * 128, 3072, 768, 0, 0),
     ('l1_c1', 'gemm', B * 56 * 56, 64, 256, 1, 0),
     ('l1_c3', 'gemm', B * 56 * 56, 256, 64, 1, 2),
     ('l2_c1', 'gemm', B * 28 * 28, 128, 512, 1, 0),
