@@ -29,7 +29,14 @@ typedef __attribute__((address_space(3))) void* lds_vptr;
 
 __device__ __attribute__((aligned(64))) uint4 g_zero_page[16];
 
-__device__ __forceinline__ int sw(int row, int kc) { return kc ^ ((row >> 1) & 7); }
+// LDS chunk swizzle (16-B chunks): BK=64 rows are 128 B, BK=32 rows are 64 B. Both make
+// every ds_read_b128 lane group of the 32x32x16 and 16x16x32 fragment reads cover the 16
+// slots of a 256-B bank row (MI355X_MICROARCH.md, LDS lane groups).
+template <int BK>
+__device__ __forceinline__ int sw(int row, int kc) {
+  if constexpr (BK == 64) return kc ^ ((row >> 1) & 7);
+  else return kc ^ ((4 - ((row >> 2) & 3)) & 3);
+}
 
 // GELU(x) = x/2 (1 + erf(x/sqrt2)) (HF "gelu"), erf by Abramowitz-Stegun 7.1.26
 // (|err| <= 1.5e-7 absolute over [-12, 12], far below the f16 rounding of FFN1's output).
@@ -56,217 +63,16 @@ __device__ __forceinline__ void wait_vm() {
   asm volatile("s_waitcnt vmcnt(%0)" ::"n"(N) : "memory");
 }
 
-template <int BM, int BN, int WM, int WN, int NS, int AM, int DBG = 0, int MF = 32>
-__global__ __launch_bounds__(64 * WM * WN) void gemm_glds_kernel(const GemmParams p) {
-  // MF: 32 = v_mfma_f32_32x32x16_f16 tiles, 16 = v_mfma_f32_16x16x32_f16 tiles
-  // DBG (probe builds only): 1 = no operand loads inside the K loop, 2 = no epilogue
-  constexpr int BK = 64;
-  constexpr int NW = WM * WN;
-  static_assert(NW == 8 || NW == 4, "4 or 8 waves");
-  constexpr int TM = BM / WM, TN = BN / WN;    // wave tile
-  constexpr int TI = TM / MF, TJ = TN / MF;    // MFxMF MFMA tiles per wave
-  typedef float accv __attribute__((ext_vector_type(MF == 32 ? 16 : 4)));
-  constexpr int NACC = MF == 32 ? 16 : 4;
-  constexpr int AI = BM / 8 / NW;              // glds wave-instructions per stage (A)
-  constexpr int BI = BN / 8 / NW;              // (B)
-  static_assert(BI >= 1 && AI >= 1, "tile too small for 8 waves");
-  constexpr int LPT = AI + BI;
-  constexpr int STAGE = (BM + BN) * BK;        // halfs per stage
-  constexpr int EPI_LD = TN + 4;               // f32 staging row (padded)
-  constexpr int EPI = NW * 32 * EPI_LD;        // floats for the epilogue staging
-  constexpr int SMEM_H = (NS * STAGE > EPI * 2) ? NS * STAGE : EPI * 2;
-  __shared__ __attribute__((aligned(16))) f16 smem[SMEM_H];
-
-  const int tid = threadIdx.x, lane = tid & 63;
-  const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
-  const int wm = wave / WN, wn = wave - (wave / WN) * WN;
-  const int M = p.M, N = p.N, K = p.K;
-  const int nbn = N / BN;
-  const int nbm = (M + BM - 1) / BM;
-  const int nwg = nbm * nbn;
-  int bid = blockIdx.x;
-  {
-    const int xcd = bid & 7, q = nwg >> 3, r = nwg & 7;
-    bid = (xcd < r ? xcd * (q + 1) : r * (q + 1) + (xcd - r) * q) + (bid >> 3);
-  }
-  const int bm = bid / nbn, bn = bid - (bid / nbn) * nbn;
-  const int m0 = bm * BM, n0 = bn * BN;
-
-  // ---- per-lane DMA sources: lane -> (row in its 8-row group, physical chunk)
-  const int lrow = lane >> 3, pchunk = lane & 7;
-  const f16* a_src[AI];
-  const f16* a2_src[AI];  // A_DUAL: second source (1x1 / stride-s view of an NHWC tensor)
-  int a_ih0[AI], a_iw0[AI];
-  bool a_ok[AI];
-#pragma unroll
-  for (int i = 0; i < AI; ++i) {
-    const int r = (wave * AI + i) * 8 + lrow;  // row within tile
-    const int m = m0 + r;
-    a_ok[i] = m < M;
-    const int mc = a_ok[i] ? m : 0;
-    const int kc = pchunk ^ ((r >> 1) & 7);
-    if constexpr (AM == A_PLAIN) {
-      a_src[i] = reinterpret_cast<const f16*>(p.A) + (size_t)mc * K + kc * 8;
-    } else if constexpr (AM == A_DUAL) {
-      a_src[i] = reinterpret_cast<const f16*>(p.A) + (size_t)mc * p.K1 + kc * 8;
-      const int ohw = p.OH * p.OW;
-      const int n = mc / ohw;
-      const int rem = mc - n * ohw;
-      const int oh = rem / p.OW;
-      const int ow = rem - oh * p.OW;
-      a2_src[i] = reinterpret_cast<const f16*>(p.A2) +
-                  (((size_t)n * p.H + oh * p.stride) * p.W + ow * p.stride) * p.C + kc * 8;
-    } else {
-      const int ohw = p.OH * p.OW;
-      const int n = mc / ohw;
-      const int rem = mc - n * ohw;
-      const int oh = rem / p.OW;
-      const int ow = rem - oh * p.OW;
-      a_ih0[i] = oh * p.stride - p.pad;
-      a_iw0[i] = ow * p.stride - p.pad;
-      a_src[i] = reinterpret_cast<const f16*>(p.A) + (size_t)n * p.H * p.W * p.C + kc * 8;
-    }
-  }
-  const f16* b_src[BI];
-#pragma unroll
-  for (int j = 0; j < BI; ++j) {
-    const int r = (wave * BI + j) * 8 + lrow;
-    const int kc = pchunk ^ ((r >> 1) & 7);
-    b_src[j] = p.B + (size_t)(n0 + r) * K + kc * 8;
-  }
-  const f16* zero = reinterpret_cast<const f16*>(g_zero_page);
-
-  auto issue = [&](int stage, int kt) {
-    const int k0 = kt * BK;
-    f16* sA = smem + stage * STAGE;
-    f16* sB = sA + BM * BK;
-    if constexpr (AM == A_PLAIN) {
-#pragma unroll
-      for (int i = 0; i < AI; ++i) {
-        const f16* src = a_ok[i] ? a_src[i] + k0 : zero;
-        __builtin_amdgcn_global_load_lds((const void*)src, (lds_vptr)(sA + (wave * AI + i) * 8 * BK), 16, 0, 0);
-      }
-    } else if constexpr (AM == A_DUAL) {
-      const bool first = k0 < p.K1;
-#pragma unroll
-      for (int i = 0; i < AI; ++i) {
-        const f16* src = !a_ok[i] ? zero : (first ? a_src[i] + k0 : a2_src[i] + (k0 - p.K1));
-        __builtin_amdgcn_global_load_lds((const void*)src, (lds_vptr)(sA + (wave * AI + i) * 8 * BK), 16, 0, 0);
-      }
-    } else {
-      const int tap = k0 / p.C;
-      const int c0 = k0 - tap * p.C;
-      const int kh = tap / p.ks;
-      const int kw = tap - kh * p.ks;
-#pragma unroll
-      for (int i = 0; i < AI; ++i) {
-        const int ih = a_ih0[i] + kh, iw = a_iw0[i] + kw;
-        const bool ok = a_ok[i] && ih >= 0 && ih < p.H && iw >= 0 && iw < p.W;
-        const f16* src = ok ? a_src[i] + ((size_t)ih * p.W + iw) * p.C + c0 : zero;
-        __builtin_amdgcn_global_load_lds((const void*)src, (lds_vptr)(sA + (wave * AI + i) * 8 * BK), 16, 0, 0);
-      }
-    }
-#pragma unroll
-    for (int j = 0; j < BI; ++j)
-      __builtin_amdgcn_global_load_lds((const void*)(b_src[j] + k0), (lds_vptr)(sB + (wave * BI + j) * 8 * BK), 16,
-                                       0, 0);
-  };
-
-  accv acc[TI][TJ];
-#pragma unroll
-  for (int i = 0; i < TI; ++i)
-#pragma unroll
-    for (int j = 0; j < TJ; ++j)
-#pragma unroll
-      for (int e = 0; e < NACC; ++e) acc[i][j][e] = 0.f;
-
-  const int nk = K / BK;
-#pragma unroll
-  for (int s = 0; s < NS - 1; ++s)
-    if (s < nk) issue(s, s);
-
+// Shared epilogue: accumulators (16x16x32 or 32x32x16 layout, wave tile (BM/WM)x(BN/WN))
+// -> bias, residual, activation -> C16 / C32. `smem` must be free (all waves past the
+// main loop's last LDS read).
+template <int BM, int BN, int WM, int WN, int MF, typename accv, int TI, int TJ>
+__device__ __forceinline__ void gemm_epilogue(const GemmParams& p, accv (&acc)[TI][TJ], f16* smem, int m0, int n0,
+                                              int wm, int wn, int wave, int lane) {
+  constexpr int TM = BM / WM, TN = BN / WN;
+  constexpr int EPI_LD = TN + 4;
+  const int M = p.M, N = p.N;
   const int lr = lane & 31, lh = lane >> 5;
-  for (int t = 0; t < nk; ++t) {
-    // tile t must have landed; tiles t+1..t+NS-2 (if issued) may stay in flight
-    const int ahead = min(nk - 1 - t, NS - 2);
-    if constexpr (NS >= 3) {
-      if (ahead >= 1) wait_vm<LPT * (NS - 2)>();
-      else wait_vm<0>();
-    } else {
-      wait_vm<0>();
-    }
-    (void)ahead;
-    __builtin_amdgcn_s_barrier();
-    asm volatile("" ::: "memory");
-    if (DBG != 1 && t + NS - 1 < nk) issue((t + NS - 1) % NS, t + NS - 1);
-    const f16* sA = smem + ((DBG == 1 ? 0 : t) % NS) * STAGE;
-    const f16* sB = sA + BM * BK;
-    if constexpr (MF == 32) {
-#pragma unroll
-      for (int s = 0; s < 4; ++s) {
-        const int kcs = 2 * s + lh;
-        half8 af[TI], bf[TJ];
-#pragma unroll
-        for (int i = 0; i < TI; ++i) {
-          const int r = wm * TM + i * 32 + lr;
-          af[i] = *reinterpret_cast<const half8*>(sA + r * BK + sw(r, kcs) * 8);
-        }
-#pragma unroll
-        for (int j = 0; j < TJ; ++j) {
-          const int r = wn * TN + j * 32 + lr;
-          bf[j] = *reinterpret_cast<const half8*>(sB + r * BK + sw(r, kcs) * 8);
-        }
-#pragma unroll
-        for (int i = 0; i < TI; ++i)
-#pragma unroll
-          for (int j = 0; j < TJ; ++j)
-            acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_f16(af[i], bf[j], acc[i][j], 0, 0, 0);
-      }
-    } else {
-      // 16x16x32: lane l holds A[row l&15][k 8(l>>4)..+7] of each 32-deep k step. Both
-      // k steps' fragments are requested up front, so the second step's LDS reads are in
-      // flight under the first step's MFMAs (counted lgkmcnt instead of a drain per group).
-      const int l16 = lane & 15, lq = lane >> 4;
-      half8 af[2][TI], bf[2][TJ];
-#pragma unroll
-      for (int s = 0; s < 2; ++s) {
-        const int kcs = 4 * s + lq;
-#pragma unroll
-        for (int i = 0; i < TI; ++i) {
-          const int r = wm * TM + i * 16 + l16;
-          af[s][i] = *reinterpret_cast<const half8*>(sA + r * BK + sw(r, kcs) * 8);
-        }
-#pragma unroll
-        for (int j = 0; j < TJ; ++j) {
-          const int r = wn * TN + j * 16 + l16;
-          bf[s][j] = *reinterpret_cast<const half8*>(sB + r * BK + sw(r, kcs) * 8);
-        }
-      }
-      __builtin_amdgcn_sched_barrier(0);  // keep all fragment reads ahead of the MFMAs
-#pragma unroll
-      for (int s = 0; s < 2; ++s)
-#pragma unroll
-        for (int i = 0; i < TI; ++i)
-#pragma unroll
-          for (int j = 0; j < TJ; ++j)
-            acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_f16(af[s][i], bf[s][j], acc[i][j], 0, 0, 0);
-    }
-  }
-  asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)" ::: "memory");
-  __builtin_amdgcn_s_barrier();
-  asm volatile("" ::: "memory");
-
-  if constexpr (DBG == 2) {
-    float s = 0.f;
-#pragma unroll
-    for (int i = 0; i < TI; ++i)
-#pragma unroll
-      for (int j = 0; j < TJ; ++j)
-#pragma unroll
-        for (int e = 0; e < NACC; ++e) s += acc[i][j][e];
-    if (s == 12345.678f) p.C32[0] = s;  // keeps the accumulators live
-    return;
-  }
   // ---- epilogue: per wave, 32-row slabs staged through LDS (f32), then written with
   // 8-element chunks where consecutive lanes cover consecutive 16-B pieces of a row
   // (CPR lanes per row), so every store / residual load instruction covers whole lines.
@@ -370,24 +176,420 @@ __global__ __launch_bounds__(64 * WM * WN) void gemm_glds_kernel(const GemmParam
   }
 }
 
+template <int BM, int BN, int WM, int WN, int NS, int AM, int DBG = 0, int MF = 32, int BK = 64>
+__global__ __launch_bounds__(64 * WM * WN, (WM * WN == 4) ? 2 : 1) void gemm_glds_kernel(const GemmParams p) {
+  // MF: 32 = v_mfma_f32_32x32x16_f16 tiles, 16 = v_mfma_f32_16x16x32_f16 tiles
+  // DBG (probe builds only): 1 = no operand loads inside the K loop, 2 = no epilogue
+  static_assert(BK == 64 || BK == 32, "BK");
+  constexpr int CH = BK / 8;                   // 16-B chunks per LDS row
+  constexpr int RPI = 64 / CH;                 // rows per glds wave-instruction (1 KB)
+  constexpr int NW = WM * WN;
+  static_assert(NW == 8 || NW == 4, "4 or 8 waves");
+  constexpr int TM = BM / WM, TN = BN / WN;    // wave tile
+  constexpr int TI = TM / MF, TJ = TN / MF;    // MFxMF MFMA tiles per wave
+  typedef float accv __attribute__((ext_vector_type(MF == 32 ? 16 : 4)));
+  constexpr int NACC = MF == 32 ? 16 : 4;
+  constexpr int AI = BM / RPI / NW;            // glds wave-instructions per stage (A)
+  constexpr int BI = BN / RPI / NW;            // (B)
+  static_assert(BI >= 1 && AI >= 1, "tile too small for 8 waves");
+  constexpr int LPT = AI + BI;
+  constexpr int STAGE = (BM + BN) * BK;        // halfs per stage
+  constexpr int EPI_LD = TN + 4;               // f32 staging row (padded)
+  constexpr int EPI = NW * 32 * EPI_LD;        // floats for the epilogue staging
+  constexpr int SMEM_H = (NS * STAGE > EPI * 2) ? NS * STAGE : EPI * 2;
+  __shared__ __attribute__((aligned(16))) f16 smem[SMEM_H];
+
+  const int tid = threadIdx.x, lane = tid & 63;
+  const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int wm = wave / WN, wn = wave - (wave / WN) * WN;
+  const int M = p.M, N = p.N, K = p.K;
+  const int nbn = N / BN;
+  const int nbm = (M + BM - 1) / BM;
+  const int nwg = nbm * nbn;
+  int bid = blockIdx.x;
+  {
+    const int xcd = bid & 7, q = nwg >> 3, r = nwg & 7;
+    bid = (xcd < r ? xcd * (q + 1) : r * (q + 1) + (xcd - r) * q) + (bid >> 3);
+  }
+  const int bm = bid / nbn, bn = bid - (bid / nbn) * nbn;
+  const int m0 = bm * BM, n0 = bn * BN;
+
+  // ---- per-lane DMA sources: lane -> (row in its 8-row group, physical chunk)
+  const int lrow = lane / CH, pchunk = lane % CH;
+  const f16* a_src[AI];
+  const f16* a2_src[AI];  // A_DUAL: second source (1x1 / stride-s view of an NHWC tensor)
+  int a_ih0[AI], a_iw0[AI];
+  bool a_ok[AI];
+#pragma unroll
+  for (int i = 0; i < AI; ++i) {
+    const int r = (wave * AI + i) * RPI + lrow;  // row within tile
+    const int m = m0 + r;
+    a_ok[i] = m < M;
+    const int mc = a_ok[i] ? m : 0;
+    const int kc = sw<BK>(r, pchunk);
+    if constexpr (AM == A_PLAIN) {
+      a_src[i] = reinterpret_cast<const f16*>(p.A) + (size_t)mc * K + kc * 8;
+    } else if constexpr (AM == A_DUAL) {
+      a_src[i] = reinterpret_cast<const f16*>(p.A) + (size_t)mc * p.K1 + kc * 8;
+      const int ohw = p.OH * p.OW;
+      const int n = mc / ohw;
+      const int rem = mc - n * ohw;
+      const int oh = rem / p.OW;
+      const int ow = rem - oh * p.OW;
+      a2_src[i] = reinterpret_cast<const f16*>(p.A2) +
+                  (((size_t)n * p.H + oh * p.stride) * p.W + ow * p.stride) * p.C + kc * 8;
+    } else {
+      const int ohw = p.OH * p.OW;
+      const int n = mc / ohw;
+      const int rem = mc - n * ohw;
+      const int oh = rem / p.OW;
+      const int ow = rem - oh * p.OW;
+      a_ih0[i] = oh * p.stride - p.pad;
+      a_iw0[i] = ow * p.stride - p.pad;
+      a_src[i] = reinterpret_cast<const f16*>(p.A) + (size_t)n * p.H * p.W * p.C + kc * 8;
+    }
+  }
+  const f16* b_src[BI];
+#pragma unroll
+  for (int j = 0; j < BI; ++j) {
+    const int r = (wave * BI + j) * RPI + lrow;
+    const int kc = sw<BK>(r, pchunk);
+    b_src[j] = p.B + (size_t)(n0 + r) * K + kc * 8;
+  }
+  const f16* zero = reinterpret_cast<const f16*>(g_zero_page);
+
+  auto issue = [&](int stage, int kt) {
+    const int k0 = kt * BK;
+    f16* sA = smem + stage * STAGE;
+    f16* sB = sA + BM * BK;
+    if constexpr (AM == A_PLAIN) {
+#pragma unroll
+      for (int i = 0; i < AI; ++i) {
+        const f16* src = a_ok[i] ? a_src[i] + k0 : zero;
+        __builtin_amdgcn_global_load_lds((const void*)src, (lds_vptr)(sA + (wave * AI + i) * RPI * BK), 16, 0, 0);
+      }
+    } else if constexpr (AM == A_DUAL) {
+      const bool first = k0 < p.K1;
+#pragma unroll
+      for (int i = 0; i < AI; ++i) {
+        const f16* src = !a_ok[i] ? zero : (first ? a_src[i] + k0 : a2_src[i] + (k0 - p.K1));
+        __builtin_amdgcn_global_load_lds((const void*)src, (lds_vptr)(sA + (wave * AI + i) * RPI * BK), 16, 0, 0);
+      }
+    } else {
+      const int tap = k0 / p.C;
+      const int c0 = k0 - tap * p.C;
+      const int kh = tap / p.ks;
+      const int kw = tap - kh * p.ks;
+#pragma unroll
+      for (int i = 0; i < AI; ++i) {
+        const int ih = a_ih0[i] + kh, iw = a_iw0[i] + kw;
+        const bool ok = a_ok[i] && ih >= 0 && ih < p.H && iw >= 0 && iw < p.W;
+        const f16* src = ok ? a_src[i] + ((size_t)ih * p.W + iw) * p.C + c0 : zero;
+        __builtin_amdgcn_global_load_lds((const void*)src, (lds_vptr)(sA + (wave * AI + i) * RPI * BK), 16, 0, 0);
+      }
+    }
+#pragma unroll
+    for (int j = 0; j < BI; ++j)
+      __builtin_amdgcn_global_load_lds((const void*)(b_src[j] + k0), (lds_vptr)(sB + (wave * BI + j) * RPI * BK), 16,
+                                       0, 0);
+  };
+
+  accv acc[TI][TJ];
+#pragma unroll
+  for (int i = 0; i < TI; ++i)
+#pragma unroll
+    for (int j = 0; j < TJ; ++j)
+#pragma unroll
+      for (int e = 0; e < NACC; ++e) acc[i][j][e] = 0.f;
+
+  const int nk = K / BK;
+#pragma unroll
+  for (int s = 0; s < NS - 1; ++s)
+    if (s < nk) issue(s, s);
+
+  const int lr = lane & 31, lh = lane >> 5;
+  for (int t = 0; t < nk; ++t) {
+    // tile t must have landed; tiles t+1..t+ahead (issued) may stay in flight
+    const int ahead = min(nk - 1 - t, NS - 2);
+    if constexpr (NS >= 5) {
+      if (ahead >= 3) wait_vm<LPT * 3>();
+      else if (ahead == 2) wait_vm<LPT * 2>();
+      else if (ahead == 1) wait_vm<LPT>();
+      else wait_vm<0>();
+    } else if constexpr (NS == 4) {
+      if (ahead >= 2) wait_vm<LPT * 2>();
+      else if (ahead == 1) wait_vm<LPT>();
+      else wait_vm<0>();
+    } else if constexpr (NS == 3) {
+      if (ahead >= 1) wait_vm<LPT>();
+      else wait_vm<0>();
+    } else {
+      wait_vm<0>();
+    }
+    (void)ahead;
+    __builtin_amdgcn_s_barrier();
+    asm volatile("" ::: "memory");
+    if (DBG != 1 && t + NS - 1 < nk) issue((t + NS - 1) % NS, t + NS - 1);
+    const f16* sA = smem + ((DBG == 1 ? 0 : t) % NS) * STAGE;
+    const f16* sB = sA + BM * BK;
+    if constexpr (MF == 32) {
+#pragma unroll
+      for (int s = 0; s < BK / 16; ++s) {
+        const int kcs = 2 * s + lh;
+        half8 af[TI], bf[TJ];
+#pragma unroll
+        for (int i = 0; i < TI; ++i) {
+          const int r = wm * TM + i * 32 + lr;
+          af[i] = *reinterpret_cast<const half8*>(sA + r * BK + sw<BK>(r, kcs) * 8);
+        }
+#pragma unroll
+        for (int j = 0; j < TJ; ++j) {
+          const int r = wn * TN + j * 32 + lr;
+          bf[j] = *reinterpret_cast<const half8*>(sB + r * BK + sw<BK>(r, kcs) * 8);
+        }
+#pragma unroll
+        for (int i = 0; i < TI; ++i)
+#pragma unroll
+          for (int j = 0; j < TJ; ++j)
+            acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_f16(af[i], bf[j], acc[i][j], 0, 0, 0);
+      }
+    } else {
+      // 16x16x32: lane l holds A[row l&15][k 8(l>>4)..+7] of each 32-deep k step. Both
+      // k steps' fragments are requested up front, so the second step's LDS reads are in
+      // flight under the first step's MFMAs (counted lgkmcnt instead of a drain per group).
+      const int l16 = lane & 15, lq = lane >> 4;
+      constexpr int KS = BK / 32;
+      half8 af[KS][TI], bf[KS][TJ];
+#pragma unroll
+      for (int s = 0; s < KS; ++s) {
+        const int kcs = 4 * s + lq;
+#pragma unroll
+        for (int i = 0; i < TI; ++i) {
+          const int r = wm * TM + i * 16 + l16;
+          af[s][i] = *reinterpret_cast<const half8*>(sA + r * BK + sw<BK>(r, kcs) * 8);
+        }
+#pragma unroll
+        for (int j = 0; j < TJ; ++j) {
+          const int r = wn * TN + j * 16 + l16;
+          bf[s][j] = *reinterpret_cast<const half8*>(sB + r * BK + sw<BK>(r, kcs) * 8);
+        }
+      }
+      __builtin_amdgcn_sched_barrier(0);  // keep all fragment reads ahead of the MFMAs
+#pragma unroll
+      for (int s = 0; s < KS; ++s)
+#pragma unroll
+        for (int i = 0; i < TI; ++i)
+#pragma unroll
+          for (int j = 0; j < TJ; ++j)
+            acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_f16(af[s][i], bf[s][j], acc[i][j], 0, 0, 0);
+    }
+  }
+  asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)" ::: "memory");
+  __builtin_amdgcn_s_barrier();
+  asm volatile("" ::: "memory");
+
+  if constexpr (DBG == 2) {
+    float s = 0.f;
+#pragma unroll
+    for (int i = 0; i < TI; ++i)
+#pragma unroll
+      for (int j = 0; j < TJ; ++j)
+#pragma unroll
+        for (int e = 0; e < NACC; ++e) s += acc[i][j][e];
+    if (s == 12345.678f) p.C32[0] = s;  // keeps the accumulators live
+    return;
+  }
+  gemm_epilogue<BM, BN, WM, WN, MF>(p, acc, smem, m0, n0, wm, wn, wave, lane);
+}
+
+
+// ---- 256x256x64 ping-pong GEMM (A_PLAIN), v_mfma_f32_16x16x32_f16, 8 waves (2 x 4).
+// Each K tile lives in one of two LDS buffers as four 16-KB pieces: A0/A1 = the 64-row
+// halves of both wave rows' 128-row strips, B0/B1 = the 32-column halves of the four wave
+// columns. A K tile is consumed in four phases, one output quadrant each:
+//   ph0 (A0,B0)  ph1 (A0,B1)  ph2 (A1,B1)  ph3 (A1,B0)
+// so the pieces fall free in the order A0, B1, A1, B0 and each is restaged for tile t+2
+// (same buffer) one phase after its last read: ph1 A0, ph2 B1, ph3 A1, next ph0 B0.
+// Every phase: ds_read its fragments + issue one piece (2 glds per lane), retire the
+// reads (lgkmcnt(0)) BEFORE the first barrier, then 16 MFMAs between two barriers. The
+// second wave row runs one barrier behind the first, so on each SIMD one wave is in its
+// MFMA section while its partner loads. ph3 waits vmcnt(6): everything but the three
+// pieces issued for tile t+2 has landed, i.e. all of tile t+1, read one phase later.
+// Same k order per output as every other tile, so results are bit-identical to them.
+template <int AM, int DBG = 0>
+__global__ __launch_bounds__(512) void gemm_pp_kernel(const GemmParams p) {
+  static_assert(AM == A_PLAIN, "ping-pong tile: plain A only");
+  constexpr int BM = 256, BN = 256, BK = 64, WM = 2, WN = 4;
+  constexpr int PIECE = 128 * BK;  // halfs
+  typedef float accv __attribute__((ext_vector_type(4)));
+  __shared__ __attribute__((aligned(16))) f16 smem[8 * PIECE];
+
+  const int tid = threadIdx.x, lane = tid & 63;
+  const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int wm = wave / WN, wn = wave - (wave / WN) * WN;
+  const int M = p.M, N = p.N, K = p.K;
+  const int nbn = N / BN;
+  const int nbm = (M + BM - 1) / BM;
+  const int nwg = nbm * nbn;
+  int bid = blockIdx.x;
+  {
+    const int xcd = bid & 7, q = nwg >> 3, r = nwg & 7;
+    bid = (xcd < r ? xcd * (q + 1) : r * (q + 1) + (xcd - r) * q) + (bid >> 3);
+  }
+  const int bm = bid / nbn, bn = bid - (bid / nbn) * nbn;
+  const int m0 = bm * BM, n0 = bn * BN;
+
+  const int lrow = lane >> 3, pchunk = lane & 7;
+  const f16* a_src[2][2];
+  const f16* b_src[2][2];
+  bool a_ok[2][2];
+#pragma unroll
+  for (int h = 0; h < 2; ++h)
+#pragma unroll
+    for (int i = 0; i < 2; ++i) {
+      const int pr = (wave * 2 + i) * 8 + lrow;  // piece-local row 0..127
+      const int kc = sw<64>(pr, pchunk);
+      const int m = m0 + (pr >> 6) * 128 + h * 64 + (pr & 63);
+      a_ok[h][i] = m < M;
+      a_src[h][i] = reinterpret_cast<const f16*>(p.A) + (size_t)(a_ok[h][i] ? m : 0) * K + kc * 8;
+      const int n = n0 + (pr >> 5) * 64 + h * 32 + (pr & 31);
+      b_src[h][i] = p.B + (size_t)n * K + kc * 8;
+    }
+  const f16* zero = reinterpret_cast<const f16*>(g_zero_page);
+  // piece: 0 = A0, 1 = A1, 2 = B0, 3 = B1
+  auto issue = [&](const int piece, const int kt) {
+    f16* dst = smem + ((kt & 1) * 4 + piece) * PIECE;
+    const int k0 = kt * BK;
+#pragma unroll
+    for (int i = 0; i < 2; ++i) {
+      const f16* src = piece < 2 ? (a_ok[piece][i] ? a_src[piece][i] + k0 : zero) : b_src[piece - 2][i] + k0;
+      __builtin_amdgcn_global_load_lds((const void*)src, (lds_vptr)(dst + (wave * 2 + i) * 8 * BK), 16, 0, 0);
+    }
+  };
+
+  accv acc[8][4];
+#pragma unroll
+  for (int i = 0; i < 8; ++i)
+#pragma unroll
+    for (int j = 0; j < 4; ++j) acc[i][j] = accv{0.f, 0.f, 0.f, 0.f};
+
+  const int l16 = lane & 15, lq = lane >> 4;
+  half8 af[2][4], bf[2][2];
+  auto read_a = [&](const int buf, const int h) {
+    const f16* s = smem + (buf * 4 + h) * PIECE;
+#pragma unroll
+    for (int k = 0; k < 2; ++k)
+#pragma unroll
+      for (int i = 0; i < 4; ++i) {
+        const int r = wm * 64 + i * 16 + l16;
+        af[k][i] = *reinterpret_cast<const half8*>(s + r * BK + sw<64>(r, 4 * k + lq) * 8);
+      }
+  };
+  auto read_b = [&](const int buf, const int h) {
+    const f16* s = smem + (buf * 4 + 2 + h) * PIECE;
+#pragma unroll
+    for (int k = 0; k < 2; ++k)
+#pragma unroll
+      for (int j = 0; j < 2; ++j) {
+        const int r = wn * 32 + j * 16 + l16;
+        bf[k][j] = *reinterpret_cast<const half8*>(s + r * BK + sw<64>(r, 4 * k + lq) * 8);
+      }
+  };
+  auto mma = [&](const int qa, const int qb) {
+    __builtin_amdgcn_sched_barrier(0);
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+    __builtin_amdgcn_s_barrier();
+    __builtin_amdgcn_sched_barrier(0);
+    __builtin_amdgcn_s_setprio(1);
+#pragma unroll
+    for (int k = 0; k < 2; ++k)
+#pragma unroll
+      for (int i = 0; i < 4; ++i)
+#pragma unroll
+        for (int j = 0; j < 2; ++j)
+          acc[qa * 4 + i][qb * 2 + j] =
+              __builtin_amdgcn_mfma_f32_16x16x32_f16(af[k][i], bf[k][j], acc[qa * 4 + i][qb * 2 + j], 0, 0, 0);
+    __builtin_amdgcn_s_setprio(0);
+    __builtin_amdgcn_sched_barrier(0);
+    __builtin_amdgcn_s_barrier();
+    __builtin_amdgcn_sched_barrier(0);
+  };
+
+  const int nk = K / BK;
+  issue(0, 0);
+  issue(3, 0);
+  issue(1, 0);
+  issue(2, 0);
+  if (nk > 1) {
+    issue(0, 1);
+    issue(3, 1);
+    issue(1, 1);
+    wait_vm<6>();
+  } else {
+    wait_vm<0>();
+  }
+  __builtin_amdgcn_s_barrier();
+  if (wm == 1) __builtin_amdgcn_s_barrier();  // stagger the second wave row by one barrier
+  __builtin_amdgcn_sched_barrier(0);
+
+  for (int t = 0; t < nk; ++t) {
+    const int buf = t & 1;
+    const bool n1 = t + 1 < nk, n2 = t + 2 < nk;
+    // ph0 (A0, B0)
+    read_a(buf, 0);
+    read_b(buf, 0);
+    if (n1) issue(2, t + 1);
+    mma(0, 0);
+    // ph1 (A0, B1)
+    read_b(buf, 1);
+    if (n2) issue(0, t + 2);
+    mma(0, 1);
+    // ph2 (A1, B1)
+    read_a(buf, 1);
+    if (n2) issue(3, t + 2);
+    mma(1, 1);
+    // ph3 (A1, B0)
+    read_b(buf, 0);
+    if (n2) {
+      issue(1, t + 2);
+      wait_vm<6>();
+    } else {
+      wait_vm<0>();
+    }
+    mma(1, 0);
+  }
+  if (wm == 0) __builtin_amdgcn_s_barrier();  // re-align the two wave rows
+  asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)" ::: "memory");
+  if constexpr (DBG == 2) {  // probe build: no epilogue
+    float s = 0.f;
+#pragma unroll
+    for (int i = 0; i < 8; ++i)
+#pragma unroll
+      for (int j = 0; j < 4; ++j) s += acc[i][j][0] + acc[i][j][1] + acc[i][j][2] + acc[i][j][3];
+    if (s == 12345.678f) p.C32[0] = s;
+    return;
+  }
+  gemm_epilogue<BM, BN, WM, WN, 16>(p, acc, smem, m0, n0, wm, wn, wave, lane);
+}
+
 // BM=256 tiles: (BN, WM, WN, NS)
 int g_gemm_debug = 0;
 
-template <int BM, int BN, int WM, int WN, int NS, int MF = 32>
+template <int BM, int BN, int WM, int WN, int NS, int MF = 32, int BK = 64>
 static int launch_cfg(const GemmParams& p, hipStream_t s) {
   const int nwg = ((p.M + BM - 1) / BM) * (p.N / BN);
   const dim3 blk(64 * WM * WN);
   if (g_gemm_debug && BN == 256 && BM == 256 && p.amode == A_PLAIN) {
     if (g_gemm_debug == 1)
-      hipLaunchKernelGGL((gemm_glds_kernel<BM, BN, WM, WN, NS, A_PLAIN, 1, MF>), dim3(nwg), blk, 0, s, p);
+      hipLaunchKernelGGL((gemm_glds_kernel<BM, BN, WM, WN, NS, A_PLAIN, 1, MF, BK>), dim3(nwg), blk, 0, s, p);
     else
-      hipLaunchKernelGGL((gemm_glds_kernel<BM, BN, WM, WN, NS, A_PLAIN, 2, MF>), dim3(nwg), blk, 0, s, p);
+      hipLaunchKernelGGL((gemm_glds_kernel<BM, BN, WM, WN, NS, A_PLAIN, 2, MF, BK>), dim3(nwg), blk, 0, s, p);
   } else if (p.amode == A_PLAIN)
-    hipLaunchKernelGGL((gemm_glds_kernel<BM, BN, WM, WN, NS, A_PLAIN, 0, MF>), dim3(nwg), blk, 0, s, p);
+    hipLaunchKernelGGL((gemm_glds_kernel<BM, BN, WM, WN, NS, A_PLAIN, 0, MF, BK>), dim3(nwg), blk, 0, s, p);
   else if (p.amode == A_DUAL)
-    hipLaunchKernelGGL((gemm_glds_kernel<BM, BN, WM, WN, NS, A_DUAL, 0, MF>), dim3(nwg), blk, 0, s, p);
+    hipLaunchKernelGGL((gemm_glds_kernel<BM, BN, WM, WN, NS, A_DUAL, 0, MF, BK>), dim3(nwg), blk, 0, s, p);
   else
-    hipLaunchKernelGGL((gemm_glds_kernel<BM, BN, WM, WN, NS, A_CONV, 0, MF>), dim3(nwg), blk, 0, s, p);
+    hipLaunchKernelGGL((gemm_glds_kernel<BM, BN, WM, WN, NS, A_CONV, 0, MF, BK>), dim3(nwg), blk, 0, s, p);
   MEC_LAUNCH_CHECK();
   return 0;
 }
@@ -414,6 +616,12 @@ int g_gemm_autotune = 1;
 // 4 waves (64 / 48 KB of LDS, so two blocks share a CU and one block's epilogue overlaps
 // the other's MFMA loop).
 // +10000: the same tile on v_mfma_f32_16x16x32_f16.
+// +20000 / +30000: 16x16x32 MFMA with 32-deep K stages and a deeper ring (256 x 256: 4 / 5
+// stages = 3 / 4 tiles in flight; 256 x 128: 6 stages), same K order, so same results.
+// 40256: the 256 x 256 ping-pong schedule (gemm_pp_kernel), plain A only.
+// 50128 / 60128: 256 x 128 on 4 waves (wave tile 128 x 64), 32-deep K stages, 3 / 2 stages
+// (74 / 49 KB LDS): two blocks per CU, so one block's epilogue runs under the other's MFMAs.
+// 50256: the same for 128 x 256.
 static int tile_bn(int id) {
   id %= 10000;
   return id > 1000 ? id - 1000 : id;
@@ -431,6 +639,22 @@ static int launch_bn(const GemmParams& p, hipStream_t s, int id) {
     case 10064: return launch_cfg<256, 64, 4, 2, 3, 16>(p, s);
     case 11128: return launch_cfg<128, 128, 2, 2, 2, 16>(p, s);
     case 11064: return launch_cfg<128, 64, 2, 2, 2, 16>(p, s);
+    case 20256: return launch_cfg<256, 256, 2, 4, 4, 16, 32>(p, s);
+    case 30256: return launch_cfg<256, 256, 2, 4, 5, 16, 32>(p, s);
+    case 20128: return launch_cfg<256, 128, 4, 2, 6, 16, 32>(p, s);
+    case 50128: return launch_cfg<256, 128, 2, 2, 3, 16, 32>(p, s);
+    case 60128: return launch_cfg<256, 128, 2, 2, 2, 16, 32>(p, s);
+    case 50256: return launch_cfg<128, 256, 2, 2, 3, 16, 32>(p, s);
+    case 40256: {
+      if (p.amode != A_PLAIN) { set_error("gemm_glds: tile 40256 (ping-pong) takes a plain A only"); return -1; }
+      const int nwg = ((p.M + 255) / 256) * (p.N / 256);
+      if (g_gemm_debug == 2)
+        hipLaunchKernelGGL((gemm_pp_kernel<A_PLAIN, 2>), dim3(nwg), dim3(512), 0, s, p);
+      else
+        hipLaunchKernelGGL((gemm_pp_kernel<A_PLAIN, 0>), dim3(nwg), dim3(512), 0, s, p);
+      MEC_LAUNCH_CHECK();
+      return 0;
+    }
     default: set_error("gemm_glds: unsupported tile id"); return -1;
   }
 }
@@ -445,13 +669,15 @@ static int heuristic_bn(const GemmParams& p) {
 
 static int tune_bn(const GemmParams& p, hipStream_t s, int* out_bn) {
   constexpr int REPS = 5;
-  const int cands[10] = {64, 128, 256, 1128, 1064, 10064, 10128, 10256, 11128, 11064};
+  const int cands[] = {64,    128,   256,   1128,  1064,  10064, 10128, 10256, 11128,
+                       11064, 20256, 30256, 20128, 40256, 50128, 60128, 50256};
   hipEvent_t ev[REPS + 1];
   for (auto& e : ev) MEC_HIP(hipEventCreate(&e));
   float best = 1e30f;
   int best_bn = heuristic_bn(p);
   for (int bn : cands) {
     if (p.N % tile_bn(bn)) continue;
+    if (bn == 40256 && p.amode != A_PLAIN) continue;
     MEC_TRY(launch_bn(p, s, bn));  // warm
     MEC_HIP(hipEventRecord(ev[0], s));
     for (int r = 0; r < REPS; ++r) {
@@ -477,7 +703,10 @@ int gemm_tuned_bn(int amode, int M, int N, int K) {
 }
 
 int launch_gemm_glds(const GemmParams& p, hipStream_t s, int force_bn) {
-  if (force_bn) return launch_bn(p, s, force_bn);
+  if (force_bn) {
+    MEC_REQUIRE(p.N % tile_bn(force_bn) == 0, "gemm_glds: forced tile width does not divide N");
+    return launch_bn(p, s, force_bn);
+  }
   const GemmKey key{p.amode, p.M, p.N, p.K, p.H, p.W, p.C, p.ks, p.stride, p.pad};
   int bn = 0;
   {

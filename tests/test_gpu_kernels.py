@@ -42,6 +42,83 @@ def test_gemm_f16(dev, M, N, K, act):
     assert _rel_err(C16.float(), ref) < 2e-3
 
 
+TILE_IDS = [64, 128, 256, 1064, 1128, 10064, 10128, 10256, 11064, 11128, 20256, 30256, 20128, 50128, 60128, 50256]
+
+
+def _forced(lib, tid, fn):
+    lib.mec_set_option(b'gemm_bn', tid)
+    try:
+        fn()
+    finally:
+        lib.mec_set_option(b'gemm_bn', 0)
+
+
+@pytest.mark.parametrize('amode', ['gemm', 'conv', 'conv1x1'])
+def test_every_tile_bit_identical(dev, amode):
+    """Every tile id (width, wave layout, MFMA shape, K-stage depth) accumulates each output
+    along the same k order, so the autotuner's choice must not change a single bit."""
+    lib = _lib.load()
+    g = torch.Generator().manual_seed(7)
+    outs = {}
+    if amode == 'gemm':
+        M, N, K = 1000, 768, 768
+        A = (torch.rand(M, K, generator=g) * 2 - 1).half().to(dev)
+        B = (torch.rand(N, K, generator=g) * 2 - 1).mul(K ** -0.5).half().to(dev)
+        bias = torch.rand(N, generator=g).to(dev)
+        R = torch.rand(M, N, generator=g).to(dev)
+        ref = torch.nn.functional.gelu(A.float() @ B.float().t() + bias + R)
+        for tid in TILE_IDS + [40256]:
+            C16 = torch.empty(M, N, dtype=torch.float16, device=dev)
+            C32 = torch.empty(M, N, device=dev)
+            _forced(lib, tid, lambda: _lib.check(lib.mec_gemm_f16(_p(A), _p(B), _p(bias), _p(R), 1, _p(C16), _p(C32),
+                                                                  M, N, K, 2, _s()), f'gemm {tid}'))
+            torch.cuda.synchronize()
+            assert _rel_err(C32, ref) < 1e-5, tid
+            outs[tid] = (C16.cpu(), C32.cpu())
+    else:
+        n, H, C, Co = 3, 15, 64, 256
+        ks, st, pd = (3, 2, 1) if amode == 'conv' else (1, 1, 0)
+        x = torch.rand(n, H, H, C, generator=g).half().to(dev)
+        w = ((torch.rand(Co, ks, ks, C, generator=g) * 2 - 1) * (C * ks * ks) ** -0.5).half().to(dev)
+        bias = torch.rand(Co, generator=g).to(dev)
+        OH = (H + 2 * pd - ks) // st + 1
+        ref = torch.relu(torch.nn.functional.conv2d(x.permute(0, 3, 1, 2).float(), w.permute(0, 3, 1, 2).float(),
+                                                    bias, stride=st, padding=pd)).permute(0, 2, 3, 1)
+        for tid in TILE_IDS:
+            y = torch.empty(n, OH, OH, Co, dtype=torch.float16, device=dev)
+            _forced(lib, tid, lambda: _lib.check(lib.mec_conv_f16(_p(x), _p(w), _p(bias), None, _p(y), n, H, H, C, Co,
+                                                                  ks, st, pd, 1, _s()), f'conv {tid}'))
+            torch.cuda.synchronize()
+            assert _rel_err(y.float(), ref) < 2e-3, tid
+            outs[tid] = (y.cpu(),)
+    first = outs[TILE_IDS[0]]
+    for tid, o in outs.items():
+        for a, b in zip(o, first):
+            assert torch.equal(a, b), f'tile {tid} differs from tile {TILE_IDS[0]}'
+
+
+@pytest.mark.parametrize('M,K', [(256, 64), (300, 128), (513, 192), (1000, 3072), (4096, 768)])
+def test_pingpong_tile_k_tails(dev, M, K):
+    """The ping-pong tile (40256) at 1, 2, 3, 48 and 12 K tiles: its prologue / restage /
+    vmcnt tails, against torch and bit-identical to the 10256 tile."""
+    lib = _lib.load()
+    N = 512
+    g = torch.Generator().manual_seed(M + K)
+    A = (torch.rand(M, K, generator=g) * 2 - 1).half().to(dev)
+    B = (torch.rand(N, K, generator=g) * 2 - 1).mul(K ** -0.5).half().to(dev)
+    bias = torch.rand(N, generator=g).to(dev)
+    ref = A.float() @ B.float().t() + bias
+    outs = []
+    for tid in (40256, 10256):
+        C32 = torch.empty(M, N, device=dev)
+        _forced(lib, tid, lambda: _lib.check(lib.mec_gemm_f16(_p(A), _p(B), _p(bias), None, 0, None, _p(C32),
+                                                              M, N, K, 0, _s()), f'gemm {tid}'))
+        torch.cuda.synchronize()
+        assert _rel_err(C32, ref) < 1e-5, tid
+        outs.append(C32.cpu())
+    assert torch.equal(outs[0], outs[1])
+
+
 def test_gemm_f16_residual_f16_asymmetric(dev):
     """A = I with an asymmetric B catches a transposed C write."""
     lib = _lib.load()

@@ -47,9 +47,11 @@ def main():
     ap = argparse.ArgumentParser()
     ap.add_argument('--impl', type=int, nargs='+', default=[1, 2])
     ap.add_argument('--bn', type=int, nargs='+', default=[0])
-    ap.add_argument('--iters', type=int, default=20)
+    ap.add_argument('--iters', type=int, default=10)
+    ap.add_argument('--rounds', type=int, default=5)
     ap.add_argument('--only', nargs='*')
     ap.add_argument('--debug', type=int, nargs='+', default=[0])
+    ap.add_argument('--torch', action='store_true', help='also time torch.mm (hipBLASLt) on plain shapes')
     a = ap.parse_args()
     lib = _lib.load()
     dev = torch.device('cuda', 0)
@@ -86,36 +88,70 @@ def main():
             def run():
                 _lib.check(lib.mec_conv_f16(p(x), p(w), p(bias), None, p(y), n, H, H, C, Co, ks, s, pd, 1, st), name)
             ref = None
-        for impl, bn, dbg in [(i, b, d) for i in a.impl for b in (a.bn if i == 2 else [0]) for d in a.debug]:
-            if True:
-                lib.mec_set_option(b'gemm_debug', dbg)
-                lib.mec_set_option(b'gemm_impl', impl)
-                lib.mec_set_option(b'gemm_bn', bn)
-                try:
-                    run()
-                except _lib.MecError as e:
-                    res.append({'shape': name, 'impl': impl, 'bn': bn, 'error': str(e)})
-                    continue
-                torch.cuda.synchronize()
+        if a.torch and kind == 'gemm':
+            Bt = Bw.t()
+            torch.mm(A, Bt)
+            torch.cuda.synchronize()
+            e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+            e0.record()
+            for _ in range(a.iters):
+                torch.mm(A, Bt)
+            e1.record()
+            torch.cuda.synchronize()
+            ms = e0.elapsed_time(e1) / a.iters
+            r = {'shape': name, 'impl': 'torch.mm', 'us': round(ms * 1e3, 1), 'tflops': round(flop / ms / 1e9, 1)}
+            print(json.dumps(r), flush=True)
+        variants = [(i, b, d) for i in a.impl for b in (a.bn if i == 2 else [0]) for d in a.debug]
+
+        def setv(impl, bn, dbg):
+            lib.mec_set_option(b'gemm_debug', dbg)
+            lib.mec_set_option(b'gemm_impl', impl)
+            lib.mec_set_option(b'gemm_bn', bn)
+
+        ok = []
+        for v in variants:  # validate + warm (and autotune for bn=0) each variant once
+            setv(*v)
+            try:
+                run()
+            except _lib.MecError as e:
+                print(json.dumps({'shape': name, 'impl': v[0], 'bn': v[1], 'error': str(e)}), flush=True)
+                continue
+            ok.append(v)
+        torch.cuda.synchronize()
+        # interleaved rounds (guide rule 24): clocks drift over a sweep, so every variant is
+        # timed in every round and the median round is reported
+        times = {v: [] for v in ok}
+        for _ in range(a.rounds):
+            for v in ok:
+                setv(*v)
                 e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
                 e0.record()
                 for _ in range(a.iters):
                     run()
                 e1.record()
                 torch.cuda.synchronize()
-                ms = e0.elapsed_time(e1) / a.iters
-                r = {'shape': name, 'impl': impl, 'bn': bn, 'dbg': dbg, 'us': round(ms * 1e3, 1), 'tflops': round(flop / ms / 1e9, 1)}
-                if ref is not None and dbg == 0:
-                    rr = ref()
-                    if act == 1:
-                        rr = torch.relu(rr + (R[:512].float() if R is not None else 0))
-                    elif act == 2:
-                        rr = torch.nn.functional.gelu(rr)
-                    elif R is not None:
-                        rr = rr + R[:512].float()
-                    r['relerr'] = float((out() - rr).abs().max() / rr.abs().max())
-                res.append(r)
-                print(json.dumps(r), flush=True)
+                times[v].append(e0.elapsed_time(e1) / a.iters)
+        for v in ok:
+            impl, bn, dbg = v
+            ms = sorted(times[v])[len(times[v]) // 2]
+            r = {'shape': name, 'impl': impl, 'bn': bn, 'dbg': dbg, 'us': round(ms * 1e3, 1),
+                 'tflops': round(flop / ms / 1e9, 1)}
+            if ref is not None and dbg == 0:
+                setv(*v)
+                run()
+                torch.cuda.synchronize()
+                rr = ref()
+                if act == 1:
+                    rr = torch.relu(rr + (R[:512].float() if R is not None else 0))
+                elif act == 2:
+                    rr = torch.nn.functional.gelu(rr)
+                elif R is not None:
+                    rr = rr + R[:512].float()
+                r['relerr'] = float((out() - rr).abs().max() / rr.abs().max())
+            if bn == 0 and kind == 'gemm':
+                r['tuned'] = lib.mec_gemm_query(0, M, N, K)
+            res.append(r)
+            print(json.dumps(r), flush=True)
     lib.mec_set_option(b'gemm_impl', 2)
     lib.mec_set_option(b'gemm_debug', 0)
     lib.mec_set_option(b'gemm_bn', 0)

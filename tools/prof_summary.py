@@ -1,6 +1,9 @@
 """Summarise a rocprofv3 rocpd database into per-kernel tables.
-usage: python tools/prof_summary.py DB [--by-grid] [--skip-first-steps N --launches-per-step L]
---by-grid splits a kernel name by launch grid (tells GEMM shapes apart)."""
+usage: python tools/prof_summary.py DB [--by-grid] [--window MARKER] [--steps K]
+--by-grid splits a kernel name by launch grid (tells GEMM shapes apart).
+--window keeps only the dispatches between the first two launches of the MARKER kernel
+(bench.py brackets its timed region with torch.cuda._sleep, i.e. a spin_kernel), so
+autotuning and warm-up launches drop out; --steps K adds a per-step column."""
 import argparse
 import sqlite3
 
@@ -10,12 +13,20 @@ def main():
     ap.add_argument('db')
     ap.add_argument('--by-grid', action='store_true')
     ap.add_argument('--match', default=None, help='substring filter on the kernel name')
+    ap.add_argument('--window', default=None, help='marker kernel name substring')
+    ap.add_argument('--steps', type=int, default=0)
     a = ap.parse_args()
     c = sqlite3.connect(a.db)
-    q = "select name, grid_x, workgroup_x, end-start from kernels order by start"
+    q = "select name, grid_x, workgroup_x, end-start, start from kernels order by start"
     rows = c.execute(q).fetchall()
+    if a.window:
+        marks = [i for i, r in enumerate(rows) if a.window in r[0]]
+        if len(marks) < 2:
+            raise SystemExit(f'fewer than two {a.window} dispatches in {a.db}')
+        t0, t1 = rows[marks[0]][4], rows[marks[1]][4]
+        rows = [r for r in rows if t0 < r[4] < t1 and a.window not in r[0]]
     agg = {}
-    for name, gx, wx, d in rows:
+    for name, gx, wx, d, _ in rows:
         if a.match and a.match not in name:
             continue
         key = (name, gx // max(wx, 1)) if a.by_grid else (name, None)
@@ -25,11 +36,16 @@ def main():
         s[2] = min(s[2], d)
         s[3] = max(s[3], d)
     tot = sum(v[1] for v in agg.values())
-    print(f"{'kernel':88s} {'blocks':>7s} {'calls':>6s} {'total_ms':>10s} {'avg_us':>9s} {'min_us':>9s} {'max_us':>9s} {'pct':>6s}")
+    ps = f" {'ms/step':>8s}" if a.steps else ''
+    print(f"{'kernel':88s} {'blocks':>7s} {'calls':>6s} {'total_ms':>10s} {'avg_us':>9s} {'min_us':>9s} {'max_us':>9s} {'pct':>6s}"
+          + ps)
     for (n, g), (cnt, s, mn, mx) in sorted(agg.items(), key=lambda kv: -kv[1][1]):
         gs = '' if g is None else str(g)
-        print(f"{n[:88]:88s} {gs:>7s} {cnt:6d} {s/1e6:10.3f} {s/cnt/1e3:9.1f} {mn/1e3:9.1f} {mx/1e3:9.1f} {100*s/tot:6.2f}")
-    print(f"total kernel time {tot/1e6:.3f} ms over {sum(v[0] for v in agg.values())} dispatches")
+        st = f" {s / 1e6 / a.steps:8.3f}" if a.steps else ''
+        print(f"{n[:88]:88s} {gs:>7s} {cnt:6d} {s/1e6:10.3f} {s/cnt/1e3:9.1f} {mn/1e3:9.1f} {mx/1e3:9.1f} {100*s/tot:6.2f}"
+              + st)
+    per = f", {tot / 1e6 / a.steps:.3f} ms/step" if a.steps else ''
+    print(f"total kernel time {tot/1e6:.3f} ms over {sum(v[0] for v in agg.values())} dispatches{per}")
 
 
 if __name__ == '__main__':
