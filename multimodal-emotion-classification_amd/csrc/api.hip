@@ -211,7 +211,7 @@ int mec_set_option(const char* key, int value) {
   if (k == "gemm_debug" && value >= 0 && value <= 2) { g_gemm_debug = value; return 0; }
   if (k == "gemm_autotune" && (value == 0 || value == 1)) { g_gemm_autotune = value; return 0; }
   const int v = value % 10000;
-  const bool deep = value == 20256 || value == 30256 || value == 20128 || value == 40256 || value == 50128 ||
+  const bool deep = value == 20256 || value == 30256 || value == 20128 || value == 40256 || value == 41256 || value == 50128 ||
                     value == 60128 || value == 50256;
   if (k == "gemm_bn" && (value == 0 || deep || (value < 20000 && (v == 64 || v == 128 || v == 256 || v == 1064 || v == 1128)))) {
     g_gemm_bn = value;

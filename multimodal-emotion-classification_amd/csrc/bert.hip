@@ -5,11 +5,16 @@
 // Per layer (M = B*L token rows; residual stream kept in fp32, GEMM operands in f16):
 //   qkv16  = h16 . Wqkv^T + b                    gemm (N=2304)
 //   ctx16  = softmax(QK^T/8 + mask_bias) V       bert_attention_kernel (MFMA, LDS)
-//   t32    = ctx16 . Wo^T + bo + h32             gemm, f32 out (residual fused)
-//   h      = LN(t32)  -> h32, h16                layernorm_kernel (eps 1e-12)
+//   t32    = ctx16 . Wo^T + bo + h               gemm, f32 out (residual fused)
+//   h      = LN(t32)  -> h16 + (mean, rstd)      layernorm_kernel (eps 1e-12)
 //   i16    = GELU(h16 . Wi^T + bi)               gemm (N=3072), erf-GELU fused
-//   t32    = i16 . Wo2^T + bo2 + h32             gemm, f32 out
+//   t32    = i16 . Wo2^T + bo2 + h               gemm, f32 out
 //   h      = LN(t32)
+// The f32 LN output h is never written (except after the embedding and the last layer):
+// the residual add that consumes it reads the pre-LN sum and the row (mean, rstd) and
+// re-evaluates the LN expression in its epilogue. The pre-LN sums alternate between two
+// f32 buffers (O-proj: h32 -> t32, FFN2: t32 -> h32). Saves a 4-byte write per element
+// per LayerNorm.
 // Head: cls = h32[:,0,:] (pre-pooler CLS feature, text_inference.py:125);
 //       probs = softmax(Wc tanh(Wp cls + bp) + bc).
 #include "block_ops.h"
@@ -70,10 +75,12 @@ __global__ __launch_bounds__(256) void bert_embed_ln_kernel(const int32_t* __res
 }
 
 // ----------------------------------------------------------------------------- LayerNorm
-__global__ __launch_bounds__(256) void bert_layernorm_kernel(const float* __restrict__ x, int M,
+__global__ __launch_bounds__(256) void bert_layernorm_kernel(const float* x, int M,
                                                              const float* __restrict__ g,
                                                              const float* __restrict__ b, float* h32,
-                                                             f16* h16) {
+                                                             f16* h16, float2* stats) {
+  // h32 may be null: the consumer of the f32 output (the next residual add) then
+  // re-derives it from x and `stats` in its GEMM epilogue (GemmParams::r_stats)
   const int lane = threadIdx.x & 63;
   const int row = blockIdx.x * 4 + (threadIdx.x >> 6);
   if (row >= M) return;
@@ -91,15 +98,16 @@ __global__ __launch_bounds__(256) void bert_layernorm_kernel(const float* __rest
 #pragma unroll
   for (int i = 0; i < 12; ++i) { const float d = v[i] - mean; q += d * d; }
   const float rstd = 1.0f / sqrtf(wave_sum(q) * (1.0f / BH) + 1e-12f);
+  if (stats && lane == 0) stats[row] = make_float2(mean, rstd);
 #pragma unroll
   for (int j = 0; j < 3; ++j) {
     const int c = j * 256 + lane * 4;
     float4 o;
-    o.x = (v[4 * j + 0] - mean) * rstd * g[c + 0] + b[c + 0];
-    o.y = (v[4 * j + 1] - mean) * rstd * g[c + 1] + b[c + 1];
-    o.z = (v[4 * j + 2] - mean) * rstd * g[c + 2] + b[c + 2];
-    o.w = (v[4 * j + 3] - mean) * rstd * g[c + 3] + b[c + 3];
-    *reinterpret_cast<float4*>(h32 + (size_t)row * BH + c) = o;
+    o.x = __builtin_fmaf((v[4 * j + 0] - mean) * rstd, g[c + 0], b[c + 0]);
+    o.y = __builtin_fmaf((v[4 * j + 1] - mean) * rstd, g[c + 1], b[c + 1]);
+    o.z = __builtin_fmaf((v[4 * j + 2] - mean) * rstd, g[c + 2], b[c + 2]);
+    o.w = __builtin_fmaf((v[4 * j + 3] - mean) * rstd, g[c + 3], b[c + 3]);
+    if (h32) *reinterpret_cast<float4*>(h32 + (size_t)row * BH + c) = o;
     half4 hh = {(f16)o.x, (f16)o.y, (f16)o.z, (f16)o.w};
     *reinterpret_cast<half4*>(h16 + (size_t)row * BH + c) = hh;
   }
@@ -291,7 +299,8 @@ int TextModel::forward(const int32_t* ids, const int32_t* mask, int B, int L, fl
   MEC_REQUIRE(ids && mask && cls && logits && probs, "text: null pointer");
   const int M = B * L;
   // workspace: h32 | t32 (f32 [M,768]) ; h16 | ctx16 (f16 [M,768]) ; qkv16 [M,2304] / i16 [M,3072]
-  const size_t need = (size_t)M * BH * 4 * 2 + (size_t)M * BH * 2 * 2 + (size_t)M * BI * 2 + (size_t)B * BH * 4;
+  const size_t need = (size_t)M * BH * 4 * 2 + (size_t)M * BH * 2 * 2 + (size_t)M * BI * 2 + (size_t)B * BH * 4 +
+                      (size_t)M * 8 * 2;
   if (M > ws_tokens) {
     MEC_TRY(ws.ensure(need));
     ws_tokens = M;
@@ -304,6 +313,9 @@ int TextModel::forward(const int32_t* ids, const int32_t* mask, int B, int L, fl
   f16* big16 = reinterpret_cast<f16*>(p);  // qkv16 [M,2304] then i16 [M,3072]
   p += (size_t)M * BI * 2;
   float* pooled = reinterpret_cast<float*>(p);  // [B,768]
+  p += (size_t)B * BH * 4;
+  float2* st1 = reinterpret_cast<float2*>(p);  // LN1 row stats [M]
+  float2* st2 = st1 + M;                       // LN2 row stats [M]
 
   const float* E = emb.as<float>();
   const float* word = E;
@@ -332,21 +344,31 @@ int TextModel::forward(const int32_t* ids, const int32_t* mask, int B, int L, fl
     hipLaunchKernelGGL(bert_attention_kernel, dim3(B * BHEADS), dim3(256), 0, s, big16, mask, ctx16);
     MEC_LAUNCH_CHECK();
     MEC_TRY(prof.end(TAG_BERT_ATTN, s));
+    const bool first = l == 0, last = l == BLAYERS - 1;
+    const float* pg2 = P + PRM_LAYER * (l - 1) + 8448;  // previous layer's LN2 (g2, b2)
+    // f32 stream ping-pong: O-proj reads h32 and writes t32, FFN2 reads t32 and writes h32,
+    // so no GEMM reads its own output (a launch stays idempotent: the tile autotuner
+    // re-runs candidates on the same buffers)
     g = GemmParams();
     g.A = ctx16; g.B = wo; g.bias = bo; g.R = h32; g.r_f32 = 1; g.C32 = t32; g.M = M; g.N = BH; g.K = BH;
+    if (!first) { g.r_stats = st2; g.r_g = pg2; g.r_b = pg2 + BH; }  // else: the embedding LN, written in full
     MEC_TRY(launch_gemm(g, s, &prof, TAG_BERT_OPROJ));
     MEC_TRY(prof.begin(TAG_BERT_LN, s));
-    hipLaunchKernelGGL(bert_layernorm_kernel, rows_grid, dim3(256), 0, s, t32, M, g1, b1, h32, h16);
+    hipLaunchKernelGGL(bert_layernorm_kernel, rows_grid, dim3(256), 0, s, t32, M, g1, b1, nullptr, h16, st1);
     MEC_LAUNCH_CHECK();
     MEC_TRY(prof.end(TAG_BERT_LN, s));
     g = GemmParams();
     g.A = h16; g.B = wi; g.bias = bi; g.act = ACT_GELU; g.C16 = big16; g.M = M; g.N = BI; g.K = BH;
     MEC_TRY(launch_gemm(g, s, &prof, TAG_BERT_FFN1));
     g = GemmParams();
-    g.A = big16; g.B = wo2; g.bias = bo2; g.R = h32; g.r_f32 = 1; g.C32 = t32; g.M = M; g.N = BH; g.K = BI;
+    g.A = big16; g.B = wo2; g.bias = bo2; g.R = t32; g.r_f32 = 1; g.r_stats = st1; g.r_g = g1; g.r_b = b1;
+    g.C32 = h32; g.M = M; g.N = BH; g.K = BI;
     MEC_TRY(launch_gemm(g, s, &prof, TAG_BERT_FFN2));
     MEC_TRY(prof.begin(TAG_BERT_LN, s));
-    hipLaunchKernelGGL(bert_layernorm_kernel, rows_grid, dim3(256), 0, s, t32, M, g2, b2, h32, h16);
+    // the last LN's f32 output feeds the pooler / CLS feature, so it is written in full
+    // (in place: each wave holds its row in registers before writing it)
+    hipLaunchKernelGGL(bert_layernorm_kernel, rows_grid, dim3(256), 0, s, h32, M, g2, b2, last ? h32 : nullptr, h16,
+                       st2);
     MEC_LAUNCH_CHECK();
     MEC_TRY(prof.end(TAG_BERT_LN, s));
   }

@@ -178,8 +178,12 @@ __global__ __launch_bounds__(256, 2) void gemm_f16_kernel(const GemmParams p) {
         if (row < M) {
           const size_t idx = (size_t)row * N + col;
           float v = acc[i][j][e] + bv;
-          if (p.R) v += p.r_f32 ? reinterpret_cast<const float*>(p.R)[idx]
-                                : (float)reinterpret_cast<const f16*>(p.R)[idx];
+          if (p.R && p.r_stats) {
+            const float2 st = p.r_stats[row];
+            v += __builtin_fmaf((reinterpret_cast<const float*>(p.R)[idx] - st.x) * st.y, p.r_g[col], p.r_b[col]);
+          } else if (p.R) {
+            v += p.r_f32 ? reinterpret_cast<const float*>(p.R)[idx] : (float)reinterpret_cast<const f16*>(p.R)[idx];
+          }
           if (p.act == ACT_RELU) v = fmaxf(v, 0.f);
           else if (p.act == ACT_GELU) v = gelu_erf(v);
           if (p.C16) p.C16[idx] = (f16)v;
@@ -212,6 +216,7 @@ int launch_gemm(const GemmParams& p, hipStream_t s, Prof* prof, int tag) {
   MEC_REQUIRE(p.K % GBK == 0, "gemm: K % 64 != 0");
   MEC_REQUIRE(p.A && p.B, "gemm: null operand");
   MEC_REQUIRE(p.C16 || p.C32, "gemm: no output");
+  MEC_REQUIRE(!p.r_stats || (p.R && p.r_f32 && p.r_g && p.r_b), "gemm: deferred-LN residual needs f32 R, gamma, beta");
   if (p.amode == A_CONV) {
     MEC_REQUIRE(p.C % 64 == 0 && p.K == p.ks * p.ks * p.C, "conv: C % 64 != 0 or K != ks*ks*C");
   } else if (p.amode == A_DUAL) {

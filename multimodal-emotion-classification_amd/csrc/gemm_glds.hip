@@ -90,6 +90,11 @@ __device__ __forceinline__ void gemm_epilogue(const GemmParams& p, accv (&acc)[T
     bias[0] = b0.x; bias[1] = b0.y; bias[2] = b0.z; bias[3] = b0.w;
     bias[4] = b1.x; bias[5] = b1.y; bias[6] = b1.z; bias[7] = b1.w;
   }
+  float lng[8], lnb[8];
+  if (p.r_stats) {
+#pragma unroll
+    for (int q = 0; q < 8; ++q) { lng[q] = p.r_g[col0 + q]; lnb[q] = p.r_b[col0 + q]; }
+  }
   constexpr int SLABS = TM / 32;
 #pragma unroll
   for (int i = 0; i < SLABS; ++i) {
@@ -124,6 +129,11 @@ __device__ __forceinline__ void gemm_epilogue(const GemmParams& p, accv (&acc)[T
           const float4 r1 = *reinterpret_cast<const float4*>(R + 4);
           rv[ps][0] = r0.x; rv[ps][1] = r0.y; rv[ps][2] = r0.z; rv[ps][3] = r0.w;
           rv[ps][4] = r1.x; rv[ps][5] = r1.y; rv[ps][6] = r1.z; rv[ps][7] = r1.w;
+          if (p.r_stats) {
+            const float2 st = p.r_stats[row];
+#pragma unroll
+            for (int q = 0; q < 8; ++q) rv[ps][q] = __builtin_fmaf((rv[ps][q] - st.x) * st.y, lng[q], lnb[q]);
+          }
         } else {
           const half8 r8 = *reinterpret_cast<const half8*>(reinterpret_cast<const f16*>(p.R) + base);
 #pragma unroll
@@ -416,13 +426,20 @@ __global__ __launch_bounds__(64 * WM * WN, (WM * WN == 4) ? 2 : 1) void gemm_gld
 // MFMA section while its partner loads. ph3 waits vmcnt(6): everything but the three
 // pieces issued for tile t+2 has landed, i.e. all of tile t+1, read one phase later.
 // Same k order per output as every other tile, so results are bit-identical to them.
-template <int AM, int DBG = 0>
+template <int AM, int DBG = 0, int BM = 256>
 __global__ __launch_bounds__(512) void gemm_pp_kernel(const GemmParams p) {
   static_assert(AM == A_PLAIN, "ping-pong tile: plain A only");
-  constexpr int BM = 256, BN = 256, BK = 64, WM = 2, WN = 4;
-  constexpr int PIECE = 128 * BK;  // halfs
+  static_assert(BM == 256 || BM == 128, "BM");
+  constexpr int BN = 256, BK = 64, WM = 2, WN = 4;
+  constexpr int PA = BM / 2;            // rows per A piece (two wave rows x BM/4)
+  constexpr int PB = 128;               // rows per B piece (four wave columns x 32)
+  constexpr int GA = PA / 64, GB = 2;   // glds per lane per piece
+  constexpr int QI = BM / 64;           // 16-row MFMA tiles per quadrant
+  constexpr int OFF_A1 = PA * BK, OFF_B0 = 2 * PA * BK, OFF_B1 = OFF_B0 + PB * BK;
+  constexpr int BUF = 2 * (PA + PB) * BK;  // halfs per buffer
+  constexpr int VM = (2 * GA + GB) * 1;    // glds of the three pieces issued for tile t+2
   typedef float accv __attribute__((ext_vector_type(4)));
-  __shared__ __attribute__((aligned(16))) f16 smem[8 * PIECE];
+  __shared__ __attribute__((aligned(16))) f16 smem[2 * BUF];
 
   const int tid = threadIdx.x, lane = tid & 63;
   const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
@@ -440,53 +457,66 @@ __global__ __launch_bounds__(512) void gemm_pp_kernel(const GemmParams p) {
   const int m0 = bm * BM, n0 = bn * BN;
 
   const int lrow = lane >> 3, pchunk = lane & 7;
-  const f16* a_src[2][2];
-  const f16* b_src[2][2];
-  bool a_ok[2][2];
+  const f16* a_src[2][GA];
+  const f16* b_src[2][GB];
+  bool a_ok[2][GA];
 #pragma unroll
-  for (int h = 0; h < 2; ++h)
+  for (int h = 0; h < 2; ++h) {
 #pragma unroll
-    for (int i = 0; i < 2; ++i) {
-      const int pr = (wave * 2 + i) * 8 + lrow;  // piece-local row 0..127
-      const int kc = sw<64>(pr, pchunk);
-      const int m = m0 + (pr >> 6) * 128 + h * 64 + (pr & 63);
+    for (int i = 0; i < GA; ++i) {
+      const int pr = (wave * GA + i) * 8 + lrow;  // A-piece row
+      const int m = m0 + (pr / (PA / 2)) * (BM / 2) + h * (BM / 4) + pr % (PA / 2);
       a_ok[h][i] = m < M;
-      a_src[h][i] = reinterpret_cast<const f16*>(p.A) + (size_t)(a_ok[h][i] ? m : 0) * K + kc * 8;
-      const int n = n0 + (pr >> 5) * 64 + h * 32 + (pr & 31);
-      b_src[h][i] = p.B + (size_t)n * K + kc * 8;
+      a_src[h][i] = reinterpret_cast<const f16*>(p.A) + (size_t)(a_ok[h][i] ? m : 0) * K + sw<64>(pr, pchunk) * 8;
     }
+#pragma unroll
+    for (int i = 0; i < GB; ++i) {
+      const int pr = (wave * GB + i) * 8 + lrow;  // B-piece row
+      const int n = n0 + (pr >> 5) * 64 + h * 32 + (pr & 31);
+      b_src[h][i] = p.B + (size_t)n * K + sw<64>(pr, pchunk) * 8;
+    }
+  }
   const f16* zero = reinterpret_cast<const f16*>(g_zero_page);
   // piece: 0 = A0, 1 = A1, 2 = B0, 3 = B1
   auto issue = [&](const int piece, const int kt) {
-    f16* dst = smem + ((kt & 1) * 4 + piece) * PIECE;
+    f16* base = smem + (kt & 1) * BUF;
     const int k0 = kt * BK;
+    if (piece < 2) {
+      f16* dst = base + piece * OFF_A1;
 #pragma unroll
-    for (int i = 0; i < 2; ++i) {
-      const f16* src = piece < 2 ? (a_ok[piece][i] ? a_src[piece][i] + k0 : zero) : b_src[piece - 2][i] + k0;
-      __builtin_amdgcn_global_load_lds((const void*)src, (lds_vptr)(dst + (wave * 2 + i) * 8 * BK), 16, 0, 0);
+      for (int i = 0; i < GA; ++i) {
+        const f16* src = a_ok[piece][i] ? a_src[piece][i] + k0 : zero;
+        __builtin_amdgcn_global_load_lds((const void*)src, (lds_vptr)(dst + (wave * GA + i) * 8 * BK), 16, 0, 0);
+      }
+    } else {
+      f16* dst = base + (piece == 2 ? OFF_B0 : OFF_B1);
+#pragma unroll
+      for (int i = 0; i < GB; ++i)
+        __builtin_amdgcn_global_load_lds((const void*)(b_src[piece - 2][i] + k0),
+                                         (lds_vptr)(dst + (wave * GB + i) * 8 * BK), 16, 0, 0);
     }
   };
 
-  accv acc[8][4];
+  accv acc[2 * QI][4];
 #pragma unroll
-  for (int i = 0; i < 8; ++i)
+  for (int i = 0; i < 2 * QI; ++i)
 #pragma unroll
     for (int j = 0; j < 4; ++j) acc[i][j] = accv{0.f, 0.f, 0.f, 0.f};
 
   const int l16 = lane & 15, lq = lane >> 4;
-  half8 af[2][4], bf[2][2];
+  half8 af[2][QI], bf[2][2];
   auto read_a = [&](const int buf, const int h) {
-    const f16* s = smem + (buf * 4 + h) * PIECE;
+    const f16* s = smem + buf * BUF + h * OFF_A1;
 #pragma unroll
     for (int k = 0; k < 2; ++k)
 #pragma unroll
-      for (int i = 0; i < 4; ++i) {
-        const int r = wm * 64 + i * 16 + l16;
+      for (int i = 0; i < QI; ++i) {
+        const int r = wm * (PA / 2) + i * 16 + l16;
         af[k][i] = *reinterpret_cast<const half8*>(s + r * BK + sw<64>(r, 4 * k + lq) * 8);
       }
   };
   auto read_b = [&](const int buf, const int h) {
-    const f16* s = smem + (buf * 4 + 2 + h) * PIECE;
+    const f16* s = smem + buf * BUF + (h ? OFF_B1 : OFF_B0);
 #pragma unroll
     for (int k = 0; k < 2; ++k)
 #pragma unroll
@@ -504,11 +534,11 @@ __global__ __launch_bounds__(512) void gemm_pp_kernel(const GemmParams p) {
 #pragma unroll
     for (int k = 0; k < 2; ++k)
 #pragma unroll
-      for (int i = 0; i < 4; ++i)
+      for (int i = 0; i < QI; ++i)
 #pragma unroll
         for (int j = 0; j < 2; ++j)
-          acc[qa * 4 + i][qb * 2 + j] =
-              __builtin_amdgcn_mfma_f32_16x16x32_f16(af[k][i], bf[k][j], acc[qa * 4 + i][qb * 2 + j], 0, 0, 0);
+          acc[qa * QI + i][qb * 2 + j] =
+              __builtin_amdgcn_mfma_f32_16x16x32_f16(af[k][i], bf[k][j], acc[qa * QI + i][qb * 2 + j], 0, 0, 0);
     __builtin_amdgcn_s_setprio(0);
     __builtin_amdgcn_sched_barrier(0);
     __builtin_amdgcn_s_barrier();
@@ -524,7 +554,7 @@ __global__ __launch_bounds__(512) void gemm_pp_kernel(const GemmParams p) {
     issue(0, 1);
     issue(3, 1);
     issue(1, 1);
-    wait_vm<6>();
+    wait_vm<VM>();
   } else {
     wait_vm<0>();
   }
@@ -552,7 +582,7 @@ __global__ __launch_bounds__(512) void gemm_pp_kernel(const GemmParams p) {
     read_b(buf, 0);
     if (n2) {
       issue(1, t + 2);
-      wait_vm<6>();
+      wait_vm<VM>();
     } else {
       wait_vm<0>();
     }
@@ -563,7 +593,7 @@ __global__ __launch_bounds__(512) void gemm_pp_kernel(const GemmParams p) {
   if constexpr (DBG == 2) {  // probe build: no epilogue
     float s = 0.f;
 #pragma unroll
-    for (int i = 0; i < 8; ++i)
+    for (int i = 0; i < 2 * QI; ++i)
 #pragma unroll
       for (int j = 0; j < 4; ++j) s += acc[i][j][0] + acc[i][j][1] + acc[i][j][2] + acc[i][j][3];
     if (s == 12345.678f) p.C32[0] = s;
@@ -618,7 +648,7 @@ int g_gemm_autotune = 1;
 // +10000: the same tile on v_mfma_f32_16x16x32_f16.
 // +20000 / +30000: 16x16x32 MFMA with 32-deep K stages and a deeper ring (256 x 256: 4 / 5
 // stages = 3 / 4 tiles in flight; 256 x 128: 6 stages), same K order, so same results.
-// 40256: the 256 x 256 ping-pong schedule (gemm_pp_kernel), plain A only.
+// 40256 / 41256: the 256 x 256 / 128 x 256 ping-pong schedule (gemm_pp_kernel), plain A only.
 // 50128 / 60128: 256 x 128 on 4 waves (wave tile 128 x 64), 32-deep K stages, 3 / 2 stages
 // (74 / 49 KB LDS): two blocks per CU, so one block's epilogue runs under the other's MFMAs.
 // 50256: the same for 128 x 256.
@@ -645,13 +675,23 @@ static int launch_bn(const GemmParams& p, hipStream_t s, int id) {
     case 50128: return launch_cfg<256, 128, 2, 2, 3, 16, 32>(p, s);
     case 60128: return launch_cfg<256, 128, 2, 2, 2, 16, 32>(p, s);
     case 50256: return launch_cfg<128, 256, 2, 2, 3, 16, 32>(p, s);
-    case 40256: {
-      if (p.amode != A_PLAIN) { set_error("gemm_glds: tile 40256 (ping-pong) takes a plain A only"); return -1; }
-      const int nwg = ((p.M + 255) / 256) * (p.N / 256);
-      if (g_gemm_debug == 2)
-        hipLaunchKernelGGL((gemm_pp_kernel<A_PLAIN, 2>), dim3(nwg), dim3(512), 0, s, p);
-      else
-        hipLaunchKernelGGL((gemm_pp_kernel<A_PLAIN, 0>), dim3(nwg), dim3(512), 0, s, p);
+    case 40256:
+    case 41256: {
+      if (p.amode != A_PLAIN) { set_error("gemm_glds: ping-pong tiles take a plain A only"); return -1; }
+      const dim3 blk(512);
+      if (id == 40256) {
+        const int nwg = ((p.M + 255) / 256) * (p.N / 256);
+        if (g_gemm_debug == 2)
+          hipLaunchKernelGGL((gemm_pp_kernel<A_PLAIN, 2, 256>), dim3(nwg), blk, 0, s, p);
+        else
+          hipLaunchKernelGGL((gemm_pp_kernel<A_PLAIN, 0, 256>), dim3(nwg), blk, 0, s, p);
+      } else {
+        const int nwg = ((p.M + 127) / 128) * (p.N / 256);
+        if (g_gemm_debug == 2)
+          hipLaunchKernelGGL((gemm_pp_kernel<A_PLAIN, 2, 128>), dim3(nwg), blk, 0, s, p);
+        else
+          hipLaunchKernelGGL((gemm_pp_kernel<A_PLAIN, 0, 128>), dim3(nwg), blk, 0, s, p);
+      }
       MEC_LAUNCH_CHECK();
       return 0;
     }
@@ -670,14 +710,14 @@ static int heuristic_bn(const GemmParams& p) {
 static int tune_bn(const GemmParams& p, hipStream_t s, int* out_bn) {
   constexpr int REPS = 5;
   const int cands[] = {64,    128,   256,   1128,  1064,  10064, 10128, 10256, 11128,
-                       11064, 20256, 30256, 20128, 40256, 50128, 60128, 50256};
+                       11064, 20256, 30256, 20128, 40256, 41256, 50128, 60128, 50256};
   hipEvent_t ev[REPS + 1];
   for (auto& e : ev) MEC_HIP(hipEventCreate(&e));
   float best = 1e30f;
   int best_bn = heuristic_bn(p);
   for (int bn : cands) {
     if (p.N % tile_bn(bn)) continue;
-    if (bn == 40256 && p.amode != A_PLAIN) continue;
+    if ((bn == 40256 || bn == 41256) && p.amode != A_PLAIN) continue;
     MEC_TRY(launch_bn(p, s, bn));  // warm
     MEC_HIP(hipEventRecord(ev[0], s));
     for (int r = 0; r < REPS; ++r) {

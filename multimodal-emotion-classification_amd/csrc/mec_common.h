@@ -107,6 +107,11 @@ struct GemmParams {
   const float* bias = nullptr;  // [N]
   const void* R = nullptr;      // residual [M,N] (f16 or f32) or null
   int r_f32 = 0;
+  // deferred LayerNorm of an f32 residual: R' = fma((R - mean[row]) * rstd[row], r_g, r_b),
+  // the exact expression bert_layernorm_kernel evaluates (so R' is that kernel's output)
+  const float2* r_stats = nullptr;  // [M] (mean, rstd) or null
+  const float* r_g = nullptr;       // [N]
+  const float* r_b = nullptr;       // [N]
   f16* C16 = nullptr;           // [M,N] f16 out or null
   float* C32 = nullptr;         // [M,N] f32 out or null
   int M = 0, N = 0, K = 0;
