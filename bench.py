@@ -27,6 +27,18 @@ FLOP_PER_SAMPLE = {'text': 2 * 11_174_221_056, 'image': 2 * 4_088_188_416, 'spee
 MI355X_F16_DENSE_TFLOPS = 2500.0  # MI355X_MICROARCH.md: ~2.5 PF dense bf16/f16 MFMA
 
 
+def tile_name(tile: int, M: int) -> str:
+    """Kernel + grid for a GEMM tile id (gemm_glds.hip, launch_bn)."""
+    if tile in (40256, 41256):
+        bm = 256 if tile == 40256 else 128
+        return f'gemm_pp_kernel<{bm}x256x64 ping-pong, mfma16x16x32> grid={((M + bm - 1) // bm) * (3072 // 256)}'
+    v, w = divmod(tile, 10000)
+    bm, bn = (128, w - 1000) if w > 1000 else (256, w)
+    mf = 32 if v == 0 else 16
+    bk = 32 if v >= 2 else 64
+    return f'gemm_glds_kernel<{bm}x{bn}x{bk}, mfma{mf}> grid={((M + bm - 1) // bm) * (3072 // bn)}'
+
+
 def parse():
     ap = argparse.ArgumentParser()
     ap.add_argument('--gpus', type=int, default=1)
@@ -35,6 +47,7 @@ def parse():
     ap.add_argument('--batch', type=int, default=256)
     ap.add_argument('--no-cpu-baseline', action='store_true')
     ap.add_argument('--cpu-seconds', type=float, default=12.0)
+    ap.add_argument('--serial', action='store_true', help='run the encoders on one stream (A/B of the concurrency)')
     return ap.parse_args()
 
 
@@ -82,7 +95,7 @@ def main():
 
     from mec import engine, synthetic as syn
     B = a.batch
-    pipe = engine.FusedPipeline(seed=1234, device=dev)
+    pipe = engine.FusedPipeline(seed=1234, device=dev, concurrent=not a.serial)
     x = engine.to_device(syn.speech_inputs(B, seed=rank), dev)
     ids_np, mask_np = syn.text_inputs(B, 128, seed=rank, ragged=False)
     ids, mask = engine.to_device(ids_np, dev), engine.to_device(mask_np, dev)
@@ -131,11 +144,7 @@ def main():
         avg_s = (ffn_ms / max(ffn_n, 1)) / 1e3
         achieved = ffn_flop / avg_s / 1e12 if ffn_n else None
         tile = pipe.text.lib.mec_gemm_query(0, M, 3072, 768)
-        bm, bnw = (128, tile % 10000 - 1000) if tile % 10000 > 1000 else (256, tile % 10000)
-        mf = 16 if tile >= 10000 else 32
-        grid = ((M + bm - 1) // bm) * (3072 // bnw)
-        kname = (f'gemm_glds_kernel<{bm},{bnw},...,A_PLAIN,mfma{mf}x{mf}> grid={grid} '
-                 f'(BERT FFN1 + GELU epilogue, M={M} N=3072 K=768)')
+        kname = tile_name(tile, M) + f' (BERT FFN1 + GELU epilogue, M={M} N=3072 K=768)'
         iso = ffn_flop / ((iso_ms / max(iso_n, 1)) / 1e3) / 1e12 if iso_n else None
         traffic, tsrc = None, None
         tf = os.path.join(ROOT, 'profiles', 'ffn1_traffic.json')

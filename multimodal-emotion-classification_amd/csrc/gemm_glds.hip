@@ -413,6 +413,7 @@ __global__ __launch_bounds__(64 * WM * WN, (WM * WN == 4) ? 2 : 1) void gemm_gld
 }
 
 
+
 // ---- 256x256x64 ping-pong GEMM (A_PLAIN), v_mfma_f32_16x16x32_f16, 8 waves (2 x 4).
 // Each K tile lives in one of two LDS buffers as four 16-KB pieces: A0/A1 = the 64-row
 // halves of both wave rows' 128-row strips, B0/B1 = the 32-column halves of the four wave
@@ -653,11 +654,13 @@ int g_gemm_autotune = 1;
 // (74 / 49 KB LDS): two blocks per CU, so one block's epilogue runs under the other's MFMAs.
 // 50256: the same for 128 x 256.
 static int tile_bn(int id) {
+  if (id >= 40000 && id < 50000) return 256;  // ping-pong tiles are 256 wide
   id %= 10000;
   return id > 1000 ? id - 1000 : id;
 }
 
 static int launch_bn(const GemmParams& p, hipStream_t s, int id) {
+  const GemmParams& p0 = p;
   switch (id) {
     case 256: return launch_cfg<256, 256, 2, 4, 2>(p, s);
     case 128: return launch_cfg<256, 128, 4, 2, 3>(p, s);
@@ -677,20 +680,23 @@ static int launch_bn(const GemmParams& p, hipStream_t s, int id) {
     case 50256: return launch_cfg<128, 256, 2, 2, 3, 16, 32>(p, s);
     case 40256:
     case 41256: {
-      if (p.amode != A_PLAIN) { set_error("gemm_glds: ping-pong tiles take a plain A only"); return -1; }
+      if (p0.amode != A_PLAIN) { set_error("gemm_glds: ping-pong tiles take a plain A only"); return -1; }
+      const GemmParams& p = p0;
       const dim3 blk(512);
+      const bool dbg = g_gemm_debug == 2;
+      const int nbn = p.N / 256;
       if (id == 40256) {
-        const int nwg = ((p.M + 255) / 256) * (p.N / 256);
-        if (g_gemm_debug == 2)
-          hipLaunchKernelGGL((gemm_pp_kernel<A_PLAIN, 2, 256>), dim3(nwg), blk, 0, s, p);
+        const dim3 grd(((p.M + 255) / 256) * nbn);
+        if (dbg)
+          hipLaunchKernelGGL((gemm_pp_kernel<A_PLAIN, 2, 256>), grd, blk, 0, s, p);
         else
-          hipLaunchKernelGGL((gemm_pp_kernel<A_PLAIN, 0, 256>), dim3(nwg), blk, 0, s, p);
+          hipLaunchKernelGGL((gemm_pp_kernel<A_PLAIN, 0, 256>), grd, blk, 0, s, p);
       } else {
-        const int nwg = ((p.M + 127) / 128) * (p.N / 256);
-        if (g_gemm_debug == 2)
-          hipLaunchKernelGGL((gemm_pp_kernel<A_PLAIN, 2, 128>), dim3(nwg), blk, 0, s, p);
+        const dim3 grd(((p.M + 127) / 128) * nbn);
+        if (dbg)
+          hipLaunchKernelGGL((gemm_pp_kernel<A_PLAIN, 2, 128>), grd, blk, 0, s, p);
         else
-          hipLaunchKernelGGL((gemm_pp_kernel<A_PLAIN, 0, 128>), dim3(nwg), blk, 0, s, p);
+          hipLaunchKernelGGL((gemm_pp_kernel<A_PLAIN, 0, 128>), grd, blk, 0, s, p);
       }
       MEC_LAUNCH_CHECK();
       return 0;
@@ -717,7 +723,7 @@ static int tune_bn(const GemmParams& p, hipStream_t s, int* out_bn) {
   int best_bn = heuristic_bn(p);
   for (int bn : cands) {
     if (p.N % tile_bn(bn)) continue;
-    if ((bn == 40256 || bn == 41256) && p.amode != A_PLAIN) continue;
+    if (bn >= 40000 && bn < 50000 && p.amode != A_PLAIN) continue;
     MEC_TRY(launch_bn(p, s, bn));  // warm
     MEC_HIP(hipEventRecord(ev[0], s));
     for (int r = 0; r < REPS; ++r) {

@@ -12,7 +12,7 @@ predict_batch(ids, mask) for a device-resident [B,128] batch.
 
 import os
 import re
-from typing import Dict
+from typing import Dict, List
 
 import numpy as np
 
@@ -45,15 +45,27 @@ class _Cleaner:
         return text.strip()
 
 
-def _local_tokenizer():
+def _local_tokenizer(fast: bool = False):
+    """The reference's tokenizer (text_inference.py:39 -> preprocessing/text_preprocessing.py:24)
+    from the local BERT_MODEL_PATH only (never a by-name hub fetch). fast=True builds the
+    Rust WordPiece (BertTokenizerFast) from the same vocab, for batched encoding."""
     if not os.path.isdir(Config.BERT_MODEL_PATH):
         return None
     try:
-        from transformers import BertTokenizer
-        return BertTokenizer.from_pretrained(Config.BERT_MODEL_PATH, local_files_only=True)
+        from transformers import BertTokenizer, BertTokenizerFast
+        cls = BertTokenizerFast if fast else BertTokenizer
+        return cls.from_pretrained(Config.BERT_MODEL_PATH, local_files_only=True)
     except Exception as e:
         print(f"Warning: Could not load BERT tokenizer: {e}")
         return None
+
+
+def encode_batch(tokenizer, texts):
+    """Batched form of the reference's per-text call (text_inference.py:78-85): raw text (no
+    clean_text), [CLS]/[SEP], pad to / truncate at MAX_TEXT_LENGTH. -> int32 ids, mask [B,128]."""
+    enc = tokenizer(list(texts), add_special_tokens=True, max_length=Config.MAX_TEXT_LENGTH,
+                    padding='max_length', truncation=True, return_tensors='np')
+    return enc['input_ids'].astype(np.int32), enc['attention_mask'].astype(np.int32)
 
 
 class TextInference:
@@ -65,6 +77,7 @@ class TextInference:
         if w is not None:
             self.model = engine.TextEncoder(w, device=device)  # raises MecError without HIP/GPU
         self.tokenizer = tokenizer if tokenizer is not None else (_local_tokenizer() if self.model else None)
+        self._fast = None  # built on first batched call
         self.device = self.model.device if self.model is not None else None
 
     def _keyword_heuristic(self, text: str) -> Dict:
@@ -116,6 +129,24 @@ class TextInference:
         if self.model is None or self.tokenizer is None:
             return None, None
         return self._forward(*self._encode(text))
+
+    def encode_batch(self, texts):
+        """int32 ids / mask [B,128] for a list of strings (the fast tokenizer from the same
+        vocab when available: same ids as the reference's BertTokenizer, tests/test_tokenizer.py)."""
+        if self._fast is None and self.tokenizer is not None and not getattr(self.tokenizer, 'is_fast', False):
+            self._fast = _local_tokenizer(fast=True) or self.tokenizer
+        return encode_batch(self._fast or self.tokenizer, texts)
+
+    def predict_texts(self, texts) -> List[Dict]:
+        """Batched `predict`: one tokenizer call and one BERT forward for all texts."""
+        texts = list(texts)
+        if self.model is None or self.tokenizer is None:
+            return [self._keyword_heuristic(t) for t in texts]
+        if not texts:
+            return []
+        ids, mask = self.encode_batch(texts)
+        _, _, probs = self.model.forward(engine.to_device(ids, self.device), engine.to_device(mask, self.device))
+        return [self._as_dict(self.emotions, p) for p in probs.cpu().numpy()]
 
     def predict_batch(self, ids, mask):
         """ids/mask: device int32 [B,128] -> (cls [B,768], logits [B,7], probs [B,7])."""

@@ -115,6 +115,7 @@ def main():
                 run()
             except _lib.MecError as e:
                 print(json.dumps({'shape': name, 'impl': v[0], 'bn': v[1], 'error': str(e)}), flush=True)
+                setv(2, 0, 0)
                 continue
             ok.append(v)
         torch.cuda.synchronize()
