@@ -18,6 +18,8 @@
 //   with 16-byte loads/stores.
 // * XCD-aware bijective block remap: blocks that share an A panel share an L2.
 #include <algorithm>
+#include <cstdio>
+#include <cstdlib>
 #include <map>
 #include <mutex>
 
@@ -769,6 +771,9 @@ int launch_gemm_glds(const GemmParams& p, hipStream_t s, int force_bn) {
     }
     std::lock_guard<std::mutex> lk(g_tuned_mu);
     g_tuned[key] = bn;
+    if (getenv("MEC_GEMM_TRACE"))  // one line per distinct shape, at its first launch
+      fprintf(stderr, "MEC_GEMM amode=%d M=%d N=%d K=%d H=%d C=%d ks=%d stride=%d act=%d R=%d r_f32=%d tile=%d\n",
+              p.amode, p.M, p.N, p.K, p.H, p.C, p.ks, p.stride, p.act, p.R != nullptr, p.r_f32, bn);
   }
   return launch_bn(p, s, bn);
 }

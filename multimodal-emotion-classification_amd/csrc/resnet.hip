@@ -2,6 +2,7 @@
 // implicit-GEMM convs) -> avgpool + 2048->512->7 head (fp32), restating
 // inference/image_inference.py:28-32 (transform), :55-65 (network + head), :70-90 (512-d
 // fc[2] feature), :117-119 (softmax).
+#include <algorithm>
 #include <cmath>
 
 #include "block_ops.h"
@@ -106,9 +107,12 @@ int resize_u8(const uint8_t* in, int B, int H, int W, uint8_t* out, int OH, int 
 // ----------------------------------------------------------------------------- stem + maxpool
 // Fused conv7x7/2 + BN + ReLU (MFMA) + maxpool3x3/2 on the u8 224x224 image.
 // One workgroup = an 8x8 tile of pooled outputs = a 17x17 region of stem outputs (with the
-// pool's halo). The u8 39x39 input patch is converted once to f16 in LDS; each thread then
-// gathers a whole im2col row (49 taps at compile-time offsets from the row's patch base)
-// into a swizzled [320 x 64] f16 tile per channel, and the 7x7 conv runs on MFMA.
+// pool's halo), from a 40x46 input patch. K is ordered (channel, kh, kw) with kw padded to
+// 8 (and kh to 8): one 16-deep MFMA k step covers two kernel rows, one per lane half, so a
+// lane's A fragment for stem pixel (y, x) and kernel row kh is the 8 consecutive patch
+// pixels [2y+kh][2x .. 2x+7] (the 8th meets a zero weight). The patch is kept as four f16
+// copies shifted by 0/2/4/6 pixels, so that slice always starts 16-B aligned in copy x&3:
+// every A fragment is ONE ds_read_b128 straight from the patch (no im2col tile).
 // ToTensor/Normalize is folded into the weights; the -mean/std term summed over the
 // in-image taps depends only on the border class of the stem pixel (rows/cols 0, 1, 111
 // have out-of-image taps), so it is a [16 classes][64] table added in the epilogue.
@@ -118,7 +122,10 @@ int resize_u8(const uint8_t* in, int B, int H, int W, uint8_t* out, int OH, int 
 constexpr int SP_T = 8;              // pooled tile
 constexpr int SP_S = 2 * SP_T + 1;   // 17 stem rows/cols
 constexpr int SP_M = 320;            // 289 padded to 10 x 32
-constexpr int SP_P = 4 * SP_T + 7;   // 39 patch rows/cols
+constexpr int SP_R = 40;             // patch rows: 2*16 + 8 (kh padded to 8)
+constexpr int SP_W = 46;             // patch cols loaded: 2*16 + 8 + 6 (largest copy shift)
+constexpr int SP_CW = 40;            // cols per shifted copy
+constexpr int SP_COPY = SP_R * SP_CW + 32;  // halfs per copy, padded: copies land 12 bank slots apart
 constexpr int SO_LD = 72;            // stem-output row (f16), padded: 144 B
 
 __device__ __forceinline__ int sp_swz(int row, int kc) { return kc ^ ((row >> 1) & 7); }
@@ -126,106 +133,148 @@ __device__ __forceinline__ int sp_swz(int row, int kc) { return kc ^ ((row >> 1)
 // border class of a stem coordinate: 0 -> 0, 1 -> 1, 111 -> 3, else 2 (interior)
 __device__ __forceinline__ int sp_cls(int o) { return o == 0 ? 0 : (o == 1 ? 1 : (o == 111 ? 3 : 2)); }
 
-__global__ __launch_bounds__(256) void stem_pool_kernel(const uint8_t* __restrict__ img, int C,
+template <int C>
+__global__ __launch_bounds__(256, 2) void stem_pool_kernel(const uint8_t* __restrict__ img, int ntiles,
                                                         const f16* __restrict__ Wst, const float* __restrict__ bias,
                                                         const float* __restrict__ corr, f16* __restrict__ out) {
-  __shared__ __attribute__((aligned(16))) f16 sA[SP_M * SO_LD];  // im2col tile, later stem outputs
-  __shared__ __attribute__((aligned(16))) f16 sB[64 * 64];
-  __shared__ f16 sP[3 * SP_P * SP_P + 64];
-  __shared__ float sCorr[16 * 64];
+  // Persistent: each workgroup walks tiles blockIdx.x, +gridDim.x, ...; the weights, bias
+  // and border table are loaded once, and the next tile's patch bytes are fetched into
+  // registers while the current tile computes.
+  constexpr int PATCH = C * 4 * SP_COPY;
+  constexpr int SOH = SP_S * SP_S * SO_LD;  // live stem-output rows only
+  constexpr int SMEM = (PATCH + C * 64 * 64 > SOH) ? PATCH + C * 64 * 64 : SOH;
+  __shared__ __attribute__((aligned(16))) f16 smem[SMEM];  // patch copies + weights, later stem outputs
+  __shared__ float sCorr[16 * 64];  // border-class correction minus the interior one
+  __shared__ float sBias[64];       // bias + interior correction
+  f16* sP = smem;
+  f16* sB = smem + PATCH;
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
-  const int b = blockIdx.x / 49, t = blockIdx.x - b * 49;
-  const int ph0 = (t / 7) * SP_T, pw0 = (t - (t / 7) * 7) * SP_T;
-  const int sr0 = 2 * ph0 - 1, sc0 = 2 * pw0 - 1;       // first stem row/col of the region
-  const int ir0 = 2 * sr0 - 3, ic0 = 2 * sc0 - 3;       // first image row/col of the patch
-  const uint8_t* im = img + (size_t)b * 224 * 224 * C;
-  {  // issue every prologue load before any use: patch bytes, border-class table
-    constexpr int PER = (3 * SP_P * SP_P + 255) / 256;  // 18
-    uint32_t px[PER];
+  uint4 wreg[C][2];
 #pragma unroll
-    for (int j = 0; j < PER; ++j) {
-      const int i = tid + 256 * j;
-      px[j] = 0;
-      if (i < C * SP_P * SP_P) {
-        const int c = i / (SP_P * SP_P), rem = i - c * SP_P * SP_P;
-        const int pr = rem / SP_P, pc = rem - (rem / SP_P) * SP_P;
-        const int y = ir0 + pr, x = ic0 + pc;
-        if (y >= 0 && y < 224 && x >= 0 && x < 224) px[j] = im[((size_t)y * 224 + x) * C + c];
-      }
-    }
-    float cr[4];
+  for (int c = 0; c < C; ++c)
 #pragma unroll
-    for (int j = 0; j < 4; ++j) cr[j] = corr[tid + 256 * j];
-#pragma unroll
-    for (int j = 0; j < PER; ++j) {
-      const int i = tid + 256 * j;
-      if (i < C * SP_P * SP_P) sP[i] = (f16)(float)px[j];
+    for (int j = 0; j < 2; ++j) {
+      const int i = tid + 256 * j, n = i >> 3, kc = i & 7;
+      wreg[c][j] = *reinterpret_cast<const uint4*>(Wst + (size_t)n * 64 * C + c * 64 + kc * 8);
     }
 #pragma unroll
-    for (int j = 0; j < 4; ++j) sCorr[tid + 256 * j] = cr[j];
+  for (int j = 0; j < 4; ++j) {
+    const int i = tid + 256 * j;
+    sCorr[i] = corr[i] - corr[(2 * 4 + 2) * 64 + (i & 63)];
   }
+  if (tid < 64) sBias[tid] = bias[tid] + corr[(2 * 4 + 2) * 64 + tid];
+
+  // patch loader: thread -> a fixed pixel pair (cols 2k, 2k+1) walking rows r0, r0+11, ...;
+  // each shifted copy then gets one whole dword per pair (shifts are even)
+  constexpr int PAIRS = SP_W / 2;                   // 23 pairs per patch row
+  constexpr int RSTEP = 256 / PAIRS;                // 11 rows per sweep
+  constexpr int ITER = (SP_R + RSTEP - 1) / RSTEP;  // 4
+  const int k = tid % PAIRS, r0 = tid / PAIRS;      // tid < 253 active
+  const bool act = tid < PAIRS * RSTEP;
+  uint32_t px[C][ITER][2];
+  auto load_patch = [&](int tile) {
+    const int b = tile / 49, t = tile - (tile / 49) * 49;
+    const int ph0 = (t / 7) * SP_T, pw0 = (t - (t / 7) * 7) * SP_T;
+    const int ir0 = 2 * (2 * ph0 - 1) - 3, ic0 = 2 * (2 * pw0 - 1) - 3;
+    const uint8_t* im = img + (size_t)b * 224 * 224 * C;
+    const int x0 = ic0 + 2 * k;
+    const bool okx0 = x0 >= 0 && x0 < 224, okx1 = x0 + 1 >= 0 && x0 + 1 < 224;
+#pragma unroll
+    for (int c = 0; c < C; ++c)
+#pragma unroll
+      for (int j = 0; j < ITER; ++j) {
+        const int pr = r0 + RSTEP * j, y = ir0 + pr;
+        const bool oky = act && pr < SP_R && y >= 0 && y < 224;
+        const uint8_t* row = im + ((size_t)(oky ? y : 0) * 224) * C + c;
+        px[c][j][0] = (oky && okx0) ? row[(size_t)x0 * C] : 0u;
+        px[c][j][1] = (oky && okx1) ? row[(size_t)(x0 + 1) * C] : 0u;
+      }
+  };
   const int lr = lane & 31, lh = lane >> 5;
   const int jt = wave & 1;          // N tile (32 of the 64 channels)
   const int it0 = wave >> 1;        // row tiles it0, it0+2, ..., it0+8
-  floatx16 acc[5];
+  int aoff[5];                      // per row tile: this lane's stem pixel -> patch offset
 #pragma unroll
-  for (int q = 0; q < 5; ++q)
-#pragma unroll
-    for (int e = 0; e < 16; ++e) acc[q][e] = 0.f;
-  for (int ch = 0; ch < C; ++ch) {
-    __syncthreads();  // patch ready / previous chunk consumed
-    for (int i = tid; i < 64 * 8; i += 256) {  // weights (channel ch) -> sB, swizzled rows
-      const int n = i >> 3, kc = i & 7;
-      *reinterpret_cast<uint4*>(sB + n * 64 + sp_swz(n, kc) * 8) =
-          *reinterpret_cast<const uint4*>(Wst + (size_t)n * 64 * C + ch * 64 + kc * 8);
-    }
-    for (int m = tid; m < SP_M; m += 256) {  // one im2col row per thread
-      const int lrow = m / SP_S, lcol = m - (m / SP_S) * SP_S;
-      const bool valid = m < SP_S * SP_S;
-      const f16* src = sP + ch * SP_P * SP_P + (2 * lrow) * SP_P + 2 * lcol;
-#pragma unroll
-      for (int kc = 0; kc < 8; ++kc) {
-        half8 h;
-#pragma unroll
-        for (int e = 0; e < 8; ++e) {
-          const int k = kc * 8 + e;  // compile-time tap -> patch offset kh*39 + kw
-          h[e] = (k < 49 && valid) ? src[(k / 7) * SP_P + (k % 7)] : (f16)0.f;
-        }
-        *reinterpret_cast<half8*>(sA + m * 64 + sp_swz(m, kc) * 8) = h;
-      }
-    }
-    __syncthreads();
-#pragma unroll
-    for (int s = 0; s < 4; ++s) {
-      const int kcs = 2 * s + lh;
-      const int rb = 32 * jt + lr;
-      const half8 bf = *reinterpret_cast<const half8*>(sB + rb * 64 + sp_swz(rb, kcs) * 8);
-#pragma unroll
-      for (int q = 0; q < 5; ++q) {
-        const int ra = 32 * (it0 + 2 * q) + lr;
-        const half8 af = *reinterpret_cast<const half8*>(sA + ra * 64 + sp_swz(ra, kcs) * 8);
-        acc[q] = __builtin_amdgcn_mfma_f32_32x32x16_f16(af, bf, acc[q], 0, 0, 0);
-      }
-    }
+  for (int q = 0; q < 5; ++q) {
+    const int m = min(32 * (it0 + 2 * q) + lr, SP_S * SP_S - 1);  // pad rows read a valid pixel
+    const int y = m / SP_S, x = m - (m / SP_S) * SP_S;
+    aoff[q] = (x & 3) * SP_COPY + (2 * y + lh) * SP_CW + 8 * (x >> 2);
   }
-  __syncthreads();  // all MFMA reads of sA done before it is reused for stem outputs
-  {  // raw conv + (bias + interior correction) -> sO [m][SO_LD] f16 (padded rows: no conflicts)
-    const int col = 32 * jt + lr;
-    const float bv = bias[col] + sCorr[(2 * 4 + 2) * 64 + col];
-    f16* sO = sA;
+  int tile = blockIdx.x;
+  if (tile < ntiles) load_patch(tile);
+  for (; tile < ntiles; tile += gridDim.x) {
+    const int b = tile / 49, t = tile - (tile / 49) * 49;
+    const int ph0 = (t / 7) * SP_T, pw0 = (t - (t / 7) * 7) * SP_T;
+    const int sr0 = 2 * ph0 - 1, sc0 = 2 * pw0 - 1;  // first stem row/col of the region
+    __syncthreads();  // previous tile's pool reads done (first tile: tables written)
+#pragma unroll
+    for (int c = 0; c < C; ++c)
+#pragma unroll
+      for (int j = 0; j < ITER; ++j) {
+        const int pr = r0 + RSTEP * j;
+        if (act && pr < SP_R) {
+          typedef _Float16 h2 __attribute__((ext_vector_type(2)));
+          const h2 v = {(f16)(float)px[c][j][0], (f16)(float)px[c][j][1]};
+#pragma unroll
+          for (int sh = 0; sh < 4; ++sh) {  // copy sh holds patch[pr][jj + 2 sh]
+            const int jj = 2 * k - 2 * sh;
+            if (jj >= 0 && jj < SP_CW)
+              *reinterpret_cast<h2*>(sP + (c * 4 + sh) * SP_COPY + pr * SP_CW + jj) = v;
+          }
+        }
+      }
+#pragma unroll
+    for (int c = 0; c < C; ++c)
+#pragma unroll
+      for (int j = 0; j < 2; ++j) {
+        const int i = tid + 256 * j, n = i >> 3, kc = i & 7;
+        *reinterpret_cast<uint4*>(sB + c * 4096 + n * 64 + sp_swz(n, kc) * 8) = wreg[c][j];
+      }
+    if (tile + (int)gridDim.x < ntiles) load_patch(tile + gridDim.x);  // in flight under this tile
+    __syncthreads();  // patch copies + weights ready
+    floatx16 acc[5];
 #pragma unroll
     for (int q = 0; q < 5; ++q)
 #pragma unroll
-      for (int e = 0; e < 16; ++e) {
-        const int m = 32 * (it0 + 2 * q) + (e & 3) + 8 * (e >> 2) + 4 * lh;
-        sO[m * SO_LD + col] = (f16)(acc[q][e] + bv);
+      for (int e = 0; e < 16; ++e) acc[q][e] = 0.f;
+#pragma unroll
+    for (int ch = 0; ch < C; ++ch) {
+      const f16* pc = sP + ch * 4 * SP_COPY;
+#pragma unroll
+      for (int s = 0; s < 4; ++s) {  // k step s: kernel rows 2s (lanes 0-31) and 2s+1 (32-63)
+        const int kcs = 2 * s + lh;
+        const int rb = 32 * jt + lr;
+        const half8 bf = *reinterpret_cast<const half8*>(sB + ch * 4096 + rb * 64 + sp_swz(rb, kcs) * 8);
+#pragma unroll
+        for (int q = 0; q < 5; ++q) {
+          const half8 af = *reinterpret_cast<const half8*>(pc + aoff[q] + 2 * s * SP_CW);
+          acc[q] = __builtin_amdgcn_mfma_f32_32x32x16_f16(bf, af, acc[q], 0, 0, 0);  // D[channel][pixel]
+        }
       }
-  }
-  __syncthreads();
+    }
+    __syncthreads();  // all MFMA reads of the patch done before it is reused for stem outputs
+    {  // raw conv + (bias + interior correction) -> sO [m][SO_LD] f16; the accumulators are
+       // transposed (lane = stem pixel, 4 consecutive channels per register quad): 8-B writes
+      f16* sO = smem;
+#pragma unroll
+      for (int q = 0; q < 5; ++q) {
+        const int m = 32 * (it0 + 2 * q) + lr;
+        if (m < SP_S * SP_S) {
+#pragma unroll
+          for (int g = 0; g < 4; ++g) {
+            const int ch = 32 * jt + 8 * g + 4 * lh;
+            const half4 h = {(f16)(acc[q][4 * g + 0] + sBias[ch + 0]), (f16)(acc[q][4 * g + 1] + sBias[ch + 1]),
+                             (f16)(acc[q][4 * g + 2] + sBias[ch + 2]), (f16)(acc[q][4 * g + 3] + sBias[ch + 3])};
+            *reinterpret_cast<half4*>(sO + m * SO_LD + ch) = h;
+          }
+        }
+      }
+    }
+    __syncthreads();
   {  // ReLU + border correction + 3x3/2 max; thread -> (pooled pixel, 16 channels)
-    const f16* sO = sA;
-    const int px = tid >> 2, c0 = (tid & 3) * 16;
-    const int py = px >> 3, pxx = px & 7;
+    const f16* sO = smem;
+    const int pp = tid >> 2, c0 = (tid & 3) * 16;  // pooled pixel, first channel
+    const int py = pp >> 3, pxx = pp & 7;
     const bool border = ph0 == 0 || pw0 == 0 || ph0 + SP_T == 56 || pw0 + SP_T == 56;
     float m[16];
 #pragma unroll
@@ -245,10 +294,7 @@ __global__ __launch_bounds__(256) void stem_pool_kernel(const uint8_t* __restric
           const bool ok = oh >= 0 && oh < 112 && ow >= 0 && ow < 112;
           const int cls = sp_cls(oh) * 4 + sp_cls(ow);
 #pragma unroll
-          for (int c = 0; c < 16; ++c) {
-            const float d = sCorr[cls * 64 + c0 + c] - sCorr[(2 * 4 + 2) * 64 + c0 + c];
-            v[c] = ok ? v[c] + d : 0.f;
-          }
+          for (int c = 0; c < 16; ++c) v[c] = ok ? v[c] + sCorr[cls * 64 + c0 + c] : 0.f;  // sCorr = deltas now
         }
 #pragma unroll
         for (int c = 0; c < 16; ++c) m[c] = fmaxf(m[c], v[c]);
@@ -259,6 +305,7 @@ __global__ __launch_bounds__(256) void stem_pool_kernel(const uint8_t* __restric
     f16* o = out + (((size_t)b * 56 + ph0 + py) * 56 + pw0 + pxx) * 64 + c0;
     *reinterpret_cast<half8*>(o) = o0;
     *reinterpret_cast<half8*>(o + 8) = o1;
+  }
   }
 }
 
@@ -338,9 +385,9 @@ int ImageModel::create(const float* blob, size_t n) {
             const double mf = (double)(float)mean[c], sf = (double)(float)stdv[c];
             a += wv / (255.0 * sf);
             cc -= wv * mf / sf;
-            w[stem_rgb.w_off + (size_t)o * 192 + 64 * c + t] = (f16)(wv / (255.0 * sf) * scale[o]);
+            w[stem_rgb.w_off + (size_t)o * 192 + 64 * c + (t / 7) * 8 + t % 7] = (f16)(wv / (255.0 * sf) * scale[o]);
           }
-          w[stem.w_off + (size_t)o * 64 + t] = (f16)(a * scale[o]);
+          w[stem.w_off + (size_t)o * 64 + (t / 7) * 8 + t % 7] = (f16)(a * scale[o]);  // k = kh*8 + kw
           c0[o * 49 + t] = cc * scale[o];
         }
       // border classes of a stem coordinate: 0, 1, interior, 111 (see sp_cls)
@@ -448,8 +495,19 @@ int ImageModel::forward_u8(const uint8_t* img, int B, int H, int W, int C, float
   {  // fused stem conv 7x7/2 + BN + ReLU + maxpool 3x3/2 -> X [B,56,56,64]
     const ConvLayer& st = C == 3 ? stem_rgb : stem;
     MEC_TRY(prof.begin(TAG_RESNET_STEM, s));
-    hipLaunchKernelGGL(stem_pool_kernel, dim3(B * 49), dim3(256), 0, s, stem_in, C, Wt + st.w_off, P + st.b_off,
-                       P + stem_corr_off, X);
+    static int ncu = 0;
+    if (!ncu) {
+      int dev = 0;
+      MEC_HIP(hipGetDevice(&dev));
+      MEC_HIP(hipDeviceGetAttribute(&ncu, hipDeviceAttributeMultiprocessorCount, dev));
+    }
+    const int ntiles = B * 49;  // two resident workgroups per CU (VGPR-bound)
+    if (C == 3)
+      hipLaunchKernelGGL(stem_pool_kernel<3>, dim3(std::min(ntiles, 2 * ncu)), dim3(256), 0, s, stem_in, ntiles,
+                         Wt + st.w_off, P + st.b_off, P + stem_corr_off, X);
+    else
+      hipLaunchKernelGGL(stem_pool_kernel<1>, dim3(std::min(ntiles, 2 * ncu)), dim3(256), 0, s, stem_in, ntiles,
+                         Wt + st.w_off, P + st.b_off, P + stem_corr_off, X);
     MEC_LAUNCH_CHECK();
     MEC_TRY(prof.end(TAG_RESNET_STEM, s));
   }
