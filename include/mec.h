@@ -25,7 +25,11 @@ extern "C" {
 
 typedef struct mec_model mec_model;
 
-enum { MEC_SPEECH = 0, MEC_TEXT = 1, MEC_IMAGE = 2, MEC_FUSION = 3 };
+enum { MEC_SPEECH = 0, MEC_TEXT = 1, MEC_IMAGE = 2, MEC_FUSION = 3, MEC_IMAGE_MBV2 = 4 };
+/* MEC_IMAGE is the reference's ResNet50 image model (inference/image_inference.py:55-65);
+ * MEC_IMAGE_MBV2 the same head on a torchvision mobilenet_v2 backbone (README.md:13 names
+ * MobileNetV2; blob = state_dict order of mec/synthetic.py:image_mbv2_spec). Both kinds are
+ * accepted by mec_image_fwd / mec_image_fwd_u8. */
 
 /* Version / diagnostics. */
 const char* mec_version(void);
@@ -39,6 +43,7 @@ long long mec_blob_size(int kind);
  *   speech  tf.keras.models.load_model + joblib scaler   inference/speech_inference.py:21-28
  *   text    BertForSequenceClassification.from_pretrained inference/text_inference.py:40-43
  *   image   _build_model + load_state_dict               inference/image_inference.py:35-40
+ *           (MEC_IMAGE_MBV2: the same with base = mobilenet_v2, base.classifier = the head)
  *   fusion  _build_fusion_model + load_state_dict        inference/multimodal_fusion.py:43-56 */
 int mec_create(int kind, const float* host_blob, size_t n, int device, mec_model** out);
 int mec_destroy(mec_model* m);

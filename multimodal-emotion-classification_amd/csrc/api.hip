@@ -37,6 +37,19 @@ size_t blob_floats(int kind) {
         }
       return s + (size_t)512 * 2048 + 512 + 7 * 512 + 7;
     }
+    case KIND_IMAGE_MBV2: {
+      size_t s = 32 * 27 + 4 * 32;
+      const int set[7][4] = {{1, 16, 1, 1}, {6, 24, 2, 2}, {6, 32, 3, 2}, {6, 64, 4, 2}, {6, 96, 3, 1}, {6, 160, 3, 2}, {6, 320, 1, 1}};
+      int cin = 32;
+      for (int i = 0; i < 7; ++i)
+        for (int r = 0; r < set[i][2]; ++r) {
+          const size_t t = set[i][0], hid = cin * t, cout = set[i][1];
+          if (t != 1) s += hid * cin + 4 * hid;
+          s += hid * 9 + 4 * hid + cout * hid + 4 * cout;
+          cin = (int)cout;
+        }
+      return s + (size_t)1280 * 320 + 4 * 1280 + (size_t)512 * 1280 + 512 + 7 * 512 + 7;
+    }
     case KIND_FUSION: {
       size_t s = 0;
       const int d[3] = {64, 768, 512};
@@ -70,6 +83,17 @@ struct mec_model {
   }
 
 static hipStream_t S(void* s) { return reinterpret_cast<hipStream_t>(s); }
+
+// Image entry points take either backbone (ResNet50 or MobileNetV2).
+static ImageNet* image_net(mec_model* m) {
+  if (!m || !m->impl) { set_error("null model handle"); return nullptr; }
+  if (m->impl->kind != KIND_IMAGE && m->impl->kind != KIND_IMAGE_MBV2) {
+    set_error("model handle has the wrong kind for this call");
+    return nullptr;
+  }
+  if (hipSetDevice(m->impl->device) != hipSuccess) { set_error("hipSetDevice failed"); return nullptr; }
+  return static_cast<ImageNet*>(m->impl);
+}
 
 template <class T>
 static T* as(mec_model* m, int kind) {
@@ -107,6 +131,7 @@ int mec_create(int kind, const float* host_blob, size_t n, int device, mec_model
       case KIND_TEXT: { auto* p = new TextModel(); impl = p; rc = p->create(host_blob, n); break; }
       case KIND_IMAGE: { auto* p = new ImageModel(); impl = p; rc = p->create(host_blob, n); break; }
       case KIND_FUSION: { auto* p = new FusionModel(); impl = p; rc = p->create(host_blob, n); break; }
+      case KIND_IMAGE_MBV2: { auto* p = new MobileNetModel(); impl = p; rc = p->create(host_blob, n); break; }
     }
     if (rc != 0) { delete impl; return -1; }
     impl->kind = kind;
@@ -144,7 +169,7 @@ int mec_text_fwd(mec_model* m, const int32_t* ids, const int32_t* mask, int B, i
 int mec_image_fwd(mec_model* m, const uint8_t* gray, int B, float* feat, float* logits, float* probs,
                   void* stream) {
   API_GUARD({
-    auto* p = as<ImageModel>(m, KIND_IMAGE);
+    auto* p = image_net(m);
     if (!p) return -1;
     return p->forward(gray, B, feat, logits, probs, S(stream));
   })
@@ -153,7 +178,7 @@ int mec_image_fwd(mec_model* m, const uint8_t* gray, int B, float* feat, float* 
 int mec_image_fwd_u8(mec_model* m, const uint8_t* img, int B, int H, int W, int C, float* feat, float* logits,
                      float* probs, void* stream) {
   API_GUARD({
-    auto* p = as<ImageModel>(m, KIND_IMAGE);
+    auto* p = image_net(m);
     if (!p) return -1;
     return p->forward_u8(img, B, H, W, C, feat, logits, probs, S(stream));
   })

@@ -186,6 +186,7 @@ __global__ __launch_bounds__(256, 2) void gemm_f16_kernel(const GemmParams p) {
           }
           if (p.act == ACT_RELU) v = fmaxf(v, 0.f);
           else if (p.act == ACT_GELU) v = gelu_erf(v);
+          else if (p.act == ACT_RELU6) v = fminf(fmaxf(v, 0.f), 6.f);
           if (p.C16) p.C16[idx] = (f16)v;
           if (p.C32) p.C32[idx] = v;
         }

@@ -162,6 +162,9 @@ __device__ __forceinline__ void gemm_epilogue(const GemmParams& p, accv (&acc)[T
       if (p.act == ACT_RELU) {
 #pragma unroll
         for (int q = 0; q < 8; ++q) v[q] = fmaxf(v[q], 0.f);
+      } else if (p.act == ACT_RELU6) {
+#pragma unroll
+        for (int q = 0; q < 8; ++q) v[q] = fminf(fmaxf(v[q], 0.f), 6.f);
       } else if (p.act == ACT_GELU) {
 #pragma unroll
         for (int q = 0; q < 8; q += 2) {

@@ -55,6 +55,8 @@ enum KernelTag : int {
   TAG_RESNET_STEM = 9,
   TAG_SPEECH = 10,
   TAG_FUSION = 11,
+  TAG_MBV2_BLOCK = 12,
+  TAG_MBV2_LAST = 13,
 };
 
 // hipEvent pairs recorded around every launch whose tag matches `tag`.
@@ -99,7 +101,7 @@ struct BlobReader {
 // C[M,N] = epilogue( A'[M,K] . B[N,K]^T ), A' = A (plain) or the im2col view of an NHWC
 // tensor (conv).
 enum AMode : int { A_PLAIN = 0, A_CONV = 1, A_DUAL = 2 };
-enum Act : int { ACT_NONE = 0, ACT_RELU = 1, ACT_GELU = 2 };
+enum Act : int { ACT_NONE = 0, ACT_RELU = 1, ACT_GELU = 2, ACT_RELU6 = 3 };
 
 struct GemmParams {
   const void* A = nullptr;   // f16 [M,K] | f16 NHWC [n,H,W,C]

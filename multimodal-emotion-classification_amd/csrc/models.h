@@ -6,7 +6,7 @@
 
 namespace mec {
 
-enum ModelKind : int { KIND_SPEECH = 0, KIND_TEXT = 1, KIND_IMAGE = 2, KIND_FUSION = 3 };
+enum ModelKind : int { KIND_SPEECH = 0, KIND_TEXT = 1, KIND_IMAGE = 2, KIND_FUSION = 3, KIND_IMAGE_MBV2 = 4 };
 
 size_t blob_floats(int kind);
 
@@ -50,6 +50,17 @@ struct TextModel : Model {
               float* probs, hipStream_t s);
 };
 
+// ---------------------------------------------------------------- image encoders
+// Both backbones take the same u8 inputs and produce the same (512-d feature, logits, probs).
+struct ImageNet : Model {
+  // img u8 [B,H,W,C]: (48,48,1) gray FER2013 (GPU resize), (224,224,1) gray, (224,224,3) RGB
+  virtual int forward_u8(const uint8_t* img, int B, int H, int W, int C, float* feat, float* logits, float* probs,
+                         hipStream_t s) = 0;
+  int forward(const uint8_t* gray, int B, float* feat, float* logits, float* probs, hipStream_t s) {
+    return forward_u8(gray, B, 48, 48, 1, feat, logits, probs, s);
+  }
+};
+
 // ---------------------------------------------------------------- ResNet50 + head
 struct ConvLayer {
   size_t w_off = 0;   // f16 [Cout][kh][kw][Cin] (BN scale folded)
@@ -61,7 +72,7 @@ struct Bottleneck {
   bool has_ds = false;
   size_t c3ds_w_off = 0, c3ds_b_off = 0;  // block 0: [conv3 | downsample] weights [4w][w+cin], summed bias
 };
-struct ImageModel : Model {
+struct ImageModel : ImageNet {
   DevBuf wts;   // f16 conv weights
   DevBuf prm;   // fp32 biases, stem weights, head
   DevBuf ws;    // workspace
@@ -72,10 +83,31 @@ struct ImageModel : Model {
   std::vector<Bottleneck> blocks;
   size_t fc1_off = 0, fc1b_off = 0, fc2_off = 0, fc2b_off = 0;
   int create(const float* blob, size_t n);
-  int forward(const uint8_t* gray, int B, float* feat, float* logits, float* probs, hipStream_t s);
-  // img u8 [B,H,W,C]: (48,48,1) gray FER2013 (GPU resize), (224,224,1) gray, (224,224,3) RGB
   int forward_u8(const uint8_t* img, int B, int H, int W, int C, float* feat, float* logits, float* probs,
-                 hipStream_t s);
+                 hipStream_t s) override;
+};
+
+// ---------------------------------------------------------------- MobileNetV2 + head
+// One inverted-residual block (features[1..17]) as packed for mbv2_block_kernel: channel
+// counts padded (cin -> cinp % 32, hidden -> hidp % 32, cout -> coutp % 16) with zero weights.
+struct MbBlock {
+  int t = 1, cin = 0, hid = 0, cout = 0, stride = 1;
+  int cinp = 0, hidp = 0, coutp = 0;
+  size_t we_off = 0, wp_off = 0;          // f16: expand [hidp][cinp], project [coutp][hidp]
+  size_t be_off = 0, wd_off = 0, bd_off = 0, bp_off = 0;  // f32: expand bias, dw [hidp/8][9][8], dw bias, project bias
+};
+struct MobileNetModel : ImageNet {
+  DevBuf wts;   // f16 1x1 weights
+  DevBuf prm;   // fp32 stem, depthwise weights, biases, head
+  DevBuf ws;    // workspace
+  int ws_batch = 0;
+  size_t stem_w_off = 0, stem_rgb_off = 0, stem_corr_off = 0;  // f32 [9][32], [3*9][32], [4 classes][32]
+  std::vector<MbBlock> blocks;
+  size_t last_w_off = 0, last_b_off = 0;  // features[18]: f16 [1280][320], f32 [1280]
+  size_t fc1_off = 0, fc1b_off = 0, fc2_off = 0, fc2b_off = 0;
+  int create(const float* blob, size_t n);
+  int forward_u8(const uint8_t* img, int B, int H, int W, int C, float* feat, float* logits, float* probs,
+                 hipStream_t s) override;
 };
 
 int resize_u8(const uint8_t* in, int B, int H, int W, uint8_t* out, int OH, int OW, hipStream_t s);

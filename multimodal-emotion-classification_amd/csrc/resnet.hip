@@ -311,14 +311,6 @@ __global__ __launch_bounds__(256, 2) void stem_pool_kernel(const uint8_t* __rest
 
 // ----------------------------------------------------------------------------- avgpool
 // AdaptiveAvgPool2d(1) on NHWC f16 -> f32 [B, C]: one thread per (sample, channel).
-__global__ __launch_bounds__(256) void avgpool_kernel(const f16* __restrict__ x, int HW, int C, float* __restrict__ y) {
-  const int b = blockIdx.x, c = blockIdx.y * 256 + threadIdx.x;
-  if (c >= C) return;
-  const f16* p = x + (size_t)b * HW * C + c;
-  float s = 0.f;
-  for (int q = 0; q < HW; ++q) s += (float)p[(size_t)q * C];
-  y[(size_t)b * C + c] = s / (float)HW;
-}
 
 // ----------------------------------------------------------------------------- model
 static const int kLayers[4][3] = {{64, 3, 1}, {128, 4, 2}, {256, 6, 2}, {512, 3, 2}};
@@ -454,10 +446,6 @@ int ImageModel::create(const float* blob, size_t n) {
   MEC_TRY(upload(wts, w.data(), w.size() * sizeof(f16)));
   MEC_TRY(upload(prm, pr.data(), pr.size() * sizeof(float)));
   return ensure_taps();
-}
-
-int ImageModel::forward(const uint8_t* gray, int B, float* feat, float* logits, float* probs, hipStream_t s) {
-  return forward_u8(gray, B, 48, 48, 1, feat, logits, probs, s);
 }
 
 int ImageModel::forward_u8(const uint8_t* img, int B, int H, int W, int C, float* feat, float* logits, float* probs,

@@ -9,7 +9,10 @@ torchvision makes) and uploaded as u8 224x224, gray (1 channel) or RGB (3 channe
 labels are Config.EMOTIONS[argmax] exactly like the reference (:121-123), including its
 class-order quirk against ImageFolder's alphabetical training order.
 
-Added beyond the reference: predict_array(u8 image) and predict_batch(u8 [B,48,48]).
+Added beyond the reference: predict_array(u8 image) and predict_batch(u8 [B,48,48]), and
+`backbone='mobilenet_v2'` (README.md:13 names MobileNetV2 as the image model; the reference
+code builds ResNet50): the same transform, head, feature and result dicts on a
+torchvision-mobilenet_v2 backbone (csrc/mobilenet.hip; parity unpinned, no reference code).
 """
 
 from typing import Dict
@@ -33,13 +36,19 @@ def _to_model_input(image) -> np.ndarray:
     return np.ascontiguousarray(r[..., :1] if gray else r)
 
 
+_KINDS = {'resnet50': 'image', 'mobilenet_v2': 'image_mbv2'}
+
+
 class ImageInference:
-    def __init__(self, weights=None, seed=None, device=None):
+    def __init__(self, weights=None, seed=None, device=None, backbone='resnet50'):
+        if backbone not in _KINDS:
+            raise ValueError(f'backbone must be one of {sorted(_KINDS)}')
         self.emotions = Config.EMOTIONS
+        self.backbone = backbone
         self.model = None
-        w = checkpoints.resolve('image', weights, seed)
-        if w is not None:
-            self.model = engine.ImageEncoder(w, device=device)  # raises MecError without HIP/GPU
+        w = checkpoints.resolve(_KINDS[backbone], weights, seed)
+        if w is not None:  # raises MecError without HIP/GPU
+            self.model = engine.IMAGE_BACKBONES[backbone](w, device=device)
         self.device = self.model.device if self.model is not None else None
 
     def _fallback(self) -> Dict:

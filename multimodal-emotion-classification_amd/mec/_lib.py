@@ -41,7 +41,8 @@ SIGNATURES = {
 
 # Kernel tags for mec_prof_enable (csrc/mec_common.h KernelTag).
 TAGS = {'bert_qkv': 1, 'bert_attn': 2, 'bert_oproj': 3, 'bert_ffn1': 4, 'bert_ffn2': 5, 'bert_ln': 6,
-        'resnet_conv3x3': 7, 'resnet_conv1x1': 8, 'resnet_stem': 9, 'speech': 10, 'fusion': 11}
+        'resnet_conv3x3': 7, 'resnet_conv1x1': 8, 'resnet_stem': 9, 'speech': 10, 'fusion': 11,
+        'mbv2_blocks': 12, 'mbv2_last': 13}
 
 
 class MecError(RuntimeError):

@@ -10,7 +10,8 @@ image_inference.py:105-106, multimodal_fusion.py:204-205). Order of precedence:
        text    BERT_MODEL_PATH/ (HF save_pretrained: model.safetensors | pytorch_model.bin),
                text_inference.py:40-41, train_text_model.py:221-222
        image   IMAGE_MODEL_PATH with .h5 -> .pt (state_dict), image_inference.py:35-38,
-               train_image_model.py:273
+               train_image_model.py:273 (image_mbv2: the same file holding a mobilenet_v2
+               `base.features.*` / `base.classifier.*` state_dict)
        fusion  FUSION_MODEL_PATH with .pkl -> .pt ({'model_state_dict','config'}),
                multimodal_fusion.py:41-54, train_fusion_model.py:609-618
        speech  a Keras .h5 needs h5py/TensorFlow (absent): use speech_weights.npz, written by
@@ -60,7 +61,7 @@ def load_checkpoint(kind: str):
             return _conform(kind, load_file(st))
         pt = os.path.join(d, 'pytorch_model.bin')
         return _conform(kind, _to_np(_torch_load(pt)))
-    if kind == 'image':
+    if kind in ('image', 'image_mbv2'):  # same file; the backbone is told by the state_dict keys
         return _conform(kind, _to_np(_torch_load(Config.IMAGE_MODEL_PATH.replace('.h5', '.pt'))))
     if kind == 'fusion':
         ck = _torch_load(Config.FUSION_MODEL_PATH.replace('.pkl', '.pt'))

@@ -158,6 +158,14 @@ class ImageEncoder(HipModel):
         return feat, logits, probs
 
 
+class MobileNetImageEncoder(ImageEncoder):
+    """The same image entry points on the MobileNetV2 backbone (csrc/mobilenet.hip)."""
+    kind = 'image_mbv2'
+
+
+IMAGE_BACKBONES = {'resnet50': ImageEncoder, 'mobilenet_v2': MobileNetImageEncoder}
+
+
 class FusionHead(HipModel):
     kind = 'fusion'
 
@@ -218,11 +226,12 @@ class FusedPipeline:
     serially so each GEMM shape is autotuned in isolation.
     """
 
-    def __init__(self, seed: int = 1234, device=None, weights=None, concurrent: bool = True):
+    def __init__(self, seed: int = 1234, device=None, weights=None, concurrent: bool = True,
+                 image_backbone: str = 'resnet50'):
         weights = weights or {}
         self.speech = SpeechEncoder(weights.get('speech'), seed, device)
         self.text = TextEncoder(weights.get('text'), seed, device)
-        self.image = ImageEncoder(weights.get('image'), seed, device)
+        self.image = IMAGE_BACKBONES[image_backbone](weights.get('image'), seed, device)
         self.fusion = FusionHead(weights.get('fusion'), seed, device)
         self.device = self.speech.device
         self.concurrent = concurrent

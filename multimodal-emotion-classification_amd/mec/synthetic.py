@@ -15,6 +15,8 @@ Tensor names/shapes follow the reference's own layouts:
   text    HF BertForSequenceClassification state_dict (text_inference.py:41)
   image   ImageEmotionModel state_dict: torchvision resnet50 under `base.` with the
           2048->512->7 head (image_inference.py:55-65)
+  image_mbv2  the same model on torchvision mobilenet_v2 (README.md:13): `base.features`
+          + a 1280->512->7 `base.classifier` head (no reference code: parity unpinned)
   fusion  MultiModalFusionModel state_dict (multimodal_fusion.py:108-154)
 """
 from __future__ import annotations
@@ -136,6 +138,61 @@ def image_spec():
     return s
 
 
+# MobileNetV2 (torchvision mobilenet_v2(weights=None), width 1.0): inverted-residual
+# settings (t, c, n, s) and the same Dropout/Linear(.,512)/ReLU/Dropout/Linear(512,7) head the
+# reference puts on ResNet50 (image_inference.py:59-65), here as base.classifier (README.md:13
+# names MobileNetV2 as the image model; the reference ships no MobileNetV2 code).
+MBV2_SETTINGS = [(1, 16, 1, 1), (6, 24, 2, 2), (6, 32, 3, 2), (6, 64, 4, 2), (6, 96, 3, 1), (6, 160, 3, 2),
+                 (6, 320, 1, 1)]
+MBV2_LAST = 1280
+MBV2_GAMMA = ((4.0, 8.0), (0.8, 1.2), (0.4, 0.8))  # BN gamma ranges: stem, expand / depthwise, projections
+
+
+def mbv2_blocks():
+    """[(t, cin, hidden, cout, stride)] for features[1..17]."""
+    out, cin = [], 32
+    for t, c, n, s in MBV2_SETTINGS:
+        for i in range(n):
+            out.append((t, cin, cin * t, c, s if i == 0 else 1))
+            cin = c
+    return out
+
+
+def image_mbv2_spec():
+    s = []
+
+    def conv(name, co, ci, k, groups=1):
+        s.append((name, (co, ci // groups, k, k), 'u', float(np.sqrt(6.0 / (ci // groups * k * k)))))
+
+    def bn(name, c, gamma=(0.8, 1.2)):
+        s.extend([(name + '.weight', (c,), 'r', gamma),
+                  (name + '.bias', (c,), 'r', (-0.1, 0.1)),
+                  (name + '.running_mean', (c,), 'r', (-0.1, 0.1)),
+                  (name + '.running_var', (c,), 'r', (0.8, 1.2))])
+
+    # BN scales (MBV2_GAMMA): every ReLU6 zeroes and saturates part of its inputs, yet the
+    # net stays well conditioned (an f16 storage of every activation moves the probs by
+    # < 1e-4 in fp32 emulation; larger gammas make the random net chaotic)
+    stem, act, proj = MBV2_GAMMA
+    conv('base.features.0.0.weight', 32, 3, 3); bn('base.features.0.1', 32, gamma=stem)
+    for i, (t, cin, hid, cout, st) in enumerate(mbv2_blocks()):
+        p = f'base.features.{i + 1}.conv.'
+        if t == 1:
+            conv(p + '0.0.weight', hid, hid, 3, groups=hid); bn(p + '0.1', hid, gamma=act)
+            conv(p + '1.weight', cout, hid, 1); bn(p + '2', cout, gamma=proj)
+        else:
+            conv(p + '0.0.weight', hid, cin, 1); bn(p + '0.1', hid, gamma=act)
+            conv(p + '1.0.weight', hid, hid, 3, groups=hid); bn(p + '1.1', hid, gamma=act)
+            conv(p + '2.weight', cout, hid, 1); bn(p + '3', cout, gamma=proj)
+    conv('base.features.18.0.weight', MBV2_LAST, 320, 1); bn('base.features.18.1', MBV2_LAST, gamma=act)
+    a1 = 1.0 / np.sqrt(float(MBV2_LAST))
+    a2 = 1.0 / np.sqrt(512.0)
+    s += [('base.classifier.1.weight', (512, MBV2_LAST), 'u', a1), ('base.classifier.1.bias', (512,), 'u', a1),
+          ('base.classifier.4.weight', (NUM_CLASSES, 512), 'u', a2),
+          ('base.classifier.4.bias', (NUM_CLASSES,), 'u', 0.05)]
+    return s
+
+
 FUSION_HIDDEN = 256
 FUSION_DIMS = {'speech': 64, 'text': 768, 'image': 512}
 
@@ -172,8 +229,9 @@ def fusion_spec():
     return s
 
 
-SPECS = {'speech': speech_spec, 'text': text_spec, 'image': image_spec, 'fusion': fusion_spec}
-KIND_IDS = {'speech': 0, 'text': 1, 'image': 2, 'fusion': 3}
+SPECS = {'speech': speech_spec, 'text': text_spec, 'image': image_spec, 'fusion': fusion_spec,
+         'image_mbv2': image_mbv2_spec}
+KIND_IDS = {'speech': 0, 'text': 1, 'image': 2, 'fusion': 3, 'image_mbv2': 4}
 
 
 def spec(kind: str):

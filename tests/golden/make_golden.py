@@ -17,6 +17,8 @@ What each fixture is pinned to:
                     call torchvision's Resize makes (inference/image_inference.py:29, :112).
   speech.npz        oracle/speech.py restatement (TensorFlow absent: restatement-pinned).
   image_full.npz    oracle/image.py restatement (torchvision absent: restatement-pinned).
+  image_mbv2.npz    oracle/image_mbv2.py restatement (MobileNetV2 backbone; no reference code
+                    and torchvision absent: restatement-pinned). `--only mbv2` writes just it.
 Only inputs (seeded), seeds and outputs are stored; weights are regenerated from seeds.
 """
 import importlib.util
@@ -151,7 +153,21 @@ def main():
     f, l, p = o_image.forward(wi, g2)
     np.savez_compressed(os.path.join(HERE, 'image_full.npz'), wseed=WSEED, gray=g2, feat=f, logits=l, probs=p)
     print('speech.npz, image_full.npz written')
+    write_mbv2(syn)
+
+
+def write_mbv2(syn):
+    sys.path.insert(0, REPO)
+    from oracle import image_mbv2 as o_mbv2
+    w = syn.weights('image_mbv2', WSEED)
+    g = syn.image_inputs(2, seed=17)
+    f, l, p = o_mbv2.forward(w, g)
+    np.savez_compressed(os.path.join(HERE, 'image_mbv2.npz'), wseed=WSEED, gray=g, feat=f, logits=l, probs=p)
+    print('image_mbv2.npz written')
 
 
 if __name__ == '__main__':
-    main()
+    if sys.argv[1:] == ['--only', 'mbv2']:
+        write_mbv2(load_synthetic())
+    else:
+        main()

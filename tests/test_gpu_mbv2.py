@@ -1,0 +1,79 @@
+"""GPU parity of the MobileNetV2 image backbone (csrc/mobilenet.hip) vs the CPU oracle
+(oracle/image_mbv2.py) and its fixture. Parity unpinned beyond the restatement (no
+reference code for MobileNetV2; torchvision absent). Tolerance as north_star: probs within
+1e-3, argmax exact on clear-margin samples."""
+import numpy as np
+import pytest
+import torch
+
+from mec import engine, synthetic as syn
+from oracle import image_mbv2 as o_mb
+
+pytestmark = pytest.mark.gpu
+
+PROB_TOL = 1e-3
+
+
+@pytest.fixture(scope='module')
+def mb(dev):
+    return engine.MobileNetImageEncoder(device=dev)
+
+
+def _np(ts):
+    torch.cuda.synchronize()
+    return [t.cpu().numpy() for t in ts]
+
+
+def _check(got, ref):
+    feat, logits, probs = got
+    rf, rl, rp = ref
+    assert np.abs(probs - rp).max() < PROB_TOL
+    assert np.abs(logits - rl).max() < 5e-3
+    assert np.abs(feat - rf).max() < 0.02 * max(1.0, np.abs(rf).max())
+    srt = np.sort(rp, axis=1)
+    clear = (srt[:, -1] - srt[:, -2]) > 2 * PROB_TOL
+    assert np.array_equal(rp.argmax(1)[clear], probs.argmax(1)[clear])
+
+
+def test_mbv2_golden(mb, dev, golden):
+    g = golden('image_mbv2.npz')
+    _check(_np(mb.forward(engine.to_device(g['gray'], dev))), (g['feat'], g['logits'], g['probs']))
+
+
+@pytest.mark.parametrize('B', [1, 3, 16])
+def test_mbv2_vs_oracle(mb, dev, B):
+    gray = syn.image_inputs(B, seed=300 + B)
+    _check(_np(mb.forward(engine.to_device(gray, dev))), o_mb.forward(syn.weights('image_mbv2'), gray))
+
+
+@pytest.mark.parametrize('C', [1, 3])
+def test_mbv2_resized_inputs(mb, dev, C):
+    img = syn.randint(7 + C, 'in/mbv2_resized', (3, 224, 224, C), 0, 256).astype(np.uint8)
+    got = _np(mb.forward_u8(engine.to_device(img, dev)))
+    _check(got, o_mb.forward_resized(syn.weights('image_mbv2'), img if C == 3 else img[..., 0]))
+
+
+def test_mbv2_border_pixels(mb, dev):
+    # saturated and zero images stress the stem's border-class bias and the ReLU6 clamps
+    gray = np.zeros((4, 48, 48), np.uint8)
+    gray[1] = 255
+    gray[2, :, :24] = 255
+    gray[3, ::2] = 255
+    _check(_np(mb.forward(engine.to_device(gray, dev))), o_mb.forward(syn.weights('image_mbv2'), gray))
+
+
+def test_mbv2_batch_invariance(mb, dev):
+    gray = syn.image_inputs(64, seed=9)
+    full = _np(mb.forward(engine.to_device(gray, dev)))[1]
+    part = _np(mb.forward(engine.to_device(gray[17:20], dev)))[1]
+    np.testing.assert_array_equal(full[17:20], part)
+
+
+def test_image_inference_mbv2(dev):
+    from inference.image_inference import ImageInference
+    inf = ImageInference(seed=1234, device=dev, backbone='mobilenet_v2')
+    gray = syn.image_inputs(1, seed=21)[0]
+    r = inf.predict_array(gray)
+    rp = o_mb.forward(syn.weights('image_mbv2'), gray[None])[2][0]
+    assert abs(r['confidence'] - float(rp.max())) < PROB_TOL
+    assert len(r['all_probabilities']) == 7

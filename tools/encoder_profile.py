@@ -22,7 +22,7 @@ from mec import engine, synthetic as syn  # noqa: E402
 
 def main():
     ap = argparse.ArgumentParser()
-    ap.add_argument('--enc', choices=['text', 'image', 'speech', 'fusion', 'pipeline'], required=True)
+    ap.add_argument('--enc', choices=['text', 'image', 'image_mbv2', 'speech', 'fusion', 'pipeline'], required=True)
     ap.add_argument('--iters', type=int, default=5)
     ap.add_argument('--batch', type=int, default=256)
     a = ap.parse_args()
@@ -35,6 +35,10 @@ def main():
         fn = lambda: m.forward(*args)  # noqa: E731
     elif a.enc == 'image':
         m = engine.ImageEncoder(device=dev)
+        g = engine.to_device(syn.image_inputs(B, seed=0), dev)
+        fn = lambda: m.forward(g)  # noqa: E731
+    elif a.enc == 'image_mbv2':
+        m = engine.MobileNetImageEncoder(device=dev)
         g = engine.to_device(syn.image_inputs(B, seed=0), dev)
         fn = lambda: m.forward(g)  # noqa: E731
     elif a.enc == 'speech':
