@@ -43,9 +43,13 @@ struct MbArgs {
 
 __device__ __forceinline__ float relu6f(float v) { return fminf(fmaxf(v, 0.f), 6.f); }
 
-// S stride, TO output tile side, CINP / COUTP padded channel counts, EXPAND (t != 1),
+// S stride, TO output tile side, CINP / HIDP / COUTP padded channel counts, EXPAND (t != 1),
 // RES (stride 1 and cin == cout), STEM: 0 = input from HBM, 1 / 3 = stem from u8 gray / RGB.
-template <int S, int TO, int CINP, int COUTP, bool EXPAND, bool RES, int STEM>
+// Latency: every global load a phase needs is issued a phase early (the input tile in one
+// unrolled burst; depthwise weights and all biases staged in LDS next to it; the project
+// weights of chunk c at the start of chunk c; the expand weights of chunk c+1 right after
+// chunk c's expand), so a chunk costs its LDS/MFMA/VALU work, not three load round trips.
+template <int S, int TO, int CINP, int HIDP, int COUTP, bool EXPAND, bool RES, int STEM>
 __global__ __launch_bounds__(256) void mbv2_block_kernel(const MbArgs a) {
   constexpr int IR = (TO - 1) * S + 3;        // input tile side (with halo)
   constexpr int NP = IR * IR;
@@ -55,12 +59,20 @@ __global__ __launch_bounds__(256) void mbv2_block_kernel(const MbArgs a) {
   constexpr int OLD = COUTP + 8;
   constexpr int NQ = TO * TO;                 // output pixels (<= 64: four 16-pixel tiles)
   constexpr int OT = COUTP / 16;              // project M tiles
+  constexpr int KX = CINP / 32;               // expand k steps
   static_assert(NQ <= 64, "tile");
-  static_assert(!STEM || (CINP == 32 && !EXPAND && S == 1), "stem fuses into block 1 only");
+  static_assert(!STEM || (CINP == 32 && HIDP == 32 && !EXPAND && S == 1), "stem fuses into block 1 only");
   __shared__ __attribute__((aligned(16))) f16 sX[MP * XLD];
   __shared__ __attribute__((aligned(16))) f16 sE[EXPAND ? MP * ELD : 8];
   __shared__ __attribute__((aligned(16))) f16 sD[64 * ELD];
   __shared__ __attribute__((aligned(16))) f16 sO[64 * OLD];
+  __shared__ __attribute__((aligned(16))) float sWd[HIDP * 9];   // [HIDP/8][9][8]
+  __shared__ __attribute__((aligned(16))) float sBd[HIDP];
+  __shared__ __attribute__((aligned(16))) float sBe[EXPAND ? HIDP : 4];
+  __shared__ __attribute__((aligned(16))) float sBp[COUTP];
+  constexpr int PR = 2 * (TO + 2) + 1;        // stem: u8 patch side (STEM > 0)
+  __shared__ __attribute__((aligned(16))) float sSW[STEM ? STEM * 9 * 32 : 4];
+  __shared__ uint8_t sPatch[STEM ? PR * PR * STEM : 4];
 
   const int tid = threadIdx.x, lane = tid & 63;
   const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
@@ -70,24 +82,62 @@ __global__ __launch_bounds__(256) void mbv2_block_kernel(const MbArgs a) {
   const int oy0 = (tt / tpr) * TO, ox0 = (tt - (tt / tpr) * tpr) * TO;
   const int iy0 = oy0 * S - 1, ix0 = ox0 * S - 1;  // input tile origin (pad 1)
   const int H = a.H;
+  const int l16 = lane & 15, lq = lane >> 4;
+
+  // ---- per-block constants -> LDS (float4 copies; every count is a multiple of 4)
+  for (int i = tid; i < HIDP * 9 / 4; i += 256)
+    reinterpret_cast<float4*>(sWd)[i] = reinterpret_cast<const float4*>(a.Wd)[i];
+  for (int i = tid; i < HIDP / 4; i += 256) {
+    reinterpret_cast<float4*>(sBd)[i] = reinterpret_cast<const float4*>(a.bd)[i];
+    if constexpr (EXPAND) reinterpret_cast<float4*>(sBe)[i] = reinterpret_cast<const float4*>(a.be)[i];
+  }
+  if (tid < COUTP / 4) reinterpret_cast<float4*>(sBp)[tid] = reinterpret_cast<const float4*>(a.bp)[tid];
+
+  // expand weights of the first chunk (A fragments, rows = hidden channels)
+  half8 af[2][KX];
+  if constexpr (EXPAND) {
+#pragma unroll
+    for (int ht = 0; ht < 2; ++ht)
+#pragma unroll
+      for (int k = 0; k < KX; ++k)
+        af[ht][k] = *reinterpret_cast<const half8*>(a.We + (size_t)(16 * ht + l16) * CINP + 32 * k + 8 * lq);
+  }
 
   // ---- stage the block input tile: sX[p][c], zeros outside the image and past cin
   if constexpr (STEM == 0) {
     constexpr int C8 = CINP / 8;
+    constexpr int NIT = (MP * C8 + 255) / 256;
     const f16* xin = a.x + (size_t)n * H * H * a.cin;
-    for (int i = tid; i < MP * C8; i += 256) {
+    half8 v[NIT];
+#pragma unroll
+    for (int j = 0; j < NIT; ++j) {  // all loads first ...
+      const int i = tid + 256 * j;
       const int p = i / C8, c8 = i - (i / C8) * C8;
       const int py = p / IR, px = p - (p / IR) * IR;
       const int iy = iy0 + py, ix = ix0 + px;
-      half8 v = {0, 0, 0, 0, 0, 0, 0, 0};
-      if (p < NP && iy >= 0 && iy < H && ix >= 0 && ix < H && c8 * 8 < a.cin)
-        v = *reinterpret_cast<const half8*>(xin + ((size_t)iy * H + ix) * a.cin + c8 * 8);
-      *reinterpret_cast<half8*>(sX + p * XLD + c8 * 8) = v;
+      v[j] = half8{0, 0, 0, 0, 0, 0, 0, 0};
+      if (i < MP * C8 && p < NP && iy >= 0 && iy < H && ix >= 0 && ix < H && c8 * 8 < a.cin)
+        v[j] = *reinterpret_cast<const half8*>(xin + ((size_t)iy * H + ix) * a.cin + c8 * 8);
+    }
+#pragma unroll
+    for (int j = 0; j < NIT; ++j) {  // ... then the LDS stores
+      const int i = tid + 256 * j;
+      const int p = i / C8, c8 = i - (i / C8) * C8;
+      if (i < MP * C8) *reinterpret_cast<half8*>(sX + p * XLD + c8 * 8) = v[j];
     }
   } else {
-    // stem conv 3x3/2 pad 1 on the u8 image for stem pixel (iy, ix) of the 112x112 grid,
-    // 8 of its 32 channels per item; fp32 like the reference (u8 * folded weight).
+    // stem conv 3x3/2 pad 1 on the u8 image for stem pixel (iy, ix) of the 112x112 grid:
+    // the u8 patch and the folded weights go to LDS, then 8 channels per item in fp32.
     const uint8_t* img = reinterpret_cast<const uint8_t*>(a.x) + (size_t)n * 224 * 224 * STEM;
+    const int ry0 = 2 * iy0 - 1, rx0 = 2 * ix0 - 1;
+    for (int i = tid; i < PR * PR * STEM; i += 256) {
+      const int c = i % STEM, pix = i / STEM;
+      const int yy = ry0 + pix / PR, xx = rx0 + pix % PR;
+      sPatch[i] = (yy >= 0 && yy < 224 && xx >= 0 && xx < 224) ? img[((size_t)yy * 224 + xx) * STEM + c] : 0;
+    }
+    for (int i = tid; i < STEM * 9 * 8; i += 256)
+      reinterpret_cast<float4*>(sSW)[i] = reinterpret_cast<const float4*>(a.stem_w)[i];
+    __syncthreads();
     for (int i = tid; i < MP * 4; i += 256) {
       const int p = i >> 2, cg = i & 3;
       const int py = p / IR, px = p - (p / IR) * IR;
@@ -101,16 +151,13 @@ __global__ __launch_bounds__(256) void mbv2_block_kernel(const MbArgs a) {
         acc[0] = c0.x; acc[1] = c0.y; acc[2] = c0.z; acc[3] = c0.w;
         acc[4] = c1.x; acc[5] = c1.y; acc[6] = c1.z; acc[7] = c1.w;
 #pragma unroll
-        for (int ky = 0; ky < 3; ++ky) {
-          const int yy = 2 * iy - 1 + ky;
+        for (int ky = 0; ky < 3; ++ky)
 #pragma unroll
-          for (int kx = 0; kx < 3; ++kx) {
-            const int xx = 2 * ix - 1 + kx;
-            const bool ok = yy >= 0 && yy < 224 && xx >= 0 && xx < 224;
+          for (int kx = 0; kx < 3; ++kx)
 #pragma unroll
             for (int c = 0; c < STEM; ++c) {
-              const float u = ok ? (float)img[((size_t)yy * 224 + xx) * STEM + c] : 0.f;
-              const float* w = a.stem_w + ((c * 3 + ky) * 3 + kx) * 32 + cg * 8;
+              const float u = (float)sPatch[((2 * py + ky) * PR + 2 * px + kx) * STEM + c];
+              const float* w = sSW + ((c * 3 + ky) * 3 + kx) * 32 + cg * 8;
               const float4 w0 = *reinterpret_cast<const float4*>(w);
               const float4 w1 = *reinterpret_cast<const float4*>(w + 4);
               acc[0] = __builtin_fmaf(u, w0.x, acc[0]); acc[1] = __builtin_fmaf(u, w0.y, acc[1]);
@@ -118,8 +165,6 @@ __global__ __launch_bounds__(256) void mbv2_block_kernel(const MbArgs a) {
               acc[4] = __builtin_fmaf(u, w1.x, acc[4]); acc[5] = __builtin_fmaf(u, w1.y, acc[5]);
               acc[6] = __builtin_fmaf(u, w1.z, acc[6]); acc[7] = __builtin_fmaf(u, w1.w, acc[7]);
             }
-          }
-        }
 #pragma unroll
         for (int j = 0; j < 8; ++j) v[j] = (f16)relu6f(acc[j]);
       }
@@ -128,7 +173,6 @@ __global__ __launch_bounds__(256) void mbv2_block_kernel(const MbArgs a) {
   }
   __syncthreads();
 
-  const int l16 = lane & 15, lq = lane >> 4;
   floatx4 acc[OT];
 #pragma unroll
   for (int o = 0; o < OT; ++o) acc[o] = floatx4{0.f, 0.f, 0.f, 0.f};
@@ -138,23 +182,23 @@ __global__ __launch_bounds__(256) void mbv2_block_kernel(const MbArgs a) {
   const int dqy = dq / TO, dqx = dq - (dq / TO) * TO;
   const int dp0 = (dqy * S) * IR + dqx * S;  // top-left tap of the 3x3 window
 
-  for (int h0 = 0; h0 < a.hidp; h0 += MB_HC) {
+#pragma unroll 1
+  for (int h0 = 0; h0 < HIDP; h0 += MB_HC) {
+    // project weights of this chunk: in flight during expand + depthwise
+    half8 pf[OT];
+#pragma unroll
+    for (int o = 0; o < OT; ++o)
+      pf[o] = *reinterpret_cast<const half8*>(a.Wp + (size_t)(16 * o + l16) * HIDP + h0 + 8 * lq);
     const f16* src;  // dw input for this chunk: row p at src + p * sld
     int sld;
     if constexpr (EXPAND) {
       // E^T[h][p] = sum_c We[h0+h][c] X[p][c]: A = weights (rows h), B = X^T (cols p), so
       // each lane ends with 4 consecutive hidden channels of one pixel (one 8-B LDS write).
-      half8 af[2][CINP / 32];
-#pragma unroll
-      for (int ht = 0; ht < 2; ++ht)
-#pragma unroll
-        for (int k = 0; k < CINP / 32; ++k)
-          af[ht][k] = *reinterpret_cast<const half8*>(a.We + (size_t)(h0 + 16 * ht + l16) * CINP + 32 * k + 8 * lq);
       float eb[2][4];
 #pragma unroll
       for (int ht = 0; ht < 2; ++ht)
 #pragma unroll
-        for (int e = 0; e < 4; ++e) eb[ht][e] = a.be[h0 + 16 * ht + 4 * lq + e];
+        for (int e = 0; e < 4; ++e) eb[ht][e] = sBe[h0 + 16 * ht + 4 * lq + e];
       for (int pt = wave; pt < MP / 16; pt += 4) {
         const int p = pt * 16 + l16;
         const int py = p / IR, px = p - (p / IR) * IR;
@@ -162,7 +206,7 @@ __global__ __launch_bounds__(256) void mbv2_block_kernel(const MbArgs a) {
         const bool valid = p < NP && iy >= 0 && iy < H && ix >= 0 && ix < H;
         floatx4 e2[2] = {floatx4{0.f, 0.f, 0.f, 0.f}, floatx4{0.f, 0.f, 0.f, 0.f}};
 #pragma unroll
-        for (int k = 0; k < CINP / 32; ++k) {
+        for (int k = 0; k < KX; ++k) {
           const half8 bf = *reinterpret_cast<const half8*>(sX + p * XLD + 32 * k + 8 * lq);
 #pragma unroll
           for (int ht = 0; ht < 2; ++ht) e2[ht] = __builtin_amdgcn_mfma_f32_16x16x32_f16(af[ht][k], bf, e2[ht], 0, 0, 0);
@@ -174,6 +218,14 @@ __global__ __launch_bounds__(256) void mbv2_block_kernel(const MbArgs a) {
           for (int e = 0; e < 4; ++e) hv[e] = valid ? (f16)relu6f(e2[ht][e] + eb[ht][e]) : (f16)0.f;  // dw zero pad
           *reinterpret_cast<half4*>(sE + p * ELD + 16 * ht + 4 * lq) = hv;
         }
+      }
+      if (h0 + MB_HC < HIDP) {  // next chunk's expand weights: in flight during dw + project
+#pragma unroll
+        for (int ht = 0; ht < 2; ++ht)
+#pragma unroll
+          for (int k = 0; k < KX; ++k)
+            af[ht][k] = *reinterpret_cast<const half8*>(a.We + (size_t)(h0 + MB_HC + 16 * ht + l16) * CINP + 32 * k +
+                                                        8 * lq);
       }
       __syncthreads();
       src = sE;
@@ -190,11 +242,11 @@ __global__ __launch_bounds__(256) void mbv2_block_kernel(const MbArgs a) {
         const int hc = h0 + 8 * dcg;
         float d[8];
         {
-          const float4 b0 = *reinterpret_cast<const float4*>(a.bd + hc);
-          const float4 b1 = *reinterpret_cast<const float4*>(a.bd + hc + 4);
+          const float4 b0 = *reinterpret_cast<const float4*>(sBd + hc);
+          const float4 b1 = *reinterpret_cast<const float4*>(sBd + hc + 4);
           d[0] = b0.x; d[1] = b0.y; d[2] = b0.z; d[3] = b0.w; d[4] = b1.x; d[5] = b1.y; d[6] = b1.z; d[7] = b1.w;
         }
-        const float* wd = a.Wd + (size_t)(hc / 8) * 72;
+        const float* wd = sWd + (hc / 8) * 72;
 #pragma unroll
         for (int ky = 0; ky < 3; ++ky)
 #pragma unroll
@@ -218,10 +270,7 @@ __global__ __launch_bounds__(256) void mbv2_block_kernel(const MbArgs a) {
     {
       const half8 bf = *reinterpret_cast<const half8*>(sD + (16 * wave + l16) * ELD + 8 * lq);
 #pragma unroll
-      for (int o = 0; o < OT; ++o) {
-        const half8 af = *reinterpret_cast<const half8*>(a.Wp + (size_t)(16 * o + l16) * a.hidp + h0 + 8 * lq);
-        acc[o] = __builtin_amdgcn_mfma_f32_16x16x32_f16(af, bf, acc[o], 0, 0, 0);
-      }
+      for (int o = 0; o < OT; ++o) acc[o] = __builtin_amdgcn_mfma_f32_16x16x32_f16(pf[o], bf, acc[o], 0, 0, 0);
     }
     if constexpr (!EXPAND) __syncthreads();  // next chunk's dw rewrites sD
   }
@@ -234,15 +283,18 @@ __global__ __launch_bounds__(256) void mbv2_block_kernel(const MbArgs a) {
 #pragma unroll
     for (int o = 0; o < OT; ++o) {
       const int c = 16 * o + 4 * lq;
+      const float4 bv = *reinterpret_cast<const float4*>(sBp + c);
+      float v[4] = {acc[o][0] + bv.x, acc[o][1] + bv.y, acc[o][2] + bv.z, acc[o][3] + bv.w};
+      if constexpr (RES) {
+        if (q < NQ) {
+          const half4 r = *reinterpret_cast<const half4*>(sX + pc * XLD + c);
+#pragma unroll
+          for (int e = 0; e < 4; ++e) v[e] += (float)r[e];
+        }
+      }
       half4 hv;
 #pragma unroll
-      for (int e = 0; e < 4; ++e) {
-        float v = acc[o][e] + a.bp[c + e];
-        if constexpr (RES) {
-          if (q < NQ) v += (float)sX[pc * XLD + c + e];
-        }
-        hv[e] = (f16)v;
-      }
+      for (int e = 0; e < 4; ++e) hv[e] = (f16)v[e];
       *reinterpret_cast<half4*>(sO + q * OLD + c) = hv;
     }
   }
@@ -419,40 +471,41 @@ int MobileNetModel::create(const float* blob, size_t n) {
   return 0;
 }
 
-template <int S, int TO, int CINP, int COUTP, bool EXPAND, bool RES, int STEM>
+template <int S, int TO, int CINP, int HIDP, int COUTP, bool EXPAND, bool RES, int STEM>
 static int launch_block(const MbArgs& a, int B, hipStream_t s) {
   const int tpr = a.OH / TO;
-  hipLaunchKernelGGL((mbv2_block_kernel<S, TO, CINP, COUTP, EXPAND, RES, STEM>), dim3(B * tpr * tpr), dim3(256), 0, s,
-                     a);
+  hipLaunchKernelGGL((mbv2_block_kernel<S, TO, CINP, HIDP, COUTP, EXPAND, RES, STEM>), dim3(B * tpr * tpr), dim3(256),
+                     0, s, a);
   MEC_LAUNCH_CHECK();
   return 0;
 }
 
-// The 17 block shapes of mobilenet_v2 (width 1.0) at 224x224: (stride, tile, cinp, coutp,
-// expand, residual). Output sides 112 / 56 use 8x8 tiles, 28 / 14 / 7 use 7x7 tiles.
+// The 17 block shapes of mobilenet_v2 (width 1.0) at 224x224: (stride, tile, cinp, hidp,
+// coutp, expand, residual). Output sides 112 / 56 use 8x8 tiles, 28 / 14 / 7 use 7x7 tiles.
 static int dispatch_block(const MbBlock& b, const MbArgs& a, int B, int stem_c, hipStream_t s) {
   const bool res = b.stride == 1 && b.cin == b.cout;
   const int TO = (a.OH % 8 == 0) ? 8 : 7;
-#define MB_CASE(S_, TO_, CI_, CO_, EX_, RS_)                                                             \
-  if (b.stride == S_ && TO == TO_ && b.cinp == CI_ && b.coutp == CO_ && (b.t != 1) == EX_ && res == RS_) \
-    return launch_block<S_, TO_, CI_, CO_, EX_, RS_, 0>(a, B, s);
+#define MB_CASE(S_, TO_, CI_, HI_, CO_, EX_, RS_)                                                     \
+  if (b.stride == S_ && TO == TO_ && b.cinp == CI_ && b.hidp == HI_ && b.coutp == CO_ && (b.t != 1) == EX_ && \
+      res == RS_)                                                                                             \
+    return launch_block<S_, TO_, CI_, HI_, CO_, EX_, RS_, 0>(a, B, s);
   if (b.t == 1) {
-    MEC_REQUIRE(b.stride == 1 && b.cinp == 32 && b.coutp == 16 && !res && TO == 8, "mbv2: block 1 shape");
-    if (stem_c == 3) return launch_block<1, 8, 32, 16, false, false, 3>(a, B, s);
-    if (stem_c == 1) return launch_block<1, 8, 32, 16, false, false, 1>(a, B, s);
-    return launch_block<1, 8, 32, 16, false, false, 0>(a, B, s);
+    MEC_REQUIRE(b.stride == 1 && b.cinp == 32 && b.hidp == 32 && b.coutp == 16 && !res && TO == 8, "mbv2: block 1 shape");
+    if (stem_c == 3) return launch_block<1, 8, 32, 32, 16, false, false, 3>(a, B, s);
+    if (stem_c == 1) return launch_block<1, 8, 32, 32, 16, false, false, 1>(a, B, s);
+    return launch_block<1, 8, 32, 32, 16, false, false, 0>(a, B, s);
   }
-  MB_CASE(2, 8, 32, 32, true, false)     // 16 -> 24, 112 -> 56
-  MB_CASE(1, 8, 32, 32, true, true)      // 24 -> 24 @ 56
-  MB_CASE(2, 7, 32, 32, true, false)     // 24 -> 32, 56 -> 28
-  MB_CASE(1, 7, 32, 32, true, true)      // 32 -> 32 @ 28
-  MB_CASE(2, 7, 32, 64, true, false)     // 32 -> 64, 28 -> 14
-  MB_CASE(1, 7, 64, 64, true, true)      // 64 -> 64 @ 14
-  MB_CASE(1, 7, 64, 96, true, false)     // 64 -> 96 @ 14
-  MB_CASE(1, 7, 96, 96, true, true)      // 96 -> 96 @ 14
-  MB_CASE(2, 7, 96, 160, true, false)    // 96 -> 160, 14 -> 7
-  MB_CASE(1, 7, 160, 160, true, true)    // 160 -> 160 @ 7
-  MB_CASE(1, 7, 160, 320, true, false)   // 160 -> 320 @ 7
+  MB_CASE(2, 8, 32, 96, 32, true, false)     // 16 -> 24, 112 -> 56
+  MB_CASE(1, 8, 32, 160, 32, true, true)      // 24 -> 24 @ 56
+  MB_CASE(2, 7, 32, 160, 32, true, false)     // 24 -> 32, 56 -> 28
+  MB_CASE(1, 7, 32, 192, 32, true, true)      // 32 -> 32 @ 28
+  MB_CASE(2, 7, 32, 192, 64, true, false)     // 32 -> 64, 28 -> 14
+  MB_CASE(1, 7, 64, 384, 64, true, true)      // 64 -> 64 @ 14
+  MB_CASE(1, 7, 64, 384, 96, true, false)     // 64 -> 96 @ 14
+  MB_CASE(1, 7, 96, 576, 96, true, true)      // 96 -> 96 @ 14
+  MB_CASE(2, 7, 96, 576, 160, true, false)    // 96 -> 160, 14 -> 7
+  MB_CASE(1, 7, 160, 960, 160, true, true)    // 160 -> 160 @ 7
+  MB_CASE(1, 7, 160, 960, 320, true, false)   // 160 -> 320 @ 7
 #undef MB_CASE
   set_error("mbv2: no kernel instance for this block shape");
   return -1;

@@ -52,36 +52,60 @@ static bool make_taps(int in_size, int out_size, int* mins, int* ns, int (*kk)[R
   return true;
 }
 
-template <int IH, int IW, int OH, int OW>
+// Packed taps: per output coordinate (first source index, k0, k1, k2); taps past the
+// filter support are 0, so every output sums exactly three terms (same value as Pillow).
+struct ResizeTaps4 {
+  int4 x[224], y[224];
+};
+
+// grid (B, 224 / RS_BAND): one band of RS_BAND output rows per workgroup. The band's few
+// source rows are resampled horizontally into LDS (u8, like Pillow's intermediate), then
+// each thread produces 4 adjacent output pixels of the vertical pass (one u32 store).
+constexpr int RS_BAND = 28;
 __global__ __launch_bounds__(256) void resize_u8_kernel(const uint8_t* __restrict__ in, uint8_t* __restrict__ out,
-                                                        const ResizeTaps* __restrict__ taps) {
-  __shared__ uint8_t src[IH * IW];
-  __shared__ uint8_t tmp[IH * OW];
-  const int b = blockIdx.x, tid = threadIdx.x;
+                                                        const ResizeTaps4* __restrict__ taps) {
+  constexpr int IH = 48, IW = 48, OW = 224, MAXR = 12;
+  __shared__ __attribute__((aligned(16))) uint8_t src[IH * IW];
+  __shared__ __attribute__((aligned(16))) uint8_t tmp[MAXR * OW];
+  const int b = blockIdx.x, r0 = blockIdx.y * RS_BAND, tid = threadIdx.x;
   const uint8_t* im = in + (size_t)b * IH * IW;
-  for (int i = tid; i < IH * IW; i += 256) src[i] = im[i];
+  if (tid < IH * IW / 16) reinterpret_cast<uint4*>(src)[tid] = reinterpret_cast<const uint4*>(im)[tid];
+  const int ys = taps->y[r0].x;                                  // first source row of the band
+  const int ye = min(taps->y[r0 + RS_BAND - 1].x + 3, IH);        // one past the last
   __syncthreads();
-  for (int i = tid; i < IH * OW; i += 256) {  // horizontal
-    const int y = i / OW, xx = i - y * OW;
-    int acc = 1 << (RS_PREC - 1);
-    const int x0 = taps->xmin[xx];
-    for (int x = 0; x < taps->xn[xx]; ++x) acc += (int)src[y * IW + x0 + x] * taps->xk[xx][x];
+  for (int i = tid; i < (ye - ys) * OW; i += 256) {  // horizontal
+    const int yr = i / OW, xx = i - yr * OW;
+    const int4 t = taps->x[xx];
+    const uint8_t* row = src + (ys + yr) * IW;
+    int acc = (1 << (RS_PREC - 1)) + (int)row[t.x] * t.y + (int)row[min(t.x + 1, IW - 1)] * t.z +
+              (int)row[min(t.x + 2, IW - 1)] * t.w;
     acc >>= RS_PREC;
     tmp[i] = (uint8_t)(acc < 0 ? 0 : (acc > 255 ? 255 : acc));
   }
   __syncthreads();
-  uint8_t* o = out + (size_t)b * OH * OW;
-  for (int i = tid; i < OH * OW; i += 256) {  // vertical
-    const int yy = i / OW, x = i - yy * OW;
-    int acc = 1 << (RS_PREC - 1);
-    const int y0 = taps->ymin[yy];
-    for (int y = 0; y < taps->yn[yy]; ++y) acc += (int)tmp[(y0 + y) * OW + x] * taps->yk[yy][y];
-    acc >>= RS_PREC;
-    o[i] = (uint8_t)(acc < 0 ? 0 : (acc > 255 ? 255 : acc));
+  uint8_t* o = out + (size_t)b * OW * OW;
+  for (int i = tid; i < RS_BAND * OW / 4; i += 256) {  // vertical, 4 pixels per thread
+    const int yl = i / (OW / 4), x4 = (i - yl * (OW / 4)) * 4;
+    const int yy = r0 + yl;
+    const int4 t = taps->y[yy];
+    const int y0 = t.x - ys;
+    const int y1 = min(t.x + 1, IH - 1) - ys, y2 = min(t.x + 2, IH - 1) - ys;
+    uint32_t packed = 0;
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+      const int x = x4 + j;
+      int acc = (1 << (RS_PREC - 1)) + (int)tmp[y0 * OW + x] * t.y + (int)tmp[min(y1, MAXR - 1) * OW + x] * t.z +
+                (int)tmp[min(y2, MAXR - 1) * OW + x] * t.w;
+      // all taps and pixels are >= 0 (upscale), so only the 255 clamp can apply. Writing
+      // the [0,255] clamp here lets the compiler (ROCm 7.2) pair two bytes into
+      // v_ashr_pk_u8_i32, whose upper 16 result bits leak into the packed word.
+      packed |= (uint32_t)min(acc >> RS_PREC, 255) << (8 * j);
+    }
+    *reinterpret_cast<uint32_t*>(o + (size_t)yy * OW + x4) = packed;
   }
 }
 
-static ResizeTaps* g_taps = nullptr;  // device copy, built once per process
+static ResizeTaps4* g_taps = nullptr;  // device copy, built once per process
 
 static int ensure_taps() {
   if (g_taps) return 0;
@@ -90,8 +114,19 @@ static int ensure_taps() {
     set_error("resize taps");
     return -1;
   }
-  MEC_HIP(hipMalloc(&g_taps, sizeof(ResizeTaps)));
-  MEC_HIP(hipMemcpy(g_taps, &h, sizeof(ResizeTaps), hipMemcpyHostToDevice));
+  ResizeTaps4 p;
+  for (int i = 0; i < 224; ++i) {
+    int kx[3] = {0, 0, 0}, ky[3] = {0, 0, 0};
+    for (int j = 0; j < h.xn[i]; ++j) kx[j] = h.xk[i][j];
+    for (int j = 0; j < h.yn[i]; ++j) ky[j] = h.yk[i][j];
+    p.x[i] = make_int4(h.xmin[i], kx[0], kx[1], kx[2]);
+    p.y[i] = make_int4(h.ymin[i], ky[0], ky[1], ky[2]);
+  }
+  // the band's source rows fit the kernel's LDS buffer
+  for (int r0 = 0; r0 < 224; r0 += RS_BAND)
+    if (std::min(p.y[r0 + RS_BAND - 1].x + 3, 48) - p.y[r0].x > 12) { set_error("resize: band too tall"); return -1; }
+  MEC_HIP(hipMalloc(&g_taps, sizeof(ResizeTaps4)));
+  MEC_HIP(hipMemcpy(g_taps, &p, sizeof(ResizeTaps4), hipMemcpyHostToDevice));
   return 0;
 }
 
@@ -99,7 +134,7 @@ int resize_u8(const uint8_t* in, int B, int H, int W, uint8_t* out, int OH, int 
   MEC_REQUIRE(H == 48 && W == 48 && OH == 224 && OW == 224, "resize: only 48x48 -> 224x224 (FER2013 -> IMAGE_SIZE)");
   if (B == 0) return 0;
   MEC_TRY(ensure_taps());
-  hipLaunchKernelGGL((resize_u8_kernel<48, 48, 224, 224>), dim3(B), dim3(256), 0, s, in, out, g_taps);
+  hipLaunchKernelGGL(resize_u8_kernel, dim3(B, 224 / RS_BAND), dim3(256), 0, s, in, out, g_taps);
   MEC_LAUNCH_CHECK();
   return 0;
 }
