@@ -48,6 +48,7 @@ def parse():
     ap.add_argument('--no-cpu-baseline', action='store_true')
     ap.add_argument('--cpu-seconds', type=float, default=12.0)
     ap.add_argument('--serial', action='store_true', help='run the encoders on one stream (A/B of the concurrency)')
+    ap.add_argument('--no-configs', action='store_true', help='skip the per-config (single-encoder) timings')
     return ap.parse_args()
 
 
@@ -80,6 +81,37 @@ def cpu_baseline(seconds: float):
     return {'value': n / el, 'unit': 'fused samples/s', 'cores': torch.get_num_threads(), 'kind': 'port',
             'sample': f'{n} fused samples (batches of {Bc}, L=128, 48x48 u8) through oracle/ fp32 torch-CPU, '
                       f'{el:.1f}s'}
+
+
+def per_config(pipe, dev, iters=10):
+    """Single-encoder throughput on the other BASELINE configs (rank 0, N=1; informational,
+    not `value`): speech B=32, image B=256 (ResNet50 and the MobileNetV2 backbone), text B=128
+    (L=128). hipEvents around `iters` back-to-back calls on the current stream, inputs in HBM."""
+    from mec import engine, synthetic as syn
+    mb = engine.MobileNetImageEncoder(device=dev)
+    xs = engine.to_device(syn.speech_inputs(32, seed=7), dev)
+    ids, mask = syn.text_inputs(128, 128, seed=7)
+    ids, mask = engine.to_device(ids, dev), engine.to_device(mask, dev)
+    g = engine.to_device(syn.image_inputs(256, seed=7), dev)
+    runs = {'speech_b32': (32, lambda: pipe.speech.forward(xs)),
+            'image_resnet50_b256': (256, lambda: pipe.image.forward(g)),
+            'image_mobilenet_v2_b256': (256, lambda: mb.forward(g)),
+            'text_bert_b128': (128, lambda: pipe.text.forward(ids, mask))}
+    out = {}
+    for name, (b, fn) in runs.items():
+        for _ in range(3):
+            fn()
+        e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+        torch.cuda.synchronize()
+        e0.record()
+        for _ in range(iters):
+            fn()
+        e1.record()
+        torch.cuda.synchronize()
+        ms = e0.elapsed_time(e1) / iters
+        out[name] = {'samples_per_s': b / ms * 1e3, 'ms_per_batch': ms}
+    mb.close()
+    return out
 
 
 def main():
@@ -177,6 +209,8 @@ def main():
             'achieved_tflops_whole_step': flop / el / 1e12,
             'roofline': roof,
         }
+        if world == 1 and not a.no_configs:
+            res['per_config'] = per_config(pipe, dev)
         if world == 1 and not a.no_cpu_baseline:
             res['cpu_baseline'] = cpu_baseline(a.cpu_seconds)
         print(json.dumps(res))
