@@ -131,6 +131,7 @@ extern int g_gemm_impl;
 extern int g_gemm_bn;
 extern int g_gemm_autotune;
 extern int g_gemm_debug;
+extern int g_gemm_prefetch_r;
 int gemm_tuned_bn(int amode, int M, int N, int K);
 
 }  // namespace mec

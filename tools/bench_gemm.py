@@ -51,6 +51,7 @@ def main():
     ap.add_argument('--rounds', type=int, default=5)
     ap.add_argument('--only', nargs='*')
     ap.add_argument('--debug', type=int, nargs='+', default=[0])
+    ap.add_argument('--prefetch', type=int, nargs='+', default=[1], help='gemm_prefetch_r values to A/B')
     ap.add_argument('--torch', action='store_true', help='also time torch.mm (hipBLASLt) on plain shapes')
     a = ap.parse_args()
     lib = _lib.load()
@@ -101,9 +102,11 @@ def main():
             ms = e0.elapsed_time(e1) / a.iters
             r = {'shape': name, 'impl': 'torch.mm', 'us': round(ms * 1e3, 1), 'tflops': round(flop / ms / 1e9, 1)}
             print(json.dumps(r), flush=True)
-        variants = [(i, b, d) for i in a.impl for b in (a.bn if i == 2 else [0]) for d in a.debug]
+        variants = [(i, b, d, f) for i in a.impl for b in (a.bn if i == 2 else [0]) for d in a.debug
+                    for f in a.prefetch]
 
-        def setv(impl, bn, dbg):
+        def setv(impl, bn, dbg, pf=1):
+            lib.mec_set_option(b'gemm_prefetch_r', pf)
             lib.mec_set_option(b'gemm_debug', dbg)
             lib.mec_set_option(b'gemm_impl', impl)
             lib.mec_set_option(b'gemm_bn', bn)
@@ -115,7 +118,7 @@ def main():
                 run()
             except _lib.MecError as e:
                 print(json.dumps({'shape': name, 'impl': v[0], 'bn': v[1], 'error': str(e)}), flush=True)
-                setv(2, 0, 0)
+                setv(2, 0, 0, 1)
                 continue
             ok.append(v)
         torch.cuda.synchronize()
@@ -133,9 +136,9 @@ def main():
                 torch.cuda.synchronize()
                 times[v].append(e0.elapsed_time(e1) / a.iters)
         for v in ok:
-            impl, bn, dbg = v
+            impl, bn, dbg, pf = v
             ms = sorted(times[v])[len(times[v]) // 2]
-            r = {'shape': name, 'impl': impl, 'bn': bn, 'dbg': dbg, 'us': round(ms * 1e3, 1),
+            r = {'shape': name, 'impl': impl, 'bn': bn, 'dbg': dbg, 'prefetch_r': pf, 'us': round(ms * 1e3, 1),
                  'tflops': round(flop / ms / 1e9, 1)}
             if ref is not None and dbg == 0:
                 setv(*v)
