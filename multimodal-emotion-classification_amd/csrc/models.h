@@ -111,5 +111,9 @@ struct MobileNetModel : ImageNet {
 };
 
 int resize_u8(const uint8_t* in, int B, int H, int W, uint8_t* out, int OH, int OW, hipStream_t s);
+// ResNet bottleneck conv2 + conv3 + residual + ReLU (stride-1 blocks, w = 64 @ 56 or 128 @ 28)
+int launch_bneck_tail(const f16* t1, const f16* x, const f16* w2, const float* b2, const f16* w3, const float* b3,
+                      f16* y, int B, int H, int w, hipStream_t s);
+extern int g_resnet_fused_tail;
 
 }  // namespace mec

@@ -10,6 +10,12 @@
 
 namespace mec {
 
+// mec_set_option("resnet_fused_tail", 0|1): layer1's stride-1 blocks through bottleneck.hip.
+// Off by default: bit-identical to the unfused path but 90-95 us slower per block at B=256
+// (tools/ab_option.py: 4.33 vs 4.14 ms per ResNet pass) — at one 114-KB workgroup per CU the
+// load, MFMA and store phases of every CU run in lockstep with nothing to overlap them.
+int g_resnet_fused_tail = 0;
+
 // ----------------------------------------------------------------------------- resize
 // Pillow ImagingResample (bilinear, 8bpc): 22-bit fixed-point taps, horizontal pass into
 // a u8 intermediate, then the vertical pass; clip8((acc + 2^21) >> 22).
@@ -544,6 +550,15 @@ int ImageModel::forward_u8(const uint8_t* img, int B, int H, int W, int C, float
     g.A = cur; g.B = Wt + bk.c1.w_off; g.bias = P + bk.c1.b_off; g.act = ACT_RELU; g.C16 = T1;
     g.M = B * H * H; g.N = wd; g.K = cin;
     MEC_TRY(launch_gemm(g, s, &prof, TAG_RESNET_CONV1X1));
+    if (!bk.has_ds && g_resnet_fused_tail && wd == 64 && H == 56) {
+      // conv2 + conv3 + residual + ReLU in one kernel (bottleneck.hip)
+      MEC_TRY(prof.begin(TAG_RESNET_CONV3X3, s));
+      MEC_TRY(launch_bneck_tail(T1, cur, Wt + bk.c2.w_off, P + bk.c2.b_off, Wt + bk.c3.w_off, P + bk.c3.b_off, other,
+                                B, H, wd, s));
+      MEC_TRY(prof.end(TAG_RESNET_CONV3X3, s));
+      std::swap(cur, other);
+      continue;
+    }
     g = GemmParams();
     g.amode = A_CONV; g.A = T1; g.B = Wt + bk.c2.w_off; g.bias = P + bk.c2.b_off; g.act = ACT_RELU; g.C16 = T2;
     g.M = B * OH * OH; g.N = wd; g.K = 9 * wd;

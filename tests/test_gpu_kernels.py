@@ -173,3 +173,18 @@ def test_resize_bit_exact_many(dev):
     _lib.check(lib.mec_resize_u8(_p(gd), 64, 48, 48, _p(out), 224, 224, _s()), 'resize')
     torch.cuda.synchronize()
     assert np.array_equal(out.cpu().numpy(), resize_bilinear_u8(gray))
+
+
+def test_fused_bottleneck_tail_bit_identical(dev):
+    """bottleneck.hip (conv2 + conv3 + residual in one kernel, opt-in) == the GEMM path."""
+    from mec import _lib, engine, synthetic as syn
+    lib = _lib.load()
+    m = engine.ImageEncoder(device=dev)
+    g = engine.to_device(syn.image_inputs(5, seed=41), dev)
+    outs = []
+    for v in (0, 1):
+        _lib.check(lib.mec_set_option(b'resnet_fused_tail', v), 'set_option')
+        outs.append([t.cpu() for t in m.forward(g)])
+    lib.mec_set_option(b'resnet_fused_tail', 0)
+    for a, b in zip(*outs):
+        assert torch.equal(a, b)
