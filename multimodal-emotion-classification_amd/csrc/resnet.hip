@@ -11,9 +11,10 @@
 namespace mec {
 
 // mec_set_option("resnet_fused_tail", 0|1): layer1's stride-1 blocks through bottleneck.hip.
-// Off by default: bit-identical to the unfused path but 90-95 us slower per block at B=256
-// (tools/ab_option.py: 4.33 vs 4.14 ms per ResNet pass) — at one 114-KB workgroup per CU the
-// load, MFMA and store phases of every CU run in lockstep with nothing to overlap them.
+// Off by default: bit-identical to the unfused path but slower at B=256 — 315 us per block
+// against 105 + 170 us for the conv2 and conv3 GEMMs (rocprofv3, tools/encoder_profile.py
+// --opt resnet_fused_tail=1). It moves fewer bytes (about 3 TB/s at 315 us) but runs one
+// 4-wave workgroup per CU, so LDS-read and barrier latency inside a tile is exposed.
 int g_resnet_fused_tail = 0;
 
 // ----------------------------------------------------------------------------- resize

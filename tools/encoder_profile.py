@@ -25,9 +25,15 @@ def main():
     ap.add_argument('--enc', choices=['text', 'image', 'image_mbv2', 'speech', 'fusion', 'pipeline'], required=True)
     ap.add_argument('--iters', type=int, default=5)
     ap.add_argument('--batch', type=int, default=256)
+    ap.add_argument('--opt', action='append', default=[], help='library option NAME=VALUE (mec_set_option)')
     a = ap.parse_args()
     dev = torch.device('cuda', 0)
     B = a.batch
+    if a.opt:
+        from mec import _lib
+        for kv in a.opt:
+            k, v = kv.split('=')
+            _lib.check(_lib.load().mec_set_option(k.encode(), int(v)), f'mec_set_option({kv})')
     if a.enc == 'text':
         m = engine.TextEncoder(device=dev)
         ids, mask = syn.text_inputs(B, 128, seed=0)
