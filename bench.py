@@ -3,7 +3,9 @@
 One step = one pass of the whole hot path over one synthetic batch already resident in
 HBM: speech DNN + BERT-base (L=128) + ResNet50 (48x48 u8 -> 224) encoders, then the
 attention-MLP fusion, then (N>1) the RCCL all-gather of the 34-float result rows.
-Weak scaling: every rank processes its own batch of 256.
+Weak scaling: every rank processes its own batch of 256. Consecutive batches are
+pipelined (engine.FusedPipeline): batch i's fusion and gather overlap batch i+1's
+encoders; the timed region ends after the last batch's gather (device synchronize).
 
     python bench.py [--gpus N] [--steps K] [--warmup W] [--batch B] [--no-cpu-baseline]
     python -m torch.distributed.run --nproc-per-node N ... bench.py --gpus N
@@ -48,6 +50,8 @@ def parse():
     ap.add_argument('--no-cpu-baseline', action='store_true')
     ap.add_argument('--cpu-seconds', type=float, default=12.0)
     ap.add_argument('--serial', action='store_true', help='run the encoders on one stream (A/B of the concurrency)')
+    ap.add_argument('--no-pipeline', action='store_true',
+                    help="run each batch's fusion on the main stream (A/B of the cross-batch overlap)")
     ap.add_argument('--no-configs', action='store_true', help='skip the per-config (single-encoder) timings')
     return ap.parse_args()
 
@@ -127,19 +131,21 @@ def main():
 
     from mec import engine, synthetic as syn
     B = a.batch
-    pipe = engine.FusedPipeline(seed=1234, device=dev, concurrent=not a.serial)
+    pipe = engine.FusedPipeline(seed=1234, device=dev, concurrent=not a.serial, pipelined=not a.no_pipeline)
     x = engine.to_device(syn.speech_inputs(B, seed=rank), dev)
     ids_np, mask_np = syn.text_inputs(B, 128, seed=rank, ragged=False)
     ids, mask = engine.to_device(ids_np, dev), engine.to_device(mask_np, dev)
     gray = engine.to_device(syn.image_inputs(B, seed=rank), dev)
     from mec import dist as mdist
 
-    def step():
-        out = pipe.forward(x, ids, mask, gray)
+    def finish(out):  # runs on the fusion's stream (FusedPipeline: batch i's fusion overlaps batch i+1)
         rows = pipe.pack_rows(out)
         if world > 1:  # one RCCL all-gather of the 34-float result rows
             rows = mdist.all_gather_rows(rows, world * B)
         return rows
+
+    def step():
+        return pipe.forward(x, ids, mask, gray, epilogue=finish)[1]
 
     for _ in range(a.warmup):
         step()

@@ -220,14 +220,21 @@ ROW = 34
 class FusedPipeline:
     """The whole tri-modal path: speech + text + image encoders, then the fusion model.
 
-    BERT runs on the caller's stream; speech and ResNet50 run concurrently on a second HIP
-    stream (their kernels fill the CUs that BERT's GEMM tails and its LayerNorm/attention
-    kernels leave idle); the fusion waits for both. The first call runs everything
-    serially so each GEMM shape is autotuned in isolation.
+    BERT runs on the caller's stream; speech and the image backbone run concurrently on a
+    second HIP stream (their kernels fill the CUs that BERT's GEMM tails and its
+    LayerNorm/attention kernels leave idle). The first call runs everything serially so each
+    GEMM shape is autotuned in isolation.
+
+    pipelined=True (the default with concurrent=True): the fusion model (and the caller's
+    `epilogue`, e.g. packing and the all-gather) runs on a third stream that waits for both
+    encoder streams, and the caller's stream does NOT wait for it. Consecutive batches
+    therefore overlap: batch i's fusion (a latency-bound kernel of ~128 workgroups) runs
+    under batch i+1's BERT instead of idling the GPU between them. Every batch's work is still
+    done; outputs are ready once `wait()` (or a device synchronize) returns.
     """
 
     def __init__(self, seed: int = 1234, device=None, weights=None, concurrent: bool = True,
-                 image_backbone: str = 'resnet50'):
+                 image_backbone: str = 'resnet50', pipelined: bool = True):
         weights = weights or {}
         self.speech = SpeechEncoder(weights.get('speech'), seed, device)
         self.text = TextEncoder(weights.get('text'), seed, device)
@@ -235,31 +242,52 @@ class FusedPipeline:
         self.fusion = FusionHead(weights.get('fusion'), seed, device)
         self.device = self.speech.device
         self.concurrent = concurrent
+        self.pipelined = concurrent and pipelined
         self._side = torch.cuda.Stream(device=self.device) if concurrent else None
+        self._tail = torch.cuda.Stream(device=self.device) if self.pipelined else None
         self._tuned = False
 
-    def forward(self, x_speech, ids, mask, gray):
+    def forward(self, x_speech, ids, mask, gray, epilogue=None):
+        """One batch through the path -> dict of per-modality and fusion outputs (and, with
+        `epilogue`, ``(outputs, epilogue(outputs))``, the callable run on the fusion's stream)."""
+        main = torch.cuda.current_stream(self.device)
         if not self.concurrent or not self._tuned:
             sf, sl, sp = self.speech.forward(x_speech)
             tf, tl, tp = self.text.forward(ids, mask)
             imf, il, ip = self.image.forward(gray)
             self._tuned = True
+            fstream = main
         else:
-            main = torch.cuda.current_stream(self.device)
             side = self._side
             side.wait_stream(main)  # inputs were produced on the main stream
             with torch.cuda.stream(side):
                 sf, sl, sp = self.speech.forward(x_speech)
                 imf, il, ip = self.image.forward(gray)
             tf, tl, tp = self.text.forward(ids, mask)
-            main.wait_stream(side)
-            for t in (sf, sl, sp, imf, il, ip):
-                t.record_stream(main)
             for t in (x_speech, gray):
                 t.record_stream(side)
-        fl, fp, aw, dw = self.fusion.forward(sf, tf, imf, sp, tp, ip)
-        return {'speech': (sf, sl, sp), 'text': (tf, tl, tp), 'image': (imf, il, ip),
-                'fusion': (fl, fp, aw, dw)}
+            if self.pipelined:
+                fstream = self._tail
+                fstream.wait_stream(main)
+                fstream.wait_stream(side)
+                for t in (sf, sl, sp, imf, il, ip, tf, tl, tp):
+                    t.record_stream(fstream)
+            else:
+                main.wait_stream(side)
+                for t in (sf, sl, sp, imf, il, ip):
+                    t.record_stream(main)
+                fstream = main
+        with torch.cuda.stream(fstream):
+            fl, fp, aw, dw = self.fusion.forward(sf, tf, imf, sp, tp, ip)
+            out = {'speech': (sf, sl, sp), 'text': (tf, tl, tp), 'image': (imf, il, ip),
+                   'fusion': (fl, fp, aw, dw)}
+            extra = epilogue(out) if epilogue is not None else None
+        return out if epilogue is None else (out, extra)
+
+    def wait(self, stream=None):
+        """Make `stream` (default: the current one) wait for the last batch's fusion."""
+        if self.pipelined:
+            (stream or torch.cuda.current_stream(self.device)).wait_stream(self._tail)
 
     @staticmethod
     def pack_rows(out) -> torch.Tensor:

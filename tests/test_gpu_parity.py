@@ -111,19 +111,42 @@ def test_image_vs_oracle(models, dev, B):
 def test_fused_pipeline(dev):
     B = 8
     pipe = engine.FusedPipeline(device=dev)
-    x = syn.speech_inputs(B, seed=3)
-    ids, mask = syn.text_inputs(B, 128, seed=3, ragged=True)
-    gray = syn.image_inputs(B, seed=3)
-    out = pipe.forward(engine.to_device(x, dev), engine.to_device(ids, dev), engine.to_device(mask, dev),
-                       engine.to_device(gray, dev))
-    rows = pipe.pack_rows(out)
+    ref = None
+    for it in range(3):  # 1st call serial (autotune), then concurrent + pipelined batches
+        x = syn.speech_inputs(B, seed=3 + it)
+        ids, mask = syn.text_inputs(B, 128, seed=3 + it, ragged=True)
+        gray = syn.image_inputs(B, seed=3 + it)
+        out, rows = pipe.forward(engine.to_device(x, dev), engine.to_device(ids, dev), engine.to_device(mask, dev),
+                                 engine.to_device(gray, dev), epilogue=pipe.pack_rows)
+        pipe.wait()
+        torch.cuda.synchronize()
+        assert rows.shape == (B, engine.ROW)
+        got = {k: [t.cpu().numpy() for t in v] for k, v in out.items()}
+        rf = o_f.forward(syn.weights('fusion'), got['speech'][0], got['text'][0], got['image'][0],
+                         got['speech'][2], got['text'][2], got['image'][2])
+        assert np.abs(got['fusion'][1] - rf[1]).max() < 1e-5
+        assert np.allclose(rows[:, 21:28].cpu().numpy(), got['fusion'][1])
+        _, _, rp = o_t.forward(syn.weights('text'), ids, mask)
+        assert np.abs(got['text'][2] - rp).max() < PROB_TOL
+
+
+def test_pipelined_batches_match_serial(dev):
+    """Overlapping batch i's fusion with batch i+1's encoders changes no result."""
+    B = 16
+    inputs = []
+    for it in range(4):
+        ids, mask = syn.text_inputs(B, 128, seed=50 + it, ragged=True)
+        inputs.append(tuple(engine.to_device(a, dev) for a in (syn.speech_inputs(B, seed=50 + it), ids, mask,
+                                                                  syn.image_inputs(B, seed=50 + it))))
+    serial = engine.FusedPipeline(device=dev, concurrent=False)
+    piped = engine.FusedPipeline(device=dev)
+    want = [engine.FusedPipeline.pack_rows(serial.forward(*a)).cpu() for a in inputs]
+    piped.forward(*inputs[0])  # autotune call
+    got = [piped.forward(*a, epilogue=engine.FusedPipeline.pack_rows)[1] for a in inputs]
+    piped.wait()
     torch.cuda.synchronize()
-    assert rows.shape == (B, engine.ROW)
-    got = {k: [t.cpu().numpy() for t in v] for k, v in out.items()}
-    rf = o_f.forward(syn.weights('fusion'), got['speech'][0], got['text'][0], got['image'][0],
-                     got['speech'][2], got['text'][2], got['image'][2])
-    assert np.abs(got['fusion'][1] - rf[1]).max() < 1e-5
-    assert np.allclose(rows[:, 21:28].cpu().numpy(), got['fusion'][1])
+    for w, g in zip(want, got):
+        assert torch.equal(w, g.cpu())
 
 
 def test_empty_batch(models, dev):
