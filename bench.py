@@ -53,6 +53,7 @@ def parse():
     ap.add_argument('--no-pipeline', action='store_true',
                     help="run each batch's fusion on the main stream (A/B of the cross-batch overlap)")
     ap.add_argument('--no-configs', action='store_true', help='skip the per-config (single-encoder) timings')
+    ap.add_argument('--text-priority', type=int, default=1, help='0: BERT on the default-priority stream (A/B)')
     return ap.parse_args()
 
 
@@ -131,7 +132,8 @@ def main():
 
     from mec import engine, synthetic as syn
     B = a.batch
-    pipe = engine.FusedPipeline(seed=1234, device=dev, concurrent=not a.serial, pipelined=not a.no_pipeline)
+    pipe = engine.FusedPipeline(seed=1234, device=dev, concurrent=not a.serial, pipelined=not a.no_pipeline,
+                                text_priority=bool(a.text_priority))
     x = engine.to_device(syn.speech_inputs(B, seed=rank), dev)
     ids_np, mask_np = syn.text_inputs(B, 128, seed=rank, ragged=False)
     ids, mask = engine.to_device(ids_np, dev), engine.to_device(mask_np, dev)

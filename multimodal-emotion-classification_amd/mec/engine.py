@@ -220,10 +220,11 @@ ROW = 34
 class FusedPipeline:
     """The whole tri-modal path: speech + text + image encoders, then the fusion model.
 
-    BERT runs on the caller's stream; speech and the image backbone run concurrently on a
-    second HIP stream (their kernels fill the CUs that BERT's GEMM tails and its
-    LayerNorm/attention kernels leave idle). The first call runs everything serially so each
-    GEMM shape is autotuned in isolation.
+    BERT runs on a high-priority stream (text_priority; else the caller's stream); speech and
+    the image backbone run concurrently on a second HIP stream at normal priority, so BERT's
+    workgroups are dispatched first and the image kernels fill the CUs that BERT's GEMM tails
+    and its LayerNorm/attention kernels leave idle (+1.5% over equal priorities). The first
+    call runs everything serially so each GEMM shape is autotuned in isolation.
 
     pipelined=True (the default with concurrent=True): the fusion model (and the caller's
     `epilogue`, e.g. packing and the all-gather) runs on a third stream that waits for both
@@ -234,7 +235,7 @@ class FusedPipeline:
     """
 
     def __init__(self, seed: int = 1234, device=None, weights=None, concurrent: bool = True,
-                 image_backbone: str = 'resnet50', pipelined: bool = True):
+                 image_backbone: str = 'resnet50', pipelined: bool = True, text_priority: bool = True):
         weights = weights or {}
         self.speech = SpeechEncoder(weights.get('speech'), seed, device)
         self.text = TextEncoder(weights.get('text'), seed, device)
@@ -245,6 +246,9 @@ class FusedPipeline:
         self.pipelined = concurrent and pipelined
         self._side = torch.cuda.Stream(device=self.device) if concurrent else None
         self._tail = torch.cuda.Stream(device=self.device) if self.pipelined else None
+        # text_priority: BERT on its own high-priority stream, so its workgroups are dispatched
+        # ahead of the image stream's and the image kernels fill the CUs BERT leaves idle
+        self._text = torch.cuda.Stream(device=self.device, priority=-1) if (concurrent and text_priority) else None
         self._tuned = False
 
     def forward(self, x_speech, ids, mask, gray, epilogue=None):
@@ -263,12 +267,25 @@ class FusedPipeline:
             with torch.cuda.stream(side):
                 sf, sl, sp = self.speech.forward(x_speech)
                 imf, il, ip = self.image.forward(gray)
-            tf, tl, tp = self.text.forward(ids, mask)
+            if self._text is not None:
+                tstream = self._text
+                tstream.wait_stream(main)
+                with torch.cuda.stream(tstream):
+                    tf, tl, tp = self.text.forward(ids, mask)
+                for t in (ids, mask):
+                    t.record_stream(tstream)
+                if not self.pipelined:
+                    main.wait_stream(tstream)
+                    for t in (tf, tl, tp):
+                        t.record_stream(main)
+            else:
+                tstream = main
+                tf, tl, tp = self.text.forward(ids, mask)
             for t in (x_speech, gray):
                 t.record_stream(side)
             if self.pipelined:
                 fstream = self._tail
-                fstream.wait_stream(main)
+                fstream.wait_stream(tstream)
                 fstream.wait_stream(side)
                 for t in (sf, sl, sp, imf, il, ip, tf, tl, tp):
                     t.record_stream(fstream)
