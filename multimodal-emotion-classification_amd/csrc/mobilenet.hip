@@ -311,6 +311,297 @@ __global__ __launch_bounds__(256) void mbv2_block_kernel(const MbArgs a) {
   }
 }
 
+// ----------------------------------------------------------------------------- wave-autonomous form
+// The same block arithmetic (same k orders, same roundings: bit-identical outputs), organised
+// so that no workgroup barrier sits inside the tile loop. Every WAVE is an independent worker
+// on 4x4 output tiles (16 pixels = one MFMA q-tile) with its own LDS slices for the input
+// tile (+ halo), the expanded chunk, the depthwise output and the output staging; the four
+// waves of a workgroup only share the block constants (depthwise weights and biases), staged
+// once. A wave's LDS writes are read back by the same wave (DS operations of one wave execute
+// in order), so the hidden-channel chunks run back to back, and the waves of a CU interleave
+// freely: the latency one wave exposes (HBM, weight fragments, LDS) is covered by the others.
+// The 4x4 tile recomputes more halo in the expand (6x6 inputs per 16 outputs at stride 1)
+// than an 8x8 tile; that is MFMA work, cheap next to the latency it removes.
+constexpr int MBW_TO = 4;
+
+template <int S, int CINP, int HIDP, int COUTP, bool EXPAND, bool RES, int STEM>
+struct MbwGeom {
+  static constexpr int IR = (MBW_TO - 1) * S + 3;   // input tile side (with halo): 6 or 9
+  static constexpr int NP = IR * IR, MP = (NP + 15) / 16 * 16;
+  static constexpr int XLD = CINP + 8, ELD = MB_HC + 8, OLD = COUTP + 8;
+  static constexpr int W_X = MP * XLD;
+  static constexpr int W_E = EXPAND ? MP * ELD : 0;
+  static constexpr int W_D = 16 * ELD;
+  // output staging: its own slice when the input tile must survive for the residual,
+  // else it reuses the input tile's slice (free after the last chunk's expand)
+  static constexpr int W_O = (RES || 16 * OLD > W_X) ? 16 * OLD : 0;
+  static constexpr int W_TOT = W_X + W_E + W_D + W_O;  // halfs per wave (all multiples of 8)
+  static constexpr bool DW_LDS = HIDP * 9 * 4 <= 16384;  // depthwise weights staged in LDS
+  static constexpr int PR = 2 * IR + 1;                  // stem: u8 patch side
+};
+
+template <int S, int CINP, int HIDP, int COUTP, bool EXPAND, bool RES, int STEM>
+__global__ __launch_bounds__(256) void mbv2_wave_kernel(const MbArgs a, int ntiles) {
+  using G = MbwGeom<S, CINP, HIDP, COUTP, EXPAND, RES, STEM>;
+  constexpr int TO = MBW_TO, IR = G::IR, NP = G::NP, MP = G::MP;
+  constexpr int XLD = G::XLD, ELD = G::ELD, OLD = G::OLD;
+  constexpr int OT = COUTP / 16, KX = CINP / 32;
+  static_assert(!STEM || (CINP == 32 && HIDP == 32 && !EXPAND && S == 1), "stem fuses into block 1 only");
+  __shared__ __attribute__((aligned(16))) f16 sw[4 * G::W_TOT];
+  __shared__ __attribute__((aligned(16))) float sWd[G::DW_LDS ? HIDP * 9 : 4];
+  __shared__ __attribute__((aligned(16))) float sBd[HIDP];
+  __shared__ __attribute__((aligned(16))) float sBe[EXPAND ? HIDP : 4];
+  __shared__ __attribute__((aligned(16))) float sBp[COUTP];
+  __shared__ __attribute__((aligned(16))) float sSW[STEM ? STEM * 9 * 32 : 4];
+  __shared__ uint8_t sPatch[STEM ? 4 * G::PR * G::PR * STEM : 4];
+
+  const int tid = threadIdx.x, lane = tid & 63;
+  const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int l16 = lane & 15, lq = lane >> 4;
+  f16* sX = sw + wave * G::W_TOT;
+  f16* sE = sX + G::W_X;
+  f16* sD = sE + G::W_E;
+  f16* sO = G::W_O ? sD + G::W_D : sX;
+
+  if constexpr (G::DW_LDS)
+    for (int i = tid; i < HIDP * 9 / 4; i += 256)
+      reinterpret_cast<float4*>(sWd)[i] = reinterpret_cast<const float4*>(a.Wd)[i];
+  for (int i = tid; i < HIDP / 4; i += 256) {
+    reinterpret_cast<float4*>(sBd)[i] = reinterpret_cast<const float4*>(a.bd)[i];
+    if constexpr (EXPAND) reinterpret_cast<float4*>(sBe)[i] = reinterpret_cast<const float4*>(a.be)[i];
+  }
+  if (tid < COUTP / 4) reinterpret_cast<float4*>(sBp)[tid] = reinterpret_cast<const float4*>(a.bp)[tid];
+  if constexpr (STEM != 0)
+    for (int i = tid; i < STEM * 9 * 8; i += 256)
+      reinterpret_cast<float4*>(sSW)[i] = reinterpret_cast<const float4*>(a.stem_w)[i];
+  __syncthreads();  // the only workgroup barrier
+
+  const int H = a.H, OH = a.OH;
+  const int tpr = (OH + TO - 1) / TO, tpi = tpr * tpr;
+  const float* wdsrc = G::DW_LDS ? sWd : a.Wd;
+  // depthwise item of this lane: output pixel dq of the tile, channels 8 dcg .. 8 dcg + 7
+  const int dq = lane >> 2, dcg = lane & 3;
+  const int dp0 = ((dq >> 2) * S) * IR + (dq & 3) * S;
+
+#pragma unroll 1
+  for (int tile = blockIdx.x * 4 + wave; tile < ntiles; tile += gridDim.x * 4) {
+    const int n = tile / tpi, tt = tile - n * tpi;
+    const int oy0 = (tt / tpr) * TO, ox0 = (tt - (tt / tpr) * tpr) * TO;
+    const int iy0 = oy0 * S - 1, ix0 = ox0 * S - 1;
+
+    // ---- stage the input tile (zeros outside the image and past cin)
+    if constexpr (STEM == 0) {
+      constexpr int C8 = CINP / 8;
+      constexpr int NIT = (MP * C8 + 63) / 64;
+      static_assert(NIT <= 32, "validity bits");
+      const f16* xin = a.x + (size_t)n * H * H * a.cin;
+      half8 v[NIT];
+      uint32_t ok = 0;
+#pragma unroll
+      for (int j = 0; j < NIT; ++j) {  // unconditional clamped loads, zeroed at the LDS write
+        const int i = lane + 64 * j;
+        const int p = min(i / C8, NP - 1), c8 = i - (i / C8) * C8;
+        const int iy = iy0 + p / IR, ix = ix0 + p % IR;
+        const bool in = i < NP * C8 && iy >= 0 && iy < H && ix >= 0 && ix < H && c8 * 8 < a.cin;
+        ok |= (uint32_t)in << j;
+        const int cy = min(max(iy, 0), H - 1), cx = min(max(ix, 0), H - 1);
+        const int cc = min(c8 * 8, a.cin - 8);
+        v[j] = *reinterpret_cast<const half8*>(xin + ((size_t)cy * H + cx) * a.cin + cc);
+      }
+#pragma unroll
+      for (int j = 0; j < NIT; ++j) {
+        const int i = lane + 64 * j;
+        const half8 z = {0, 0, 0, 0, 0, 0, 0, 0};
+        if (i < MP * C8) *reinterpret_cast<half8*>(sX + (i / C8) * XLD + (i % C8) * 8) = ((ok >> j) & 1) ? v[j] : z;
+      }
+    } else {
+      constexpr int PR = G::PR;
+      uint8_t* patch = sPatch + wave * PR * PR * STEM;
+      const uint8_t* img = reinterpret_cast<const uint8_t*>(a.x) + (size_t)n * 224 * 224 * STEM;
+      const int ry0 = 2 * iy0 - 1, rx0 = 2 * ix0 - 1;
+      for (int i = lane; i < PR * PR * STEM; i += 64) {
+        const int c = i % STEM, pix = i / STEM;
+        const int yy = ry0 + pix / PR, xx = rx0 + pix % PR;
+        const int cy = min(max(yy, 0), 223), cx = min(max(xx, 0), 223);
+        const uint8_t u = img[((size_t)cy * 224 + cx) * STEM + c];
+        patch[i] = (yy >= 0 && yy < 224 && xx >= 0 && xx < 224) ? u : 0;
+      }
+      for (int i = lane; i < MP * 4; i += 64) {
+        const int p = i >> 2, cg = i & 3;
+        const int py = p / IR, px = p - (p / IR) * IR;
+        const int iy = iy0 + py, ix = ix0 + px;
+        half8 v = {0, 0, 0, 0, 0, 0, 0, 0};
+        if (p < NP && iy >= 0 && iy < 112 && ix >= 0 && ix < 112) {
+          const int cls = (iy == 0 ? 2 : 0) + (ix == 0 ? 1 : 0);
+          float acc[8];
+          const float4 c0 = *reinterpret_cast<const float4*>(a.stem_corr + cls * 32 + cg * 8);
+          const float4 c1 = *reinterpret_cast<const float4*>(a.stem_corr + cls * 32 + cg * 8 + 4);
+          acc[0] = c0.x; acc[1] = c0.y; acc[2] = c0.z; acc[3] = c0.w;
+          acc[4] = c1.x; acc[5] = c1.y; acc[6] = c1.z; acc[7] = c1.w;
+#pragma unroll
+          for (int ky = 0; ky < 3; ++ky)
+#pragma unroll
+            for (int kx = 0; kx < 3; ++kx)
+#pragma unroll
+              for (int c = 0; c < STEM; ++c) {
+                const float u = (float)patch[((2 * py + ky) * PR + 2 * px + kx) * STEM + c];
+                const float* w = sSW + ((c * 3 + ky) * 3 + kx) * 32 + cg * 8;
+                const float4 w0 = *reinterpret_cast<const float4*>(w);
+                const float4 w1 = *reinterpret_cast<const float4*>(w + 4);
+                acc[0] = __builtin_fmaf(u, w0.x, acc[0]); acc[1] = __builtin_fmaf(u, w0.y, acc[1]);
+                acc[2] = __builtin_fmaf(u, w0.z, acc[2]); acc[3] = __builtin_fmaf(u, w0.w, acc[3]);
+                acc[4] = __builtin_fmaf(u, w1.x, acc[4]); acc[5] = __builtin_fmaf(u, w1.y, acc[5]);
+                acc[6] = __builtin_fmaf(u, w1.z, acc[6]); acc[7] = __builtin_fmaf(u, w1.w, acc[7]);
+              }
+#pragma unroll
+          for (int j = 0; j < 8; ++j) v[j] = (f16)relu6f(acc[j]);
+        }
+        *reinterpret_cast<half8*>(sX + p * XLD + cg * 8) = v;
+      }
+    }
+
+    floatx4 acc[OT];
+#pragma unroll
+    for (int o = 0; o < OT; ++o) acc[o] = floatx4{0.f, 0.f, 0.f, 0.f};
+
+    // Weight fragments of a hidden-channel chunk: expand (af) and project (pf). With two
+    // register sets (PF2) the next chunk's fragments are in flight while this chunk computes.
+    constexpr bool PF2 = OT + (EXPAND ? 2 * KX : 0) <= 6;  // larger sets cost occupancy (measured)
+    auto loadw = [&](int h0, half8 (&af)[2][KX], half8 (&pf)[OT]) {
+#pragma unroll
+      for (int o = 0; o < OT; ++o)
+        pf[o] = *reinterpret_cast<const half8*>(a.Wp + (size_t)(16 * o + l16) * HIDP + h0 + 8 * lq);
+      if constexpr (EXPAND) {
+#pragma unroll
+        for (int ht = 0; ht < 2; ++ht)
+#pragma unroll
+          for (int k = 0; k < KX; ++k)
+            af[ht][k] = *reinterpret_cast<const half8*>(a.We + (size_t)(h0 + 16 * ht + l16) * CINP + 32 * k + 8 * lq);
+      }
+    };
+    auto chunk = [&](int h0, const half8 (&af)[2][KX], const half8 (&pf)[OT]) {
+      const f16* src;
+      int sld;
+      if constexpr (EXPAND) {
+        float eb[2][4];
+#pragma unroll
+        for (int ht = 0; ht < 2; ++ht)
+#pragma unroll
+          for (int e = 0; e < 4; ++e) eb[ht][e] = sBe[h0 + 16 * ht + 4 * lq + e];
+#pragma unroll
+        for (int pt = 0; pt < MP / 16; ++pt) {
+          const int p = pt * 16 + l16;
+          const int iy = iy0 + p / IR, ix = ix0 + p % IR;
+          const bool valid = p < NP && iy >= 0 && iy < H && ix >= 0 && ix < H;
+          floatx4 e2[2] = {floatx4{0.f, 0.f, 0.f, 0.f}, floatx4{0.f, 0.f, 0.f, 0.f}};
+#pragma unroll
+          for (int k = 0; k < KX; ++k) {
+            const half8 bf = *reinterpret_cast<const half8*>(sX + p * XLD + 32 * k + 8 * lq);
+#pragma unroll
+            for (int ht = 0; ht < 2; ++ht)
+              e2[ht] = __builtin_amdgcn_mfma_f32_16x16x32_f16(af[ht][k], bf, e2[ht], 0, 0, 0);
+          }
+#pragma unroll
+          for (int ht = 0; ht < 2; ++ht) {
+            half4 hv;
+#pragma unroll
+            for (int e = 0; e < 4; ++e) hv[e] = valid ? (f16)relu6f(e2[ht][e] + eb[ht][e]) : (f16)0.f;
+            *reinterpret_cast<half4*>(sE + p * ELD + 16 * ht + 4 * lq) = hv;
+          }
+        }
+        src = sE;
+        sld = ELD;
+      } else {
+        src = sX + h0;
+        sld = XLD;
+      }
+      // ---- depthwise 3x3/S + BN + ReLU6 (fp32): 16 pixels x 32 channels, 8 per lane
+      {
+        const int hc = h0 + 8 * dcg;
+        float d[8];
+        {
+          const float4 b0 = *reinterpret_cast<const float4*>(sBd + hc);
+          const float4 b1 = *reinterpret_cast<const float4*>(sBd + hc + 4);
+          d[0] = b0.x; d[1] = b0.y; d[2] = b0.z; d[3] = b0.w; d[4] = b1.x; d[5] = b1.y; d[6] = b1.z; d[7] = b1.w;
+        }
+        const float* wd = wdsrc + (size_t)(hc / 8) * 72;
+#pragma unroll
+        for (int ky = 0; ky < 3; ++ky)
+#pragma unroll
+          for (int kx = 0; kx < 3; ++kx) {
+            const half8 ev = *reinterpret_cast<const half8*>(src + (dp0 + ky * IR + kx) * sld + 8 * dcg);
+            const float4 w0 = *reinterpret_cast<const float4*>(wd + (ky * 3 + kx) * 8);
+            const float4 w1 = *reinterpret_cast<const float4*>(wd + (ky * 3 + kx) * 8 + 4);
+            d[0] = __builtin_fmaf((float)ev[0], w0.x, d[0]); d[1] = __builtin_fmaf((float)ev[1], w0.y, d[1]);
+            d[2] = __builtin_fmaf((float)ev[2], w0.z, d[2]); d[3] = __builtin_fmaf((float)ev[3], w0.w, d[3]);
+            d[4] = __builtin_fmaf((float)ev[4], w1.x, d[4]); d[5] = __builtin_fmaf((float)ev[5], w1.y, d[5]);
+            d[6] = __builtin_fmaf((float)ev[6], w1.z, d[6]); d[7] = __builtin_fmaf((float)ev[7], w1.w, d[7]);
+          }
+        half8 out;
+#pragma unroll
+        for (int j = 0; j < 8; ++j) out[j] = (f16)relu6f(d[j]);
+        *reinterpret_cast<half8*>(sD + dq * ELD + 8 * dcg) = out;
+      }
+      // ---- project: out^T[o][q] += Wp[o][h0 .. h0+31] . D[q][:]
+      {
+        const half8 bf = *reinterpret_cast<const half8*>(sD + l16 * ELD + 8 * lq);
+#pragma unroll
+        for (int o = 0; o < OT; ++o) acc[o] = __builtin_amdgcn_mfma_f32_16x16x32_f16(pf[o], bf, acc[o], 0, 0, 0);
+      }
+    };
+    half8 afA[2][KX], pfA[OT];
+    if constexpr (PF2) {
+      half8 afB[2][KX], pfB[OT];
+      loadw(0, afA, pfA);
+#pragma unroll 1
+      for (int h0 = 0; h0 < HIDP; h0 += 2 * MB_HC) {
+        if (h0 + MB_HC < HIDP) loadw(h0 + MB_HC, afB, pfB);
+        chunk(h0, afA, pfA);
+        if (h0 + MB_HC >= HIDP) break;
+        if (h0 + 2 * MB_HC < HIDP) loadw(h0 + 2 * MB_HC, afA, pfA);
+        chunk(h0 + MB_HC, afB, pfB);
+      }
+    } else {
+#pragma unroll 1
+      for (int h0 = 0; h0 < HIDP; h0 += MB_HC) {
+        loadw(h0, afA, pfA);
+        chunk(h0, afA, pfA);
+      }
+    }
+
+    // ---- epilogue: + BN shift (+ residual from the staged input tile) -> f16 -> 16-B row stores
+    {
+      const int q = l16;
+      const int pc = ((q >> 2) * S + 1) * IR + (q & 3) * S + 1;
+      half4 hv[OT];
+#pragma unroll
+      for (int o = 0; o < OT; ++o) {  // all residual reads before any staging write (sO may alias sX)
+        const int c = 16 * o + 4 * lq;
+        const float4 bv = *reinterpret_cast<const float4*>(sBp + c);
+        float v[4] = {acc[o][0] + bv.x, acc[o][1] + bv.y, acc[o][2] + bv.z, acc[o][3] + bv.w};
+        if constexpr (RES) {
+          const half4 r = *reinterpret_cast<const half4*>(sX + pc * XLD + c);
+#pragma unroll
+          for (int e = 0; e < 4; ++e) v[e] += (float)r[e];
+        }
+#pragma unroll
+        for (int e = 0; e < 4; ++e) hv[o][e] = (f16)v[e];
+      }
+#pragma unroll
+      for (int o = 0; o < OT; ++o) *reinterpret_cast<half4*>(sO + q * OLD + 16 * o + 4 * lq) = hv[o];
+      const int C8 = a.cout / 8;
+      f16* yout = a.y + (size_t)n * OH * OH * a.cout;
+      for (int i = lane; i < 16 * C8; i += 64) {
+        const int qq = i / C8, c8 = i - (i / C8) * C8;
+        const int oy = oy0 + (qq >> 2), ox = ox0 + (qq & 3);
+        if (oy < OH && ox < OH)
+          *reinterpret_cast<half8*>(yout + ((size_t)oy * OH + ox) * a.cout + c8 * 8) =
+              *reinterpret_cast<const half8*>(sO + qq * OLD + c8 * 8);
+      }
+    }
+  }
+}
+
 // ----------------------------------------------------------------------------- model
 
 static int pad_to(int v, int m) { return (v + m - 1) / m * m; }
@@ -471,13 +762,65 @@ int MobileNetModel::create(const float* blob, size_t n) {
   return 0;
 }
 
+// mec_set_option("mbv2_impl"): 1 = workgroup tiles, 2 = wave-autonomous tiles, 0 = per block
+// shape, whichever ran faster at its first launch (hipEvents, median of 3; both forms are
+// bit-identical, so the choice changes speed only). Measured at B=256: the wave form wins
+// the stride-2 blocks and the mid-size stride-1 ones, the workgroup form the stem block and
+// the wide late blocks (their depthwise weights no longer fit beside four waves' tiles).
+int g_mbv2_impl = 0;
+
 template <int S, int TO, int CINP, int HIDP, int COUTP, bool EXPAND, bool RES, int STEM>
-static int launch_block(const MbArgs& a, int B, hipStream_t s) {
-  const int tpr = a.OH / TO;
-  hipLaunchKernelGGL((mbv2_block_kernel<S, TO, CINP, HIDP, COUTP, EXPAND, RES, STEM>), dim3(B * tpr * tpr), dim3(256),
-                     0, s, a);
+static int run_block(const MbArgs& a, int B, hipStream_t s, int impl) {
+  if (impl == 2) {
+    static int ncu = 0;
+    if (!ncu) {
+      int dev = 0;
+      MEC_HIP(hipGetDevice(&dev));
+      MEC_HIP(hipDeviceGetAttribute(&ncu, hipDeviceAttributeMultiprocessorCount, dev));
+    }
+    const int tpr = (a.OH + MBW_TO - 1) / MBW_TO;
+    const int ntiles = B * tpr * tpr;
+    const int grid = std::min((ntiles + 3) / 4, 8 * ncu);  // waves loop over the remaining tiles
+    hipLaunchKernelGGL((mbv2_wave_kernel<S, CINP, HIDP, COUTP, EXPAND, RES, STEM>), dim3(grid), dim3(256), 0, s, a,
+                       ntiles);
+  } else {
+    const int tpr = a.OH / TO;
+    hipLaunchKernelGGL((mbv2_block_kernel<S, TO, CINP, HIDP, COUTP, EXPAND, RES, STEM>), dim3(B * tpr * tpr),
+                       dim3(256), 0, s, a);
+  }
   MEC_LAUNCH_CHECK();
   return 0;
+}
+
+template <int S, int TO, int CINP, int HIDP, int COUTP, bool EXPAND, bool RES, int STEM>
+static int launch_block(const MbArgs& a, int B, hipStream_t s) {
+  static int choice = 0;  // per block shape, once tuned
+  int impl = g_mbv2_impl;
+  if (impl == 0) {
+    hipStreamCaptureStatus cs = hipStreamCaptureStatusNone;
+    if (!choice && hipStreamIsCapturing(s, &cs) == hipSuccess && cs == hipStreamCaptureStatusNone) {
+      constexpr int REPS = 3;
+      hipEvent_t ev[REPS + 1];
+      for (auto& e : ev) MEC_HIP(hipEventCreate(&e));
+      float best = 1e30f;
+      for (int cand = 1; cand <= 2; ++cand) {
+        MEC_TRY((run_block<S, TO, CINP, HIDP, COUTP, EXPAND, RES, STEM>(a, B, s, cand)));  // warm
+        MEC_HIP(hipEventRecord(ev[0], s));
+        for (int r = 0; r < REPS; ++r) {
+          MEC_TRY((run_block<S, TO, CINP, HIDP, COUTP, EXPAND, RES, STEM>(a, B, s, cand)));
+          MEC_HIP(hipEventRecord(ev[r + 1], s));
+        }
+        MEC_HIP(hipEventSynchronize(ev[REPS]));
+        float t[REPS];
+        for (int r = 0; r < REPS; ++r) MEC_HIP(hipEventElapsedTime(&t[r], ev[r], ev[r + 1]));
+        std::sort(t, t + REPS);
+        if (t[REPS / 2] < best) { best = t[REPS / 2]; choice = cand; }
+      }
+      for (auto& e : ev) (void)hipEventDestroy(e);
+    }
+    impl = choice ? choice : 1;
+  }
+  return run_block<S, TO, CINP, HIDP, COUTP, EXPAND, RES, STEM>(a, B, s, impl);
 }
 
 // The 17 block shapes of mobilenet_v2 (width 1.0) at 224x224: (stride, tile, cinp, hidp,
