@@ -238,6 +238,11 @@ int mec_set_option(const char* key, int value) {
   if (k == "gemm_prefetch_r" && (value == 0 || value == 1)) { g_gemm_prefetch_r = value; return 0; }
   if (k == "resnet_fused_tail" && (value == 0 || value == 1)) { g_resnet_fused_tail = value; return 0; }
   if (k == "mbv2_impl" && value >= 0 && value <= 2) { g_mbv2_impl = value; return 0; }
+  if (k == "conv3x3_direct" && (value == 0 || value == 1)) { g_conv3x3_direct = value; return 0; }
+  if (k == "conv3x3_debug" && (value == 0 || value == 1 || value == 2 || value == 4 || value == 7)) {
+    g_conv3x3_debug = value;
+    return 0;
+  }
   const int v = value % 10000;
   const bool deep = value == 20256 || value == 30256 || value == 20128 || value == 40256 || value == 41256 || value == 50128 ||
                     value == 60128 || value == 50256;

@@ -210,6 +210,7 @@ static int launch_mode(const GemmParams& p, hipStream_t s) {
 
 int g_gemm_impl = 2;  // 1 = register-staged 128x128 kernel, 2 = glds pipelined (default)
 int g_gemm_bn = 0;    // 0 = auto tile width
+int g_conv3x3_direct = 1;  // ResNet layer1 conv2 on the halo-tile kernel (conv3x3.hip)
 
 int launch_gemm(const GemmParams& p, hipStream_t s, Prof* prof, int tag) {
   MEC_REQUIRE(p.M > 0 && p.N > 0 && p.K > 0, "gemm: empty shape");
@@ -229,7 +230,10 @@ int launch_gemm(const GemmParams& p, hipStream_t s, Prof* prof, int tag) {
   }
   if (prof) MEC_TRY(prof->begin(tag, s));
   int rc;
-  if (g_gemm_impl == 2)
+  if (g_conv3x3_direct && !g_gemm_bn && p.amode == A_CONV && p.ks == 3 && p.stride == 1 && p.pad == 1 && p.H == 56 &&
+      p.W == 56 && p.C == 64 && p.N == 64 && p.act == ACT_RELU && !p.R && p.C16 && !p.C32 && p.M % (56 * 56) == 0)
+    rc = launch_conv3x3_c64(reinterpret_cast<const f16*>(p.A), p.B, p.bias, p.C16, p.M / (56 * 56), 56, 64, 64, s);
+  else if (g_gemm_impl == 2)
     rc = launch_gemm_glds(p, s, g_gemm_bn);
   else
     rc = (p.N % 128 == 0) ? launch_mode<128, 128>(p, s) : launch_mode<128, 64>(p, s);

@@ -132,6 +132,12 @@ extern int g_gemm_bn;
 extern int g_gemm_autotune;
 extern int g_gemm_debug;
 extern int g_gemm_prefetch_r;
+// 3x3/1 conv 64 -> 64 on 56x56 (+ BN shift + ReLU) as a halo-tile kernel (conv3x3.hip);
+// launch_gemm routes matching A_CONV shapes to it while g_conv3x3_direct is set
+int launch_conv3x3_c64(const f16* x, const f16* w, const float* bias, f16* y, int B, int H, int C, int Cout,
+                       hipStream_t s);
+extern int g_conv3x3_direct;
+extern int g_conv3x3_debug;
 int gemm_tuned_bn(int amode, int M, int N, int K);
 
 }  // namespace mec

@@ -188,3 +188,31 @@ def test_fused_bottleneck_tail_bit_identical(dev):
     lib.mec_set_option(b'resnet_fused_tail', 0)
     for a, b in zip(*outs):
         assert torch.equal(a, b)
+
+
+@pytest.mark.parametrize('n', [1, 3, 37, 75])
+def test_conv3x3_c64_bit_identical(dev, n):
+    """ResNet layer1's 3x3 conv (56x56, 64 -> 64) on the halo-tile kernel (conv3x3.hip) vs the
+    implicit-GEMM path: bit-identical, and close to torch fp32. n = 37 / 75 give 259 / 525
+    tiles, so workgroups walk several tiles through both halo buffers."""
+    lib = _lib.load()
+    g = torch.Generator().manual_seed(n)
+    x = torch.rand(n, 56, 56, 64, generator=g).half().to(dev)
+    w = ((torch.rand(64, 3, 3, 64, generator=g) * 2 - 1) * 576 ** -0.5).half().to(dev)
+    bias = (torch.rand(64, generator=g) - 0.5).to(dev)
+    outs = []
+    for direct in (1, 0):
+        _lib.check(lib.mec_set_option(b'conv3x3_direct', direct), 'option')
+        y = torch.full((n, 56, 56, 64), float('nan'), dtype=torch.float16, device=dev)
+        try:
+            _lib.check(lib.mec_conv_f16(_p(x), _p(w), _p(bias), None, _p(y), n, 56, 56, 64, 64, 3, 1, 1, 1, _s()),
+                       'conv')
+        finally:
+            lib.mec_set_option(b'conv3x3_direct', 1)
+        torch.cuda.synchronize()
+        outs.append(y.cpu())
+    ref = torch.relu(torch.nn.functional.conv2d(x.permute(0, 3, 1, 2).float(), w.permute(0, 3, 1, 2).float(), bias,
+                                                padding=1)).permute(0, 2, 3, 1).cpu()
+    assert not torch.isnan(outs[0]).any()
+    assert _rel_err(outs[0].float(), ref) < 2e-3
+    assert torch.equal(outs[0], outs[1])

@@ -15,6 +15,9 @@ def main():
     ap.add_argument('--match', default=None, help='substring filter on the kernel name')
     ap.add_argument('--window', default=None, help='marker kernel name substring')
     ap.add_argument('--steps', type=int, default=0)
+    ap.add_argument('--sequence', action='store_true',
+                    help='with --window and --steps: list one step\'s dispatches in launch order, '
+                         'each averaged over the steps')
     a = ap.parse_args()
     c = sqlite3.connect(a.db)
     q = "select name, grid_x, workgroup_x, end-start, start from kernels order by start"
@@ -25,6 +28,19 @@ def main():
             raise SystemExit(f'fewer than two {a.window} dispatches in {a.db}')
         t0, t1 = rows[marks[0]][4], rows[marks[1]][4]
         rows = [r for r in rows if t0 < r[4] < t1 and a.window not in r[0]]
+    if a.sequence:
+        if not (a.window and a.steps) or len(rows) % a.steps:
+            raise SystemExit('--sequence needs --window, --steps and a whole number of dispatches per step')
+        n = len(rows) // a.steps
+        tot = 0.0
+        print(f"{'#':>4s} {'kernel':80s} {'blocks':>7s} {'avg_us':>9s} {'min_us':>9s} {'cum_ms':>8s}")
+        for i in range(n):
+            ds = [rows[k * n + i][3] for k in range(a.steps)]
+            name, gx, wx = rows[i][0], rows[i][1], rows[i][2]
+            tot += sum(ds) / len(ds)
+            print(f"{i:4d} {name[:80]:80s} {gx // max(wx, 1):7d} {sum(ds) / len(ds) / 1e3:9.1f} {min(ds) / 1e3:9.1f} "
+                  f"{tot / 1e6:8.3f}")
+        return
     agg = {}
     for name, gx, wx, d, _ in rows:
         if a.match and a.match not in name:
