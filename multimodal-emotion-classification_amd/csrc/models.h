@@ -115,6 +115,7 @@ int resize_u8(const uint8_t* in, int B, int H, int W, uint8_t* out, int OH, int 
 int launch_bneck_tail(const f16* t1, const f16* x, const f16* w2, const float* b2, const f16* w3, const float* b3,
                       f16* y, int B, int H, int w, hipStream_t s);
 extern int g_resnet_fused_tail;
+extern int g_resnet_chunk;
 
 extern int g_mbv2_impl;
 

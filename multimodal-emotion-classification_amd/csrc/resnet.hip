@@ -16,6 +16,10 @@ namespace mec {
 // --opt resnet_fused_tail=1). It moves fewer bytes (about 3 TB/s at 315 us) but runs one
 // 4-wave workgroup per CU, so LDS-read and barrier latency inside a tile is exposed.
 int g_resnet_fused_tail = 0;
+// Images per layer1-2 pass (0 = whole batch). Measured at B = 256 (tools/encoder_profile.py
+// --opt resnet_chunk=N): 0 -> 4.23-4.25 ms, 128 -> 4.38, 64 -> 4.44-4.49, 32 -> 5.08: the
+// smaller GEMMs lose more than the cache residency gains, so chunking is off.
+int g_resnet_chunk = 0;
 
 // ----------------------------------------------------------------------------- resize
 // Pillow ImagingResample (bilinear, 8bpc): 22-bit fixed-point taps, horizontal pass into
@@ -541,45 +545,70 @@ int ImageModel::forward_u8(const uint8_t* img, int B, int H, int W, int C, float
     MEC_LAUNCH_CHECK();
     MEC_TRY(prof.end(TAG_RESNET_STEM, s));
   }
+  // Bottleneck blocks [b0, b1) over images [i0, i0 + nb) of the batch (NHWC buffers are
+  // image-major, so an image range is a pointer offset). cur/other swap once per block.
+  auto run_blocks = [&](size_t b0, size_t b1, int i0, int nb, int Hin, f16*& cur, f16*& other) -> int {
+    int H = Hin;
+    for (size_t bi = b0; bi < b1; ++bi) {
+      const Bottleneck& bk = blocks[bi];
+      const int wd = bk.c1.cout, cin = bk.c1.cin, st = bk.c2.stride;
+      const int OH = (H + 2 - 3) / st + 1;
+      f16* in = cur + (size_t)i0 * H * H * cin;
+      f16* out = other + (size_t)i0 * OH * OH * 4 * wd;
+      f16* t1 = T1 + (size_t)i0 * H * H * wd;
+      f16* t2 = T2 + (size_t)i0 * OH * OH * wd;
+      GemmParams g;
+      g.A = in; g.B = Wt + bk.c1.w_off; g.bias = P + bk.c1.b_off; g.act = ACT_RELU; g.C16 = t1;
+      g.M = nb * H * H; g.N = wd; g.K = cin;
+      MEC_TRY(launch_gemm(g, s, &prof, TAG_RESNET_CONV1X1));
+      if (!bk.has_ds && g_resnet_fused_tail && wd == 64 && H == 56) {
+        // conv2 + conv3 + residual + ReLU in one kernel (bottleneck.hip)
+        MEC_TRY(prof.begin(TAG_RESNET_CONV3X3, s));
+        MEC_TRY(launch_bneck_tail(t1, in, Wt + bk.c2.w_off, P + bk.c2.b_off, Wt + bk.c3.w_off, P + bk.c3.b_off, out,
+                                  nb, H, wd, s));
+        MEC_TRY(prof.end(TAG_RESNET_CONV3X3, s));
+        std::swap(cur, other);
+        continue;
+      }
+      g = GemmParams();
+      g.amode = A_CONV; g.A = t1; g.B = Wt + bk.c2.w_off; g.bias = P + bk.c2.b_off; g.act = ACT_RELU; g.C16 = t2;
+      g.M = nb * OH * OH; g.N = wd; g.K = 9 * wd;
+      g.H = H; g.W = H; g.C = wd; g.OH = OH; g.OW = OH; g.ks = 3; g.stride = st; g.pad = 1;
+      MEC_TRY(launch_gemm(g, s, &prof, TAG_RESNET_CONV3X3));
+      if (bk.has_ds) {  // conv3 + downsample + add + ReLU in one dual-source GEMM
+        g = GemmParams();
+        g.amode = A_DUAL; g.A = t2; g.K1 = wd; g.A2 = in; g.B = Wt + bk.c3ds_w_off; g.bias = P + bk.c3ds_b_off;
+        g.act = ACT_RELU; g.C16 = out; g.M = nb * OH * OH; g.N = 4 * wd; g.K = wd + cin;
+        g.H = H; g.W = H; g.C = cin; g.OH = OH; g.OW = OH; g.ks = 1; g.stride = st; g.pad = 0;
+        MEC_TRY(launch_gemm(g, s, &prof, TAG_RESNET_CONV1X1));
+      } else {
+        g = GemmParams();
+        g.A = t2; g.B = Wt + bk.c3.w_off; g.bias = P + bk.c3.b_off; g.R = in; g.act = ACT_RELU; g.C16 = out;
+        g.M = nb * OH * OH; g.N = 4 * wd; g.K = wd;
+        MEC_TRY(launch_gemm(g, s, &prof, TAG_RESNET_CONV1X1));
+      }
+      std::swap(cur, other);
+      H = OH;
+    }
+    return 0;
+  };
+  // Layers 1-2 can run over chunks of g_resnet_chunk images, so that a chunk's activations
+  // stay in the 256-MB Infinity Cache between a block's producer and consumer kernels (off by
+  // default: measured slower, see g_resnet_chunk). Every GEMM row and conv pixel is computed
+  // the same way at any batch split, so the outputs do not depend on the chunk size.
+  constexpr size_t kL12 = 7;  // layer1 (3 blocks) + layer2 (4 blocks)
   f16* cur = X;
   f16* other = Y;
-  H = 56;
-  for (const Bottleneck& bk : blocks) {
-    const int wd = bk.c1.cout, cin = bk.c1.cin, st = bk.c2.stride;
-    const int OH = (H + 2 - 3) / st + 1;
-    GemmParams g;
-    g.A = cur; g.B = Wt + bk.c1.w_off; g.bias = P + bk.c1.b_off; g.act = ACT_RELU; g.C16 = T1;
-    g.M = B * H * H; g.N = wd; g.K = cin;
-    MEC_TRY(launch_gemm(g, s, &prof, TAG_RESNET_CONV1X1));
-    if (!bk.has_ds && g_resnet_fused_tail && wd == 64 && H == 56) {
-      // conv2 + conv3 + residual + ReLU in one kernel (bottleneck.hip)
-      MEC_TRY(prof.begin(TAG_RESNET_CONV3X3, s));
-      MEC_TRY(launch_bneck_tail(T1, cur, Wt + bk.c2.w_off, P + bk.c2.b_off, Wt + bk.c3.w_off, P + bk.c3.b_off, other,
-                                B, H, wd, s));
-      MEC_TRY(prof.end(TAG_RESNET_CONV3X3, s));
-      std::swap(cur, other);
-      continue;
-    }
-    g = GemmParams();
-    g.amode = A_CONV; g.A = T1; g.B = Wt + bk.c2.w_off; g.bias = P + bk.c2.b_off; g.act = ACT_RELU; g.C16 = T2;
-    g.M = B * OH * OH; g.N = wd; g.K = 9 * wd;
-    g.H = H; g.W = H; g.C = wd; g.OH = OH; g.OW = OH; g.ks = 3; g.stride = st; g.pad = 1;
-    MEC_TRY(launch_gemm(g, s, &prof, TAG_RESNET_CONV3X3));
-    if (bk.has_ds) {  // conv3 + downsample + add + ReLU in one dual-source GEMM
-      g = GemmParams();
-      g.amode = A_DUAL; g.A = T2; g.K1 = wd; g.A2 = cur; g.B = Wt + bk.c3ds_w_off; g.bias = P + bk.c3ds_b_off;
-      g.act = ACT_RELU; g.C16 = other; g.M = B * OH * OH; g.N = 4 * wd; g.K = wd + cin;
-      g.H = H; g.W = H; g.C = cin; g.OH = OH; g.OW = OH; g.ks = 1; g.stride = st; g.pad = 0;
-      MEC_TRY(launch_gemm(g, s, &prof, TAG_RESNET_CONV1X1));
-    } else {
-      g = GemmParams();
-      g.A = T2; g.B = Wt + bk.c3.w_off; g.bias = P + bk.c3.b_off; g.R = cur; g.act = ACT_RELU; g.C16 = other;
-      g.M = B * OH * OH; g.N = 4 * wd; g.K = wd;
-      MEC_TRY(launch_gemm(g, s, &prof, TAG_RESNET_CONV1X1));
-    }
-    std::swap(cur, other);
-    H = OH;
+  const int chunk = g_resnet_chunk > 0 ? std::min(g_resnet_chunk, B) : B;
+  for (int i0 = 0; i0 < B; i0 += chunk) {
+    f16* c = X;
+    f16* o = Y;
+    MEC_TRY(run_blocks(0, kL12, i0, std::min(chunk, B - i0), 56, c, o));
+    cur = c;
+    other = o;
   }
+  MEC_TRY(run_blocks(kL12, blocks.size(), 0, B, 28, cur, other));
+  H = 7;
   hipLaunchKernelGGL(avgpool_kernel, dim3(B, 2048 / 256), dim3(256), 0, s, cur, H * H, 2048, pooled);
   MEC_LAUNCH_CHECK();
   // fc[1] Linear(2048,512) + fc[2] ReLU -> the 512-d feature (extract_features)
