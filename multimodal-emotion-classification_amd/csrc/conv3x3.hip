@@ -46,6 +46,7 @@ static_assert(C3_TAIL > 0 && C3_TAIL <= 64, "halo tail must fit one wave");
 // hidden from it, the fragment reads get counted waits. The DMA is ordered only by this
 // kernel's explicit vmcnt waits and barriers (MI355X_MICROARCH.md: nothing else orders a
 // ds_read behind a pending LDS DMA).
+#pragma clang diagnostic ignored "-Winline-asm"  // m0: see pw_chain.hip
 __device__ __forceinline__ void c3_dma(const void* src, uint32_t lds) {
   asm volatile("s_mov_b32 m0, %1\n\ts_nop 0\n\tglobal_load_lds_dwordx4 %0, off" ::"v"(src), "s"(lds) : "memory", "m0");
 }

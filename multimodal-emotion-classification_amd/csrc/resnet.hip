@@ -20,6 +20,7 @@ int g_resnet_fused_tail = 0;
 // --opt resnet_chunk=N): 0 -> 4.23-4.25 ms, 128 -> 4.38, 64 -> 4.44-4.49, 32 -> 5.08: the
 // smaller GEMMs lose more than the cache residency gains, so chunking is off.
 int g_resnet_chunk = 0;
+int g_pw_chain = 1;  // layer1 conv3 + next conv1 seam kernel (pw_chain.hip)
 
 // ----------------------------------------------------------------------------- resize
 // Pillow ImagingResample (bilinear, 8bpc): 22-bit fixed-point taps, horizontal pass into
@@ -549,6 +550,7 @@ int ImageModel::forward_u8(const uint8_t* img, int B, int H, int W, int C, float
   // image-major, so an image range is a pointer offset). cur/other swap once per block.
   auto run_blocks = [&](size_t b0, size_t b1, int i0, int nb, int Hin, f16*& cur, f16*& other) -> int {
     int H = Hin;
+    bool conv1_done = false;  // this block's conv1 already ran in the previous block's seam kernel
     for (size_t bi = b0; bi < b1; ++bi) {
       const Bottleneck& bk = blocks[bi];
       const int wd = bk.c1.cout, cin = bk.c1.cin, st = bk.c2.stride;
@@ -558,9 +560,12 @@ int ImageModel::forward_u8(const uint8_t* img, int B, int H, int W, int C, float
       f16* t1 = T1 + (size_t)i0 * H * H * wd;
       f16* t2 = T2 + (size_t)i0 * OH * OH * wd;
       GemmParams g;
-      g.A = in; g.B = Wt + bk.c1.w_off; g.bias = P + bk.c1.b_off; g.act = ACT_RELU; g.C16 = t1;
-      g.M = nb * H * H; g.N = wd; g.K = cin;
-      MEC_TRY(launch_gemm(g, s, &prof, TAG_RESNET_CONV1X1));
+      if (!conv1_done) {
+        g.A = in; g.B = Wt + bk.c1.w_off; g.bias = P + bk.c1.b_off; g.act = ACT_RELU; g.C16 = t1;
+        g.M = nb * H * H; g.N = wd; g.K = cin;
+        MEC_TRY(launch_gemm(g, s, &prof, TAG_RESNET_CONV1X1));
+      }
+      conv1_done = false;
       if (!bk.has_ds && g_resnet_fused_tail && wd == 64 && H == 56) {
         // conv2 + conv3 + residual + ReLU in one kernel (bottleneck.hip)
         MEC_TRY(prof.begin(TAG_RESNET_CONV3X3, s));
@@ -581,6 +586,19 @@ int ImageModel::forward_u8(const uint8_t* img, int B, int H, int W, int C, float
         g.act = ACT_RELU; g.C16 = out; g.M = nb * OH * OH; g.N = 4 * wd; g.K = wd + cin;
         g.H = H; g.W = H; g.C = cin; g.OH = OH; g.OW = OH; g.ks = 1; g.stride = st; g.pad = 0;
         MEC_TRY(launch_gemm(g, s, &prof, TAG_RESNET_CONV1X1));
+      } else if (g_pw_chain && wd == 64 && OH == 56 && bi + 1 < b1 && blocks[bi + 1].c1.cin == 256 &&
+                 blocks[bi + 1].c1.cout == 64) {
+        // conv3 + residual + ReLU, then the next block's conv1 on the rows just produced
+        // (pw_chain.hip): the block output is not read back from HBM. Layer1 block 2 -> 3
+        // only: 186 us against 164 + 111 us for the two GEMMs. The 256 -> 128 seam into
+        // layer2 (N2 = 128, two tile buffers) measured 297 us against 162 + 132, so it is
+        // not taken.
+        const Bottleneck& nx = blocks[bi + 1];
+        MEC_TRY(prof.begin(TAG_RESNET_CONV1X1, s));
+        MEC_TRY(launch_pw_chain(t2, in, Wt + bk.c3.w_off, P + bk.c3.b_off, Wt + nx.c1.w_off, P + nx.c1.b_off, out,
+                                T1 + (size_t)i0 * OH * OH * nx.c1.cout, nb * OH * OH, nx.c1.cout, s));
+        MEC_TRY(prof.end(TAG_RESNET_CONV1X1, s));
+        conv1_done = true;
       } else {
         g = GemmParams();
         g.A = t2; g.B = Wt + bk.c3.w_off; g.bias = P + bk.c3.b_off; g.R = in; g.act = ACT_RELU; g.C16 = out;

@@ -216,3 +216,25 @@ def test_conv3x3_c64_bit_identical(dev, n):
     assert not torch.isnan(outs[0]).any()
     assert _rel_err(outs[0].float(), ref) < 2e-3
     assert torch.equal(outs[0], outs[1])
+
+
+@pytest.mark.parametrize('B', [3, 37])
+def test_pw_chain_bit_identical(dev, B):
+    """ResNet50 with layer1's conv3 + next-conv1 seam kernel (pw_chain.hip) and with the two
+    GEMMs it replaces: identical features, logits and probabilities (B = 3: 147 tiles, fewer
+    than the CUs; B = 37: 1813 tiles, several per workgroup through every buffer)."""
+    from mec import engine, synthetic as syn
+    lib = _lib.load()
+    enc = engine.ImageEncoder(device=dev)
+    gray = engine.to_device(syn.image_inputs(B, seed=77 + B), dev)
+    outs = []
+    for chain in (1, 0):
+        _lib.check(lib.mec_set_option(b'pw_chain', chain), 'option')
+        try:
+            res = enc.forward(gray)
+            torch.cuda.synchronize()
+            outs.append([t.cpu() for t in res])
+        finally:
+            lib.mec_set_option(b'pw_chain', 1)
+    for a, b in zip(*outs):
+        assert torch.equal(a, b)
