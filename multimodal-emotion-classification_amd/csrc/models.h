@@ -120,6 +120,9 @@ extern int g_pw_chain;
 // layer1 seam: conv3 (64 -> 256) + residual + ReLU, then the next block's conv1 (256 -> N2)
 int launch_pw_chain(const f16* t2, const f16* xin, const f16* w3, const float* b3, const f16* w1, const float* b1,
                     f16* xout, f16* t1, int M, int N2, hipStream_t s);
+// layer1 block 1 -> 2 seam: conv3 + downsample (K = [T2 | X0]) + ReLU, then block 2's conv1
+int launch_pw_chain_dual(const f16* t2, const f16* x0, const f16* w3ds, const float* b3ds, const f16* w1,
+                         const float* b1, f16* xout, f16* t1, int M, hipStream_t s);
 
 extern int g_mbv2_impl;
 

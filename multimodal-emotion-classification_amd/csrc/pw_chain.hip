@@ -249,4 +249,202 @@ int launch_pw_chain(const f16* t2, const f16* xin, const f16* w3, const float* b
   return 0;
 }
 
+// Block 1 -> block 2 seam of layer1: block 1's conv3 and its downsample projection as ONE
+// product over K = [T2 (64) | X0 (64)] (the A_DUAL GEMM's concatenation: bn3(conv3(t)) +
+// bn_ds(conv_ds(x)) = [t | x] . [W3' | Wds']^T + (b3 + bds)) + ReLU, then block 2's conv1
+// (256 -> 64) + ReLU on the rows just produced. No residual rows to stream: the tile's input
+// is 64 x 256 B (T2 | X0), its outputs 64 x 512 B (block output) and 64 x 128 B (conv1).
+// conv3 weights (256 x 128) are split over the waves: wave (h, g) holds output channels
+// 128h .. 128h+127 (8 x 4 A fragments in registers) for tile rows 32g .. 32g+31.
+__global__ __launch_bounds__(256, 1) void pw_chain_dual_kernel(const f16* __restrict__ a, const f16* __restrict__ a2,
+                                                               const f16* __restrict__ w3, const float* __restrict__ b3,
+                                                               const f16* __restrict__ w1, const float* __restrict__ b1,
+                                                               f16* __restrict__ x, f16* __restrict__ t1, int ntiles) {
+  constexpr int N2 = 64, NB = 3, K3 = 128;
+  constexpr int AB = PC_BM * K3 * 2;          // 16 KB of [T2 | X0] rows per tile
+  constexpr int W1B = N2 * PC_N3 * 2;
+  constexpr int DMA_PER_TILE = AB / 16 / 256;  // 4 per lane
+  constexpr int T1C = N2 / 8;
+  constexpr int ST_X = PC_RB / 16 / 256, ST_T1 = PC_BM * T1C / 256;
+  __shared__ __attribute__((aligned(16))) char smem[NB * AB + PC_RB + W1B];
+  __shared__ float sb3[PC_N3], sb1[N2];
+  const int tid = threadIdx.x, lane = tid & 63;
+  const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int l16 = lane & 15, lq = lane >> 4;
+  const int h = wave & 1, g = wave >> 1;
+  const uint32_t lds0 = pc_lds(smem), rb = lds0 + NB * AB, ldsw1 = rb + PC_RB;
+
+#pragma unroll
+  for (int i = 0; i < W1B / 16 / 256; ++i) {
+    const int q = i * 256 + tid, row = q / 32, c = q % 32;
+    const u32x4 v = reinterpret_cast<const u32x4*>(w1)[q];
+    pc_st(ldsw1 + row * 512 + ((c ^ (row & 15)) << 4), v);
+  }
+  for (int i = tid; i < PC_N3; i += 256) sb3[i] = b3[i];
+  if (tid < N2) sb1[tid] = b1[tid];
+  half8 wf[8][4];  // A fragments: co = 128h + 16cf + l16, k = 32s + 8lq .. +7
+#pragma unroll
+  for (int cf = 0; cf < 8; ++cf)
+#pragma unroll
+    for (int s = 0; s < 4; ++s)
+      wf[cf][s] = *reinterpret_cast<const half8*>(w3 + (size_t)(128 * h + 16 * cf + l16) * K3 + 32 * s + 8 * lq);
+#pragma unroll
+  for (int cf = 0; cf < 8; ++cf)
+#pragma unroll
+    for (int s = 0; s < 4; ++s) asm volatile("" : "+v"(wf[cf][s]));
+
+  // one tile's [T2 | X0] rows: 16 chunks per 256-B row, chunk c at c ^ (row & 15)
+  auto issue = [&](int t, int b) {
+    const uint32_t base = lds0 + b * AB;
+    const f16* at = a + (size_t)t * PC_BM * 64;
+    const f16* a2t = a2 + (size_t)t * PC_BM * 64;
+#pragma unroll
+    for (int i = 0; i < DMA_PER_TILE; ++i) {
+      const int q = i * 256 + tid, row = q >> 4, c = (q & 15) ^ (row & 15);
+      const f16* src = c < 8 ? at + row * 64 + c * 8 : a2t + row * 64 + (c - 8) * 8;
+      pc_dma(src, base + (uint32_t)(i * 256 + wave * 64) * 16u);
+    }
+  };
+
+  int t = blockIdx.x;
+  const int G = gridDim.x;
+#pragma unroll
+  for (int k = 0; k < NB - 1; ++k)
+    if (t + k * G < ntiles) issue(t + k * G, k);
+  __syncthreads();
+  int b = 0, prev_stores = 0;
+#pragma unroll 1
+  for (; t < ntiles; t += G) {
+    const bool ahead = t + G < ntiles;
+    if (ahead) {
+      if (prev_stores) asm volatile("s_waitcnt vmcnt(%0)" ::"n"(DMA_PER_TILE + ST_X + ST_T1) : "memory");
+      else asm volatile("s_waitcnt vmcnt(%0)" ::"n"(DMA_PER_TILE) : "memory");
+    } else {
+      if (prev_stores) asm volatile("s_waitcnt vmcnt(%0)" ::"n"(ST_X + ST_T1) : "memory");
+      else asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    }
+    __builtin_amdgcn_s_barrier();  // tile t landed; buffer (b-1) and the staging rows are free
+    if (t + (NB - 1) * G < ntiles) issue(t + (NB - 1) * G, (b + NB - 1) % NB);
+    const uint32_t ab = lds0 + b * AB;
+
+    // ---- conv3 + downsample: out^T[co][px], k = 0..127 (four 32-deep steps)
+    floatx4 acc[2][8];
+#pragma unroll
+    for (int j = 0; j < 2; ++j)
+#pragma unroll
+      for (int cf = 0; cf < 8; ++cf) acc[j][cf] = floatx4{0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+    for (int s = 0; s < 4; ++s) {
+      half8 xf[2];
+#pragma unroll
+      for (int j = 0; j < 2; ++j) {
+        const int rw = 32 * g + 16 * j + l16;
+        xf[j] = pc_ld<half8>(ab + rw * 256 + (((4 * s + lq) ^ (rw & 15)) << 4));
+      }
+#pragma unroll
+      for (int j = 0; j < 2; ++j)
+#pragma unroll
+        for (int cf = 0; cf < 8; ++cf)
+          acc[j][cf] = __builtin_amdgcn_mfma_f32_16x16x32_f16(wf[cf][s], xf[j], acc[j][cf], 0, 0, 0);
+    }
+    // epilogue: (acc + bias) + 0, ReLU, f16 -> staged block-output rows
+#pragma unroll
+    for (int j = 0; j < 2; ++j) {
+      const int rw = 32 * g + 16 * j + l16;
+#pragma unroll
+      for (int cf = 0; cf < 8; ++cf) {
+        const int co = 128 * h + 16 * cf + 4 * lq;
+        half4 hv;
+#pragma unroll
+        for (int e = 0; e < 4; ++e) {
+          float v = acc[j][cf][e] + sb3[co + e];
+          v += 0.f;
+          hv[e] = (f16)fmaxf(v, 0.f);
+        }
+        pc_st(rb + rw * 512 + (((co >> 3) ^ (rw & 15)) << 4) + (lq & 1) * 8, hv);
+      }
+    }
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+    __builtin_amdgcn_s_barrier();
+
+    {
+      f16* xo = x + (size_t)t * PC_BM * PC_N3;
+#pragma unroll
+      for (int i = 0; i < ST_X; ++i) {
+        const int q = i * 256 + tid, rr = q >> 5, c = q & 31;
+        const u32x4 v = pc_ld<u32x4>(rb + rr * 512 + ((c ^ (rr & 15)) << 4));
+        *reinterpret_cast<u32x4*>(xo + (size_t)q * 8) = v;
+      }
+    }
+    // ---- block 2's conv1: wave w -> tile rows 16w .. 16w+15, all 64 output channels
+    const int row = 16 * wave + l16;
+    floatx4 acc1[N2 / 16];
+#pragma unroll
+    for (int cf = 0; cf < N2 / 16; ++cf) acc1[cf] = floatx4{0.f, 0.f, 0.f, 0.f};
+    half8 xf[2], wv[2][N2 / 16];
+    auto rd1 = [&](int s, int k) {
+      const int kc = 4 * s + lq;
+      xf[k] = pc_ld<half8>(rb + row * 512 + ((kc ^ (row & 15)) << 4));
+#pragma unroll
+      for (int cf = 0; cf < N2 / 16; ++cf) {
+        const int co = 16 * cf + l16;
+        wv[k][cf] = pc_ld<half8>(ldsw1 + co * 512 + ((kc ^ (co & 15)) << 4));
+      }
+    };
+    rd1(0, 0);
+#pragma unroll
+    for (int s = 0; s < 8; ++s) {
+      if (s + 1 < 8) rd1(s + 1, (s + 1) & 1);
+#pragma unroll
+      for (int cf = 0; cf < N2 / 16; ++cf)
+        acc1[cf] = __builtin_amdgcn_mfma_f32_16x16x32_f16(wv[s & 1][cf], xf[s & 1], acc1[cf], 0, 0, 0);
+    }
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+    __builtin_amdgcn_s_barrier();  // every wave is done reading the block-output rows
+#pragma unroll
+    for (int cf = 0; cf < N2 / 16; ++cf) {
+      const int co = 16 * cf + 4 * lq;
+      half4 hv;
+#pragma unroll
+      for (int e = 0; e < 4; ++e) {
+        float v = acc1[cf][e] + sb1[co + e];
+        v += 0.f;
+        hv[e] = (f16)fmaxf(v, 0.f);
+      }
+      pc_st(rb + row * (N2 * 2) + (((2 * cf + (lq >> 1)) ^ (row & (T1C - 1))) << 4) + (lq & 1) * 8, hv);
+    }
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+    __builtin_amdgcn_s_barrier();
+    {
+      f16* to = t1 + (size_t)t * PC_BM * N2;
+#pragma unroll
+      for (int i = 0; i < ST_T1; ++i) {
+        const int q = i * 256 + tid, rr = q / T1C, c = q % T1C;
+        const u32x4 v = pc_ld<u32x4>(rb + rr * (N2 * 2) + ((c ^ (rr & (T1C - 1))) << 4));
+        *reinterpret_cast<u32x4*>(to + (size_t)q * 8) = v;
+      }
+    }
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+    prev_stores = 1;
+    b = (b + 1) % NB;
+  }
+}
+
+int launch_pw_chain_dual(const f16* t2, const f16* x0, const f16* w3ds, const float* b3ds, const f16* w1,
+                         const float* b1, f16* xout, f16* t1, int M, hipStream_t s) {
+  MEC_REQUIRE(M > 0 && M % PC_BM == 0, "pw_chain_dual: rows must be a multiple of 64");
+  MEC_REQUIRE(t2 && x0 && w3ds && b3ds && w1 && b1 && xout && t1, "pw_chain_dual: null pointer");
+  static int ncu = 0;
+  if (!ncu) {
+    int dev = 0;
+    MEC_HIP(hipGetDevice(&dev));
+    MEC_HIP(hipDeviceGetAttribute(&ncu, hipDeviceAttributeMultiprocessorCount, dev));
+  }
+  const int ntiles = M / PC_BM;
+  hipLaunchKernelGGL(pw_chain_dual_kernel, dim3(std::min(ntiles, ncu)), dim3(256), 0, s, t2, x0, w3ds, b3ds, w1, b1,
+                     xout, t1, ntiles);
+  MEC_LAUNCH_CHECK();
+  return 0;
+}
+
 }  // namespace mec

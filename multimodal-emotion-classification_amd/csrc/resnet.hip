@@ -580,7 +580,16 @@ int ImageModel::forward_u8(const uint8_t* img, int B, int H, int W, int C, float
       g.M = nb * OH * OH; g.N = wd; g.K = 9 * wd;
       g.H = H; g.W = H; g.C = wd; g.OH = OH; g.OW = OH; g.ks = 3; g.stride = st; g.pad = 1;
       MEC_TRY(launch_gemm(g, s, &prof, TAG_RESNET_CONV3X3));
-      if (bk.has_ds) {  // conv3 + downsample + add + ReLU in one dual-source GEMM
+      if (bk.has_ds && g_pw_chain && wd == 64 && st == 1 && cin == 64 && OH == 56 && bi + 1 < b1 &&
+          blocks[bi + 1].c1.cin == 256 && blocks[bi + 1].c1.cout == 64) {
+        // layer1 block 1: conv3 + downsample + ReLU, then block 2's conv1 (pw_chain.hip)
+        const Bottleneck& nx = blocks[bi + 1];
+        MEC_TRY(prof.begin(TAG_RESNET_CONV1X1, s));
+        MEC_TRY(launch_pw_chain_dual(t2, in, Wt + bk.c3ds_w_off, P + bk.c3ds_b_off, Wt + nx.c1.w_off,
+                                     P + nx.c1.b_off, out, T1 + (size_t)i0 * OH * OH * 64, nb * OH * OH, s));
+        MEC_TRY(prof.end(TAG_RESNET_CONV1X1, s));
+        conv1_done = true;
+      } else if (bk.has_ds) {  // conv3 + downsample + add + ReLU in one dual-source GEMM
         g = GemmParams();
         g.amode = A_DUAL; g.A = t2; g.K1 = wd; g.A2 = in; g.B = Wt + bk.c3ds_w_off; g.bias = P + bk.c3ds_b_off;
         g.act = ACT_RELU; g.C16 = out; g.M = nb * OH * OH; g.N = 4 * wd; g.K = wd + cin;
