@@ -118,18 +118,27 @@ __global__ __launch_bounds__(256) void bert_layernorm_kernel(const float* x, int
 // 81-83). Wave w owns queries 32w..32w+31. S^T = K Q^T is computed so that each lane holds
 // one query's scores (keys in registers): the row softmax is lane-local plus one
 // cross-half shuffle, and the f32 score tile becomes the B operand of O^T = V^T P^T with
-// no LDS round trip (k order permuted; V^T is read to match).
+// no LDS round trip (k order permuted; V^T is read to match). V stays row-major in LDS
+// (one 16-B write per loaded chunk); its V^T fragments come from ds_read_b64_tr_b16, the
+// gfx950 transposed read (4 keys x 16 d per 16-lane group, delivered column-major).
 constexpr int ATT_L = 128;
-constexpr int VT_LD = ATT_L + 4;  // padded row (264 B): conflict-free ds_read_b64
 
 __device__ __forceinline__ int aswz(int row, int kc) { return kc ^ ((row >> 1) & 7); }
+// V rows: chunk kc ^ 4 on rows with bit 1 set, so a 32-lane half's four rows x 64 B of a
+// transposed read cover all 64 banks
+__device__ __forceinline__ int vswz(int row, int kc) { return kc ^ (((row >> 1) & 1) << 2); }
+typedef short s16x4 __attribute__((__vector_size__(4 * sizeof(short))));
+__device__ __forceinline__ half4 lds_tr16(const f16* p) {
+  const s16x4 v = __builtin_amdgcn_ds_read_tr16_b64_v4i16((__attribute__((address_space(3))) s16x4*)p);
+  return __builtin_bit_cast(half4, v);
+}
 
 __global__ __launch_bounds__(256) void bert_attention_kernel(const f16* __restrict__ qkv,
                                                              const int32_t* __restrict__ mask,
                                                              f16* __restrict__ ctx) {
   __shared__ __attribute__((aligned(16))) f16 sQ[ATT_L * BDH];
   __shared__ __attribute__((aligned(16))) f16 sK[ATT_L * BDH];
-  __shared__ __attribute__((aligned(16))) f16 sVt[BDH * VT_LD];
+  __shared__ __attribute__((aligned(16))) f16 sV[ATT_L * BDH];
   __shared__ float sBias[ATT_L];
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   const int b = blockIdx.x / BHEADS, h = blockIdx.x - (blockIdx.x / BHEADS) * BHEADS;
@@ -144,9 +153,7 @@ __global__ __launch_bounds__(256) void bert_attention_kernel(const f16* __restri
     const uint4 v = *reinterpret_cast<const uint4*>(src + 2 * BH);
     *reinterpret_cast<uint4*>(sQ + row * BDH + aswz(row, kc) * 8) = q;
     *reinterpret_cast<uint4*>(sK + row * BDH + aswz(row, kc) * 8) = k;
-    const f16* vv = reinterpret_cast<const f16*>(&v);
-#pragma unroll
-    for (int e = 0; e < 8; ++e) sVt[(kc * 8 + e) * VT_LD + row] = vv[e];
+    *reinterpret_cast<uint4*>(sV + row * BDH + vswz(row, kc) * 8) = v;
   }
   if (tid < ATT_L) sBias[tid] = mask[(size_t)b * ATT_L + tid] ? 0.f : -3.4028234663852886e38f;  // finfo(f32).min
   __syncthreads();
@@ -195,31 +202,48 @@ __global__ __launch_bounds__(256) void bert_attention_kernel(const f16* __restri
   for (int u = 0; u < 2; ++u)
 #pragma unroll
     for (int e = 0; e < 16; ++e) o[u][e] = 0.f;
+  // transposed-read lane roles: lane 4q + p of each 16-lane group addresses key row q of the
+  // block, d columns 4p .. 4p+3; the group's 16 columns are d = 32u + 16 ((lane >> 4) & 1) + ..
+  const int tq = (lane >> 2) & 3, tp = lane & 3, tg = (lane >> 4) & 1;
 #pragma unroll
   for (int st = 0; st < 8; ++st) {
     const int t = st >> 1, sp = st & 1;
     half8 pb;
 #pragma unroll
     for (int j = 0; j < 8; ++j) pb[j] = (f16)(s[t][8 * sp + j] * inv);
-    const int kb = 32 * t + 16 * sp + 4 * lh;  // keys kb..kb+3 (j<4) and kb+8..kb+11 (j>=4)
+    const int kq = 32 * t + 16 * sp + 4 * lh + tq;  // keys kb..kb+3 (j<4) and kb+8..kb+11 (j>=4)
 #pragma unroll
     for (int u = 0; u < 2; ++u) {
-      const int d = 32 * u + lr;
-      const half4 lo = *reinterpret_cast<const half4*>(sVt + d * VT_LD + kb);
-      const half4 hi = *reinterpret_cast<const half4*>(sVt + d * VT_LD + kb + 8);
+      const int dc = 32 * u + 16 * tg + 4 * tp;
+      // lane gets V[kb + 0..3][d = 32u + lr] and V[kb + 8..11][d]
+      const half4 lo = lds_tr16(sV + kq * BDH + vswz(kq, dc >> 3) * 8 + (dc & 7));
+      const half4 hi = lds_tr16(sV + (kq + 8) * BDH + vswz(kq + 8, dc >> 3) * 8 + (dc & 7));
       half8 va = {lo[0], lo[1], lo[2], lo[3], hi[0], hi[1], hi[2], hi[3]};
       o[u] = __builtin_amdgcn_mfma_f32_32x32x16_f16(va, pb, o[u], 0, 0, 0);
     }
   }
-  // o[u][e] = O[query 32w+lr][d = 32u + (e&3) + 8(e>>2) + 4lh]
-  f16* dst = ctx + ((size_t)b * ATT_L + 32 * wave + lr) * BH + h * BDH;
+  // o[u][e] = O[query 32w+lr][d = 32u + (e&3) + 8(e>>2) + 4lh]. Staged through this wave's
+  // own 32 rows of sQ (only this wave read them, in S^T), then written as whole 128-B head
+  // rows: 8-B stores straight from the MFMA layout touch 32 rows per instruction.
+  {
+    f16* so = sQ + (32 * wave + lr) * BDH;
+    const int rq = 32 * wave + lr;
 #pragma unroll
-  for (int u = 0; u < 2; ++u)
+    for (int u = 0; u < 2; ++u)
 #pragma unroll
-    for (int gq = 0; gq < 4; ++gq) {
-      half4 hv = {(f16)o[u][4 * gq + 0], (f16)o[u][4 * gq + 1], (f16)o[u][4 * gq + 2], (f16)o[u][4 * gq + 3]};
-      *reinterpret_cast<half4*>(dst + 32 * u + 8 * gq + 4 * lh) = hv;
-    }
+      for (int gq = 0; gq < 4; ++gq) {
+        half4 hv = {(f16)o[u][4 * gq + 0], (f16)o[u][4 * gq + 1], (f16)o[u][4 * gq + 2], (f16)o[u][4 * gq + 3]};
+        const int d = 32 * u + 8 * gq + 4 * lh;  // 16-B chunk d >> 3 of the row, half (d >> 2) & 1
+        *reinterpret_cast<half4*>(so + aswz(rq, d >> 3) * 8 + (d & 7)) = hv;
+      }
+  }
+  asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");  // wave-local rows: no barrier needed
+#pragma unroll
+  for (int i = 0; i < 4; ++i) {
+    const int c = 64 * i + lane, r = 32 * wave + (c >> 3), kc = c & 7;
+    const uint4 v = *reinterpret_cast<const uint4*>(sQ + r * BDH + aswz(r, kc) * 8);
+    *reinterpret_cast<uint4*>(ctx + ((size_t)b * ATT_L + r) * BH + h * BDH + kc * 8) = v;
+  }
 }
 
 // ----------------------------------------------------------------------------- model
