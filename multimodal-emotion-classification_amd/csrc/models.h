@@ -117,6 +117,7 @@ int launch_bneck_tail(const f16* t1, const f16* x, const f16* w2, const float* b
 extern int g_resnet_fused_tail;
 extern int g_resnet_chunk;
 extern int g_pw_chain;
+extern int g_pw_chain_form;
 // layer1 seam: conv3 (64 -> 256) + residual + ReLU, then the next block's conv1 (256 -> N2)
 int launch_pw_chain(const f16* t2, const f16* xin, const f16* w3, const float* b3, const f16* w1, const float* b1,
                     f16* xout, f16* t1, int M, int N2, hipStream_t s);

@@ -225,6 +225,201 @@ __global__ __launch_bounds__(256, 1) void pw_chain_kernel(const f16* __restrict_
   }
 }
 
+// Register-weight form of the residual seam: both products' weights live in registers, split
+// over the waves: wave (h, g) holds conv3 channels 128h .. 128h+127 (8 x 2 A fragments) and
+// conv1 channels (N2/2)h .. (N2/2)(h+1) - 1 ((N2/32) x 8 A fragments) and computes tile rows
+// 32g .. 32g+31 of both. No weights in LDS, so three 40-KB tile buffers fit at any N2.
+template <int N2>
+__global__ __launch_bounds__(256, 1) void pw_chain2_kernel(const f16* __restrict__ a, const f16* __restrict__ r,
+                                                           const f16* __restrict__ w3, const float* __restrict__ b3,
+                                                           const f16* __restrict__ w1, const float* __restrict__ b1,
+                                                           f16* __restrict__ x, f16* __restrict__ t1, int ntiles) {
+  static_assert(N2 == 64 || N2 == 128, "N2");
+  constexpr int NB = 3;
+  constexpr int DMA_PER_TILE = (PC_AB + PC_RB) / 16 / 256;  // 10 per lane
+  constexpr int T1C = N2 / 8;
+  constexpr int ST_X = PC_RB / 16 / 256, ST_T1 = PC_BM * T1C / 256;
+  constexpr int CF1 = N2 / 32;  // conv1 16-channel fragments per wave
+  __shared__ __attribute__((aligned(16))) char smem[NB * PC_BUF];
+  __shared__ float sb3[PC_N3], sb1[N2];
+  const int tid = threadIdx.x, lane = tid & 63;
+  const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int l16 = lane & 15, lq = lane >> 4;
+  const int h = wave & 1, g = wave >> 1;
+  const uint32_t lds0 = pc_lds(smem);
+
+  for (int i = tid; i < PC_N3; i += 256) sb3[i] = b3[i];
+  if (tid < N2) sb1[tid] = b1[tid];
+  half8 wf3[8][2], wf1[CF1][8];
+#pragma unroll
+  for (int cf = 0; cf < 8; ++cf)
+#pragma unroll
+    for (int s = 0; s < 2; ++s)
+      wf3[cf][s] = *reinterpret_cast<const half8*>(w3 + (size_t)(128 * h + 16 * cf + l16) * PC_K3 + 32 * s + 8 * lq);
+#pragma unroll
+  for (int cf = 0; cf < CF1; ++cf)
+#pragma unroll
+    for (int s = 0; s < 8; ++s)
+      wf1[cf][s] = *reinterpret_cast<const half8*>(w1 + (size_t)((N2 / 2) * h + 16 * cf + l16) * PC_N3 + 32 * s + 8 * lq);
+#pragma unroll
+  for (int cf = 0; cf < 8; ++cf)
+#pragma unroll
+    for (int s = 0; s < 2; ++s) asm volatile("" : "+v"(wf3[cf][s]));
+#pragma unroll
+  for (int cf = 0; cf < CF1; ++cf)
+#pragma unroll
+    for (int s = 0; s < 8; ++s) asm volatile("" : "+v"(wf1[cf][s]));
+
+  auto issue = [&](int t, int b) {
+    const uint32_t base = lds0 + b * PC_BUF;
+    const f16* at = a + (size_t)t * PC_BM * PC_K3;
+    const f16* rt = r + (size_t)t * PC_BM * PC_N3;
+#pragma unroll
+    for (int i = 0; i < PC_AB / 16 / 256; ++i) {
+      const int q = i * 256 + tid, row = q >> 3, c = (q & 7) ^ (row & 7);
+      pc_dma(at + row * PC_K3 + c * 8, base + (uint32_t)(i * 256 + wave * 64) * 16u);
+    }
+#pragma unroll
+    for (int i = 0; i < PC_RB / 16 / 256; ++i) {
+      const int q = i * 256 + tid, row = q >> 5, c = (q & 31) ^ (row & 15);
+      pc_dma(rt + row * PC_N3 + c * 8, base + PC_AB + (uint32_t)(i * 256 + wave * 64) * 16u);
+    }
+  };
+
+  int t = blockIdx.x;
+  const int G = gridDim.x;
+#pragma unroll
+  for (int k = 0; k < NB - 1; ++k)
+    if (t + k * G < ntiles) issue(t + k * G, k);
+  __syncthreads();
+  int b = 0, prev_stores = 0;
+#pragma unroll 1
+  for (; t < ntiles; t += G) {
+    const bool ahead = t + G < ntiles;
+    if (ahead) {
+      if (prev_stores) asm volatile("s_waitcnt vmcnt(%0)" ::"n"(DMA_PER_TILE + ST_X + ST_T1) : "memory");
+      else asm volatile("s_waitcnt vmcnt(%0)" ::"n"(DMA_PER_TILE) : "memory");
+    } else {
+      if (prev_stores) asm volatile("s_waitcnt vmcnt(%0)" ::"n"(ST_X + ST_T1) : "memory");
+      else asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    }
+    __builtin_amdgcn_s_barrier();
+    if (t + (NB - 1) * G < ntiles) issue(t + (NB - 1) * G, (b + NB - 1) % NB);
+    const uint32_t ab = lds0 + b * PC_BUF, rb = ab + PC_AB;
+
+    // ---- conv3 over this wave's 128 channels x 32 rows
+    floatx4 acc[2][8];
+#pragma unroll
+    for (int j = 0; j < 2; ++j)
+#pragma unroll
+      for (int cf = 0; cf < 8; ++cf) acc[j][cf] = floatx4{0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+    for (int s = 0; s < 2; ++s) {
+      half8 xf[2];
+#pragma unroll
+      for (int j = 0; j < 2; ++j) {
+        const int rw = 32 * g + 16 * j + l16;
+        xf[j] = pc_ld<half8>(ab + rw * 128 + (((4 * s + lq) ^ (rw & 7)) << 4));
+      }
+#pragma unroll
+      for (int j = 0; j < 2; ++j)
+#pragma unroll
+        for (int cf = 0; cf < 8; ++cf)
+          acc[j][cf] = __builtin_amdgcn_mfma_f32_16x16x32_f16(wf3[cf][s], xf[j], acc[j][cf], 0, 0, 0);
+    }
+#pragma unroll
+    for (int j = 0; j < 2; ++j) {
+      const int rw = 32 * g + 16 * j + l16;
+#pragma unroll
+      for (int cf = 0; cf < 8; ++cf) {
+        const int co = 128 * h + 16 * cf + 4 * lq;
+        const uint32_t ad = rb + rw * 512 + (((co >> 3) ^ (rw & 15)) << 4) + (lq & 1) * 8;
+        const half4 rv = pc_ld<half4>(ad);
+        half4 hv;
+#pragma unroll
+        for (int e = 0; e < 4; ++e) {
+          float v = acc[j][cf][e] + sb3[co + e];
+          v += (float)rv[e];
+          hv[e] = (f16)fmaxf(v, 0.f);
+        }
+        pc_st(ad, hv);
+      }
+    }
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+    __builtin_amdgcn_s_barrier();
+    {
+      f16* xo = x + (size_t)t * PC_BM * PC_N3;
+#pragma unroll
+      for (int i = 0; i < ST_X; ++i) {
+        const int q = i * 256 + tid, rr = q >> 5, c = q & 31;
+        const u32x4 v = pc_ld<u32x4>(rb + rr * 512 + ((c ^ (rr & 15)) << 4));
+        *reinterpret_cast<u32x4*>(xo + (size_t)q * 8) = v;
+      }
+    }
+    // ---- conv1 over this wave's N2/2 channels x 32 rows (k = 0..255)
+    floatx4 acc1[2][CF1];
+#pragma unroll
+    for (int j = 0; j < 2; ++j)
+#pragma unroll
+      for (int cf = 0; cf < CF1; ++cf) acc1[j][cf] = floatx4{0.f, 0.f, 0.f, 0.f};
+    half8 xf[2][2];
+    auto rd1 = [&](int s, int k) {
+#pragma unroll
+      for (int j = 0; j < 2; ++j) {
+        const int rw = 32 * g + 16 * j + l16;
+        xf[k][j] = pc_ld<half8>(rb + rw * 512 + (((4 * s + lq) ^ (rw & 15)) << 4));
+      }
+    };
+    rd1(0, 0);
+#pragma unroll
+    for (int s = 0; s < 8; ++s) {
+      if (s + 1 < 8) rd1(s + 1, (s + 1) & 1);
+#pragma unroll
+      for (int j = 0; j < 2; ++j)
+#pragma unroll
+        for (int cf = 0; cf < CF1; ++cf)
+          acc1[j][cf] = __builtin_amdgcn_mfma_f32_16x16x32_f16(wf1[cf][s], xf[s & 1][j], acc1[j][cf], 0, 0, 0);
+    }
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+    __builtin_amdgcn_s_barrier();
+#pragma unroll
+    for (int j = 0; j < 2; ++j) {
+      const int rw = 32 * g + 16 * j + l16;
+#pragma unroll
+      for (int cf = 0; cf < CF1; ++cf) {
+        const int co = (N2 / 2) * h + 16 * cf + 4 * lq;
+        half4 hv;
+#pragma unroll
+        for (int e = 0; e < 4; ++e) {
+          float v = acc1[j][cf][e] + sb1[co + e];
+          v += 0.f;
+          hv[e] = (f16)fmaxf(v, 0.f);
+        }
+        pc_st(rb + rw * (N2 * 2) + (((co >> 3) ^ (rw & (T1C - 1))) << 4) + (lq & 1) * 8, hv);
+      }
+    }
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+    __builtin_amdgcn_s_barrier();
+    {
+      f16* to = t1 + (size_t)t * PC_BM * N2;
+#pragma unroll
+      for (int i = 0; i < ST_T1; ++i) {
+        const int q = i * 256 + tid, rr = q / T1C, c = q % T1C;
+        const u32x4 v = pc_ld<u32x4>(rb + rr * (N2 * 2) + ((c ^ (rr & (T1C - 1))) << 4));
+        *reinterpret_cast<u32x4*>(to + (size_t)q * 8) = v;
+      }
+    }
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+    prev_stores = 1;
+    b = (b + 1) % NB;
+  }
+}
+
+// 0: per-N2 default (N2 = 64: LDS-weight form; N2 = 128: register-weight form), 1: LDS-weight
+// form, 2: register-weight form. At N2 = 64 the two forms time the same (3.826 / 3.828 ms for
+// the image encoder); at N2 = 128 the LDS-weight form holds only two tile buffers.
+int g_pw_chain_form = 0;
+
 int launch_pw_chain(const f16* t2, const f16* xin, const f16* w3, const float* b3, const f16* w1, const float* b1,
                     f16* xout, f16* t1, int M, int N2, hipStream_t s) {
   MEC_REQUIRE(M > 0 && M % PC_BM == 0, "pw_chain: rows must be a multiple of 64");
@@ -237,10 +432,15 @@ int launch_pw_chain(const f16* t2, const f16* xin, const f16* w3, const float* b
   }
   const int ntiles = M / PC_BM;
   const dim3 grd(std::min(ntiles, ncu)), blk(256);
-  if (N2 == 64)
+  const int form = g_pw_chain_form ? g_pw_chain_form : (N2 == 64 ? 1 : 2);
+  if (N2 == 64 && form == 1)
     hipLaunchKernelGGL(pw_chain_kernel<64>, grd, blk, 0, s, t2, xin, w3, b3, w1, b1, xout, t1, ntiles);
-  else if (N2 == 128)
+  else if (N2 == 64)
+    hipLaunchKernelGGL(pw_chain2_kernel<64>, grd, blk, 0, s, t2, xin, w3, b3, w1, b1, xout, t1, ntiles);
+  else if (N2 == 128 && form == 1)
     hipLaunchKernelGGL(pw_chain_kernel<128>, grd, blk, 0, s, t2, xin, w3, b3, w1, b1, xout, t1, ntiles);
+  else if (N2 == 128)
+    hipLaunchKernelGGL(pw_chain2_kernel<128>, grd, blk, 0, s, t2, xin, w3, b3, w1, b1, xout, t1, ntiles);
   else {
     set_error("pw_chain: N2 must be 64 or 128");
     return -1;

@@ -20,7 +20,10 @@ int g_resnet_fused_tail = 0;
 // --opt resnet_chunk=N): 0 -> 4.23-4.25 ms, 128 -> 4.38, 64 -> 4.44-4.49, 32 -> 5.08: the
 // smaller GEMMs lose more than the cache residency gains, so chunking is off.
 int g_resnet_chunk = 0;
-int g_pw_chain = 1;  // layer1 conv3 + next conv1 seam kernel (pw_chain.hip)
+// layer1 seam kernels (pw_chain.hip): 0 off, 1 the 256 -> 64 seams (block 1 -> 2, 2 -> 3),
+// 2 also the 256 -> 128 seam into layer2 (block 3 -> layer2 block 1). Image encoder at
+// B = 256 (tools/ab_option.py, one process): 4.03 / 3.83 / 3.75 ms for 0 / 1 / 2.
+int g_pw_chain = 2;
 
 // ----------------------------------------------------------------------------- resize
 // Pillow ImagingResample (bilinear, 8bpc): 22-bit fixed-point taps, horizontal pass into
@@ -596,12 +599,12 @@ int ImageModel::forward_u8(const uint8_t* img, int B, int H, int W, int C, float
         g.H = H; g.W = H; g.C = cin; g.OH = OH; g.OW = OH; g.ks = 1; g.stride = st; g.pad = 0;
         MEC_TRY(launch_gemm(g, s, &prof, TAG_RESNET_CONV1X1));
       } else if (g_pw_chain && wd == 64 && OH == 56 && bi + 1 < b1 && blocks[bi + 1].c1.cin == 256 &&
-                 blocks[bi + 1].c1.cout == 64) {
+                 (blocks[bi + 1].c1.cout == 64 || (g_pw_chain == 2 && blocks[bi + 1].c1.cout == 128))) {
         // conv3 + residual + ReLU, then the next block's conv1 on the rows just produced
-        // (pw_chain.hip): the block output is not read back from HBM. Layer1 block 2 -> 3
-        // only: 186 us against 164 + 111 us for the two GEMMs. The 256 -> 128 seam into
-        // layer2 (N2 = 128, two tile buffers) measured 297 us against 162 + 132, so it is
-        // not taken.
+        // (pw_chain.hip): the block output is not read back from HBM. Block 2 -> 3: 186 us
+        // against 164 + 111 us for the two GEMMs; block 3 -> layer2 (N2 = 128) in the
+        // register-weight form (the LDS-weight form, two tile buffers, took 297 us against
+        // 162 + 132).
         const Bottleneck& nx = blocks[bi + 1];
         MEC_TRY(prof.begin(TAG_RESNET_CONV1X1, s));
         MEC_TRY(launch_pw_chain(t2, in, Wt + bk.c3.w_off, P + bk.c3.b_off, Wt + nx.c1.w_off, P + nx.c1.b_off, out,

@@ -220,21 +220,25 @@ def test_conv3x3_c64_bit_identical(dev, n):
 
 @pytest.mark.parametrize('B', [3, 37])
 def test_pw_chain_bit_identical(dev, B):
-    """ResNet50 with layer1's conv3 + next-conv1 seam kernel (pw_chain.hip) and with the two
-    GEMMs it replaces: identical features, logits and probabilities (B = 3: 147 tiles, fewer
-    than the CUs; B = 37: 1813 tiles, several per workgroup through every buffer)."""
+    """ResNet50 with layer1's seam kernels (pw_chain.hip: block 1 -> 2 dual seam, block 2 -> 3
+    and 3 -> layer2 residual seams, in both weight placements) and with the GEMMs they
+    replace: identical features, logits and probabilities (B = 3: 147 tiles, fewer than the
+    CUs; B = 37: 1813 tiles, several per workgroup through every buffer)."""
     from mec import engine, synthetic as syn
     lib = _lib.load()
     enc = engine.ImageEncoder(device=dev)
     gray = engine.to_device(syn.image_inputs(B, seed=77 + B), dev)
     outs = []
-    for chain in (1, 0):
+    for chain, form in ((0, 0), (1, 0), (2, 0), (2, 1), (2, 2)):
         _lib.check(lib.mec_set_option(b'pw_chain', chain), 'option')
+        _lib.check(lib.mec_set_option(b'pw_chain_form', form), 'option')
         try:
             res = enc.forward(gray)
             torch.cuda.synchronize()
             outs.append([t.cpu() for t in res])
         finally:
             lib.mec_set_option(b'pw_chain', 1)
-    for a, b in zip(*outs):
-        assert torch.equal(a, b)
+            lib.mec_set_option(b'pw_chain_form', 0)
+    for o in outs[1:]:
+        for a, b in zip(o, outs[0]):
+            assert torch.equal(a, b)

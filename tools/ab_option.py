@@ -7,6 +7,7 @@ encoder's outputs under each value are compared with the first value's."""
 import argparse
 import json
 import os
+import time
 import sys
 
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
@@ -19,7 +20,7 @@ from mec import _lib, engine, synthetic as syn  # noqa: E402
 
 def main():
     ap = argparse.ArgumentParser()
-    ap.add_argument('--enc', choices=['text', 'image', 'image_mbv2'], required=True)
+    ap.add_argument('--enc', choices=['text', 'image', 'image_mbv2', 'pipeline'], required=True)
     ap.add_argument('--opt', required=True)
     ap.add_argument('--values', type=int, nargs='+', required=True)
     ap.add_argument('--iters', type=int, default=5)
@@ -27,7 +28,12 @@ def main():
     a = ap.parse_args()
     dev = torch.device('cuda', 0)
     lib = _lib.load()
-    if a.enc == 'text':
+    if a.enc == 'pipeline':  # the bench step: speech + text + image + fusion on three streams
+        m = engine.FusedPipeline(seed=1234, device=dev)
+        ids, mask = syn.text_inputs(256, 128, seed=0)
+        args = tuple(engine.to_device(v, dev) for v in (syn.speech_inputs(256, seed=0), ids, mask,
+                                                        syn.image_inputs(256, seed=0)))
+    elif a.enc == 'text':
         m = engine.TextEncoder(device=dev)
         ids, mask = syn.text_inputs(256, 128, seed=0)
         args = (engine.to_device(ids, dev), engine.to_device(mask, dev))
@@ -35,21 +41,27 @@ def main():
         m = engine.ImageEncoder(device=dev) if a.enc == 'image' else engine.MobileNetImageEncoder(device=dev)
         args = (engine.to_device(syn.image_inputs(256, seed=0), dev),)
     outs, times = {}, {v: [] for v in a.values}
+    def fwd():
+        r = m.forward(*args)
+        if isinstance(r, dict):
+            return [v for v in r.values() if torch.is_tensor(v)]
+        return r if isinstance(r, (tuple, list)) else (r,)
+
     for v in a.values:
         _lib.check(lib.mec_set_option(a.opt.encode(), v), 'set_option')
-        outs[v] = [t.clone() for t in m.forward(*args)]
-        m.forward(*args)
+        outs[v] = [t.clone() for t in fwd()]
+        torch.cuda.synchronize()
+        fwd()
     torch.cuda.synchronize()
     for _ in range(a.rounds):
         for v in a.values:
             lib.mec_set_option(a.opt.encode(), v)
-            e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
-            e0.record()
-            for _ in range(a.iters):
-                m.forward(*args)
-            e1.record()
             torch.cuda.synchronize()
-            times[v].append(e0.elapsed_time(e1) / a.iters)
+            t0 = time.perf_counter()
+            for _ in range(a.iters):
+                fwd()
+            torch.cuda.synchronize()
+            times[v].append((time.perf_counter() - t0) * 1e3 / a.iters)
     base = outs[a.values[0]]
     for v in a.values:
         d = [float((x - y).abs().max()) for x, y in zip(outs[v], base)]
