@@ -20,6 +20,7 @@ int g_resnet_fused_tail = 0;
 // --opt resnet_chunk=N): 0 -> 4.23-4.25 ms, 128 -> 4.38, 64 -> 4.44-4.49, 32 -> 5.08: the
 // smaller GEMMs lose more than the cache residency gains, so chunking is off.
 int g_resnet_chunk = 0;
+int g_stem_debug = 0;  // probe variants of stem_pool_kernel (wrong results), tools/ab_option.py
 // layer1 seam kernels (pw_chain.hip): 0 off, 1 the 256 -> 64 seams (block 1 -> 2, 2 -> 3),
 // 2 also the 256 -> 128 seam into layer2 (block 3 -> layer2 block 1). Image encoder at
 // B = 256 (tools/ab_option.py, one process): 4.03 / 3.83 / 3.75 ms for 0 / 1 / 2.
@@ -183,7 +184,7 @@ __device__ __forceinline__ int sp_swz(int row, int kc) { return kc ^ ((row >> 1)
 // border class of a stem coordinate: 0 -> 0, 1 -> 1, 111 -> 3, else 2 (interior)
 __device__ __forceinline__ int sp_cls(int o) { return o == 0 ? 0 : (o == 1 ? 1 : (o == 111 ? 3 : 2)); }
 
-template <int C>
+template <int C, int DBG = 0>
 __global__ __launch_bounds__(256, 2) void stem_pool_kernel(const uint8_t* __restrict__ img, int ntiles,
                                                         const f16* __restrict__ Wst, const float* __restrict__ bias,
                                                         const float* __restrict__ corr, f16* __restrict__ out) {
@@ -280,7 +281,7 @@ __global__ __launch_bounds__(256, 2) void stem_pool_kernel(const uint8_t* __rest
         const int i = tid + 256 * j, n = i >> 3, kc = i & 7;
         *reinterpret_cast<uint4*>(sB + c * 4096 + n * 64 + sp_swz(n, kc) * 8) = wreg[c][j];
       }
-    if (tile + (int)gridDim.x < ntiles) load_patch(tile + gridDim.x);  // in flight under this tile
+    if (!(DBG & 4) && tile + (int)gridDim.x < ntiles) load_patch(tile + gridDim.x);  // in flight under this tile
     __syncthreads();  // patch copies + weights ready
     floatx16 acc[5];
 #pragma unroll
@@ -288,7 +289,7 @@ __global__ __launch_bounds__(256, 2) void stem_pool_kernel(const uint8_t* __rest
 #pragma unroll
       for (int e = 0; e < 16; ++e) acc[q][e] = 0.f;
 #pragma unroll
-    for (int ch = 0; ch < C; ++ch) {
+    for (int ch = 0; ch < (DBG & 1 ? 0 : C); ++ch) {
       const f16* pc = sP + ch * 4 * SP_COPY;
 #pragma unroll
       for (int s = 0; s < 4; ++s) {  // k step s: kernel rows 2s (lanes 0-31) and 2s+1 (32-63)
@@ -303,58 +304,58 @@ __global__ __launch_bounds__(256, 2) void stem_pool_kernel(const uint8_t* __rest
       }
     }
     __syncthreads();  // all MFMA reads of the patch done before it is reused for stem outputs
-    {  // raw conv + (bias + interior correction) -> sO [m][SO_LD] f16; the accumulators are
-       // transposed (lane = stem pixel, 4 consecutive channels per register quad): 8-B writes
+    {  // conv + bias (+ the border class's correction) -> sO [m][SO_LD] f16, pre-ReLU; stem
+       // pixels outside the 112x112 image -> 0 (every pool window holds an in-image pixel and
+       // the pooled values are post-ReLU >= 0, so this equals torch's -inf pool padding). The
+       // accumulators are transposed (lane = stem pixel, 4 consecutive channels per register
+       // quad): 8-B writes.
       f16* sO = smem;
+      const bool border = ph0 == 0 || pw0 == 0 || ph0 + SP_T == 56 || pw0 + SP_T == 56;
 #pragma unroll
       for (int q = 0; q < 5; ++q) {
         const int m = 32 * (it0 + 2 * q) + lr;
         if (m < SP_S * SP_S) {
+          const int y = m / SP_S, x = m - (m / SP_S) * SP_S;
+          const int oh = sr0 + y, ow = sc0 + x;
+          const bool ok = oh >= 0 && oh < 112 && ow >= 0 && ow < 112;
+          const int cls = sp_cls(oh) * 4 + sp_cls(ow);
 #pragma unroll
           for (int g = 0; g < 4; ++g) {
             const int ch = 32 * jt + 8 * g + 4 * lh;
-            const half4 h = {(f16)(acc[q][4 * g + 0] + sBias[ch + 0]), (f16)(acc[q][4 * g + 1] + sBias[ch + 1]),
-                             (f16)(acc[q][4 * g + 2] + sBias[ch + 2]), (f16)(acc[q][4 * g + 3] + sBias[ch + 3])};
+            float v[4];
+#pragma unroll
+            for (int e = 0; e < 4; ++e) v[e] = acc[q][4 * g + e] + sBias[ch + e];
+            if (border) {  // sCorr holds each class's correction minus the interior one
+#pragma unroll
+              for (int e = 0; e < 4; ++e) v[e] = ok ? v[e] + sCorr[cls * 64 + ch + e] : 0.f;
+            }
+            const half4 h = {(f16)v[0], (f16)v[1], (f16)v[2], (f16)v[3]};
             *reinterpret_cast<half4*>(sO + m * SO_LD + ch) = h;
           }
         }
       }
     }
     __syncthreads();
-  {  // ReLU + border correction + 3x3/2 max; thread -> (pooled pixel, 16 channels)
+  {  // ReLU + 3x3/2 max on packed f16 (max commutes with the monotone f16 rounding).
+     // Thread -> 16-B channel chunk c of pooled pixel (px, py), py = wave + 4 pass; the lane
+     // bits are dealt to (c, px) so that every ds_read_b128 lane group hits 16 distinct bank
+     // slots on the 144-B stem-output rows (3x fewer LDS cycles than 16 channels per thread).
     const f16* sO = smem;
-    const int pp = tid >> 2, c0 = (tid & 3) * 16;  // pooled pixel, first channel
-    const int py = pp >> 3, pxx = pp & 7;
-    const bool border = ph0 == 0 || pw0 == 0 || ph0 + SP_T == 56 || pw0 + SP_T == 56;
-    float m[16];
+    const int c = ((lane >> 2) & 1) | (((lane >> 3) & 1) << 1) | ((lane & 1) << 2);
+    const int pxx = ((lane >> 5) & 1) | (((lane >> 4) & 1) << 1) | (((lane >> 1) & 1) << 2);
 #pragma unroll
-    for (int c = 0; c < 16; ++c) m[c] = 0.f;  // post-ReLU values are >= 0
+    for (int pass = 0; pass < 2; ++pass) {
+      const int py = wave + 4 * pass;
+      half8 m0 = {0, 0, 0, 0, 0, 0, 0, 0};  // post-ReLU values are >= 0
 #pragma unroll
-    for (int dy = 0; dy < 3; ++dy)
+      for (int dy = 0; dy < (DBG & 2 ? 0 : 3); ++dy)
 #pragma unroll
-      for (int dx = 0; dx < 3; ++dx) {
-        const int oh = sr0 + 2 * py + dy, ow = sc0 + 2 * pxx + dx;
-        const int mm = (2 * py + dy) * SP_S + 2 * pxx + dx;
-        const half8 a0 = *reinterpret_cast<const half8*>(sO + mm * SO_LD + c0);
-        const half8 a1 = *reinterpret_cast<const half8*>(sO + mm * SO_LD + c0 + 8);
-        float v[16];
-#pragma unroll
-        for (int c = 0; c < 8; ++c) { v[c] = (float)a0[c]; v[8 + c] = (float)a1[c]; }
-        if (border) {
-          const bool ok = oh >= 0 && oh < 112 && ow >= 0 && ow < 112;
-          const int cls = sp_cls(oh) * 4 + sp_cls(ow);
-#pragma unroll
-          for (int c = 0; c < 16; ++c) v[c] = ok ? v[c] + sCorr[cls * 64 + c0 + c] : 0.f;  // sCorr = deltas now
+        for (int dx = 0; dx < 3; ++dx) {
+          const int mm = (2 * py + dy) * SP_S + 2 * pxx + dx;
+          m0 = __builtin_elementwise_max(m0, *reinterpret_cast<const half8*>(sO + mm * SO_LD + 8 * c));
         }
-#pragma unroll
-        for (int c = 0; c < 16; ++c) m[c] = fmaxf(m[c], v[c]);
-      }
-    half8 o0, o1;
-#pragma unroll
-    for (int c = 0; c < 8; ++c) { o0[c] = (f16)m[c]; o1[c] = (f16)m[8 + c]; }
-    f16* o = out + (((size_t)b * 56 + ph0 + py) * 56 + pw0 + pxx) * 64 + c0;
-    *reinterpret_cast<half8*>(o) = o0;
-    *reinterpret_cast<half8*>(o + 8) = o1;
+      *reinterpret_cast<half8*>(out + (((size_t)b * 56 + ph0 + py) * 56 + pw0 + pxx) * 64 + 8 * c) = m0;
+    }
   }
   }
 }
@@ -540,12 +541,21 @@ int ImageModel::forward_u8(const uint8_t* img, int B, int H, int W, int C, float
       MEC_HIP(hipDeviceGetAttribute(&ncu, hipDeviceAttributeMultiprocessorCount, dev));
     }
     const int ntiles = B * 49;  // two resident workgroups per CU (VGPR-bound)
+    const dim3 sg(std::min(ntiles, 2 * ncu)), sb(256);
+    const f16* sw = Wt + st.w_off;
+    const float *sbias = P + st.b_off, *scorr = P + stem_corr_off;
     if (C == 3)
-      hipLaunchKernelGGL(stem_pool_kernel<3>, dim3(std::min(ntiles, 2 * ncu)), dim3(256), 0, s, stem_in, ntiles,
-                         Wt + st.w_off, P + st.b_off, P + stem_corr_off, X);
+      hipLaunchKernelGGL(stem_pool_kernel<3>, sg, sb, 0, s, stem_in, ntiles, sw, sbias, scorr, X);
+    else if (g_stem_debug == 0)
+      hipLaunchKernelGGL(stem_pool_kernel<1>, sg, sb, 0, s, stem_in, ntiles, sw, sbias, scorr, X);
+    else if (g_stem_debug == 1)  // probe builds (wrong results): no MFMA / no pool / no prefetch
+      hipLaunchKernelGGL((stem_pool_kernel<1, 1>), sg, sb, 0, s, stem_in, ntiles, sw, sbias, scorr, X);
+    else if (g_stem_debug == 2)
+      hipLaunchKernelGGL((stem_pool_kernel<1, 2>), sg, sb, 0, s, stem_in, ntiles, sw, sbias, scorr, X);
+    else if (g_stem_debug == 4)
+      hipLaunchKernelGGL((stem_pool_kernel<1, 4>), sg, sb, 0, s, stem_in, ntiles, sw, sbias, scorr, X);
     else
-      hipLaunchKernelGGL(stem_pool_kernel<1>, dim3(std::min(ntiles, 2 * ncu)), dim3(256), 0, s, stem_in, ntiles,
-                         Wt + st.w_off, P + st.b_off, P + stem_corr_off, X);
+      hipLaunchKernelGGL((stem_pool_kernel<1, 7>), sg, sb, 0, s, stem_in, ntiles, sw, sbias, scorr, X);
     MEC_LAUNCH_CHECK();
     MEC_TRY(prof.end(TAG_RESNET_STEM, s));
   }
