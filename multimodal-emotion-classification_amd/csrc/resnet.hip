@@ -193,12 +193,15 @@ __global__ __launch_bounds__(256, 2) void stem_pool_kernel(const uint8_t* __rest
   // registers while the current tile computes.
   constexpr int PATCH = C * 4 * SP_COPY;
   constexpr int SOH = SP_S * SP_S * SO_LD;  // live stem-output rows only
-  constexpr int SMEM = (PATCH + C * 64 * 64 > SOH) ? PATCH + C * 64 * 64 : SOH;
-  __shared__ __attribute__((aligned(16))) f16 smem[SMEM];  // patch copies + weights, later stem outputs
+  constexpr int SMEM = PATCH + C * 64 * 64 + SOH;
+  // patch copies | weights (written once) | stem outputs: separate regions, so the weights
+  // stay resident and the epilogue needs no barrier behind the MFMA reads of the patch
+  __shared__ __attribute__((aligned(16))) f16 smem[SMEM];
   __shared__ float sCorr[16 * 64];  // border-class correction minus the interior one
   __shared__ float sBias[64];       // bias + interior correction
   f16* sP = smem;
   f16* sB = smem + PATCH;
+  f16* const sOut = smem + PATCH + C * 64 * 64;
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   uint4 wreg[C][2];
 #pragma unroll
@@ -214,6 +217,13 @@ __global__ __launch_bounds__(256, 2) void stem_pool_kernel(const uint8_t* __rest
     sCorr[i] = corr[i] - corr[(2 * 4 + 2) * 64 + (i & 63)];
   }
   if (tid < 64) sBias[tid] = bias[tid] + corr[(2 * 4 + 2) * 64 + tid];
+#pragma unroll
+  for (int c = 0; c < C; ++c)
+#pragma unroll
+    for (int j = 0; j < 2; ++j) {
+      const int i = tid + 256 * j, n = i >> 3, kc = i & 7;
+      *reinterpret_cast<uint4*>(sB + c * 4096 + n * 64 + sp_swz(n, kc) * 8) = wreg[c][j];
+    }
 
   // patch loader: thread -> a fixed pixel pair (cols 2k, 2k+1) walking rows r0, r0+11, ...;
   // each shifted copy then gets one whole dword per pair (shifts are even)
@@ -263,23 +273,17 @@ __global__ __launch_bounds__(256, 2) void stem_pool_kernel(const uint8_t* __rest
 #pragma unroll
       for (int j = 0; j < ITER; ++j) {
         const int pr = r0 + RSTEP * j;
-        if (act && pr < SP_R) {
-          typedef _Float16 h2 __attribute__((ext_vector_type(2)));
-          const h2 v = {(f16)(float)px[c][j][0], (f16)(float)px[c][j][1]};
+        const bool rok = act && pr < SP_R;
+        typedef _Float16 h2 __attribute__((ext_vector_type(2)));
+        const h2 v = {(f16)(float)px[c][j][0], (f16)(float)px[c][j][1]};
 #pragma unroll
-          for (int sh = 0; sh < 4; ++sh) {  // copy sh holds patch[pr][jj + 2 sh]
-            const int jj = 2 * k - 2 * sh;
-            if (jj >= 0 && jj < SP_CW)
-              *reinterpret_cast<h2*>(sP + (c * 4 + sh) * SP_COPY + pr * SP_CW + jj) = v;
-          }
+        for (int sh = 0; sh < 4; ++sh) {  // copy sh holds patch[pr][jj + 2 sh]
+          // branch-free: writes that fall outside the copy go to its 32-half pad tail
+          const int jj = 2 * k - 2 * sh;
+          const bool ok = rok && jj >= 0 && jj < SP_CW;
+          const int off = ok ? pr * SP_CW + jj : SP_R * SP_CW + 2 * (k & 15);
+          *reinterpret_cast<h2*>(sP + (c * 4 + sh) * SP_COPY + off) = v;
         }
-      }
-#pragma unroll
-    for (int c = 0; c < C; ++c)
-#pragma unroll
-      for (int j = 0; j < 2; ++j) {
-        const int i = tid + 256 * j, n = i >> 3, kc = i & 7;
-        *reinterpret_cast<uint4*>(sB + c * 4096 + n * 64 + sp_swz(n, kc) * 8) = wreg[c][j];
       }
     if (!(DBG & 4) && tile + (int)gridDim.x < ntiles) load_patch(tile + gridDim.x);  // in flight under this tile
     __syncthreads();  // patch copies + weights ready
@@ -303,13 +307,12 @@ __global__ __launch_bounds__(256, 2) void stem_pool_kernel(const uint8_t* __rest
         }
       }
     }
-    __syncthreads();  // all MFMA reads of the patch done before it is reused for stem outputs
     {  // conv + bias (+ the border class's correction) -> sO [m][SO_LD] f16, pre-ReLU; stem
        // pixels outside the 112x112 image -> 0 (every pool window holds an in-image pixel and
        // the pooled values are post-ReLU >= 0, so this equals torch's -inf pool padding). The
        // accumulators are transposed (lane = stem pixel, 4 consecutive channels per register
        // quad): 8-B writes.
-      f16* sO = smem;
+      f16* sO = sOut;
       const bool border = ph0 == 0 || pw0 == 0 || ph0 + SP_T == 56 || pw0 + SP_T == 56;
 #pragma unroll
       for (int q = 0; q < 5; ++q) {
@@ -340,7 +343,7 @@ __global__ __launch_bounds__(256, 2) void stem_pool_kernel(const uint8_t* __rest
      // Thread -> 16-B channel chunk c of pooled pixel (px, py), py = wave + 4 pass; the lane
      // bits are dealt to (c, px) so that every ds_read_b128 lane group hits 16 distinct bank
      // slots on the 144-B stem-output rows (3x fewer LDS cycles than 16 channels per thread).
-    const f16* sO = smem;
+    const f16* sO = sOut;
     const int c = ((lane >> 2) & 1) | (((lane >> 3) & 1) << 1) | ((lane & 1) << 2);
     const int pxx = ((lane >> 5) & 1) | (((lane >> 4) & 1) << 1) | (((lane >> 1) & 1) << 2);
 #pragma unroll
