@@ -133,31 +133,11 @@ __device__ __forceinline__ half4 lds_tr16(const f16* p) {
   return __builtin_bit_cast(half4, v);
 }
 
-__global__ __launch_bounds__(256) void bert_attention_kernel(const f16* __restrict__ qkv,
-                                                             const int32_t* __restrict__ mask,
-                                                             f16* __restrict__ ctx) {
-  __shared__ __attribute__((aligned(16))) f16 sQ[ATT_L * BDH];
-  __shared__ __attribute__((aligned(16))) f16 sK[ATT_L * BDH];
-  __shared__ __attribute__((aligned(16))) f16 sV[ATT_L * BDH];
-  __shared__ float sBias[ATT_L];
-  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
-  const int b = blockIdx.x / BHEADS, h = blockIdx.x - (blockIdx.x / BHEADS) * BHEADS;
-  const f16* base = qkv + (size_t)b * ATT_L * (3 * BH) + h * BDH;
-#pragma unroll
-  for (int i = 0; i < 4; ++i) {
-    const int c = tid + 256 * i;
-    const int row = c >> 3, kc = c & 7;
-    const f16* src = base + (size_t)row * (3 * BH) + kc * 8;
-    const uint4 q = *reinterpret_cast<const uint4*>(src);
-    const uint4 k = *reinterpret_cast<const uint4*>(src + BH);
-    const uint4 v = *reinterpret_cast<const uint4*>(src + 2 * BH);
-    *reinterpret_cast<uint4*>(sQ + row * BDH + aswz(row, kc) * 8) = q;
-    *reinterpret_cast<uint4*>(sK + row * BDH + aswz(row, kc) * 8) = k;
-    *reinterpret_cast<uint4*>(sV + row * BDH + vswz(row, kc) * 8) = v;
-  }
-  if (tid < ATT_L) sBias[tid] = mask[(size_t)b * ATT_L + tid] ? 0.f : -3.4028234663852886e38f;  // finfo(f32).min
-  __syncthreads();
-
+// One (sequence, head) on 4 waves (wave w: queries 32w .. 32w+31) from Q, K (aswz rows)
+// and V (vswz rows) in LDS; sQ's rows are reused to stage the output, which is written to
+// ctx_row0 (query row 0 of this sequence and head, row stride BH).
+__device__ __forceinline__ void attn_head(f16* sQ, const f16* sK, const f16* sV, const float* sBias, int wave,
+                                          int lane, f16* ctx_row0) {
   const int lr = lane & 31, lh = lane >> 5;
   floatx16 s[4];
 #pragma unroll
@@ -242,9 +222,177 @@ __global__ __launch_bounds__(256) void bert_attention_kernel(const f16* __restri
   for (int i = 0; i < 4; ++i) {
     const int c = 64 * i + lane, r = 32 * wave + (c >> 3), kc = c & 7;
     const uint4 v = *reinterpret_cast<const uint4*>(sQ + r * BDH + aswz(r, kc) * 8);
-    *reinterpret_cast<uint4*>(ctx + ((size_t)b * ATT_L + r) * BH + h * BDH + kc * 8) = v;
+    *reinterpret_cast<uint4*>(ctx_row0 + (size_t)r * BH + kc * 8) = v;
   }
 }
+
+__global__ __launch_bounds__(256) void bert_attention_kernel(const f16* __restrict__ qkv,
+                                                             const int32_t* __restrict__ mask,
+                                                             f16* __restrict__ ctx) {
+  __shared__ __attribute__((aligned(16))) f16 sQ[ATT_L * BDH];
+  __shared__ __attribute__((aligned(16))) f16 sK[ATT_L * BDH];
+  __shared__ __attribute__((aligned(16))) f16 sV[ATT_L * BDH];
+  __shared__ float sBias[ATT_L];
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int b = blockIdx.x / BHEADS, h = blockIdx.x - (blockIdx.x / BHEADS) * BHEADS;
+  const f16* base = qkv + (size_t)b * ATT_L * (3 * BH) + h * BDH;
+#pragma unroll
+  for (int i = 0; i < 4; ++i) {
+    const int c = tid + 256 * i;
+    const int row = c >> 3, kc = c & 7;
+    const f16* src = base + (size_t)row * (3 * BH) + kc * 8;
+    const uint4 q = *reinterpret_cast<const uint4*>(src);
+    const uint4 k = *reinterpret_cast<const uint4*>(src + BH);
+    const uint4 v = *reinterpret_cast<const uint4*>(src + 2 * BH);
+    *reinterpret_cast<uint4*>(sQ + row * BDH + aswz(row, kc) * 8) = q;
+    *reinterpret_cast<uint4*>(sK + row * BDH + aswz(row, kc) * 8) = k;
+    *reinterpret_cast<uint4*>(sV + row * BDH + vswz(row, kc) * 8) = v;
+  }
+  if (tid < ATT_L) sBias[tid] = mask[(size_t)b * ATT_L + tid] ? 0.f : -3.4028234663852886e38f;  // finfo(f32).min
+  __syncthreads();
+  attn_head(sQ, sK, sV, sBias, wave, lane, ctx + (size_t)b * ATT_L * BH + h * BDH);
+}
+
+// ----------------------------------------------------------------------------- QKV + attention
+// The QKV projection and the attention of one (sequence, head pair) in one workgroup, so Q,
+// K and V never go through HBM (unfused: a 151-MB write by the QKV GEMM and the same read by
+// the attention kernel per layer at B = 256):
+//   * a 128 (tokens) x 384 (Q | K | V of heads 2hp, 2hp+1) x 768 GEMM tile, 8 waves (2 x 4,
+//     wave tile 64 x 96), v_mfma_f32_16x16x32_f16 computed transposed (out^T = W . X^T, so a
+//     lane holds 4 consecutive features of one token), A and B staged HBM -> LDS by
+//     global_load_lds_dwordx4 in two 64-KB stages (128-B rows, kc ^ ((row>>1)&7) swizzle);
+//   * the epilogue adds the bias exactly as the GEMM epilogue does ((acc + b) + 0, f16) and
+//     writes Q, K, V straight into the attention's LDS images (aswz / vswz rows);
+//   * each 4-wave half then runs attn_head on one head.
+// Same k order as the QKV GEMM tiles and the same attention code: ctx is bit-identical to
+// the unfused pair (tests/test_gpu_parity.py::test_text_qkv_attn_bit_identical).
+constexpr int QA_BM = 128, QA_BN = 384, QA_BK = 64, QA_NK = BH / QA_BK;
+constexpr int QA_STAGE = (QA_BM + QA_BN) * QA_BK;  // halfs per stage (64 KB)
+
+__global__ __launch_bounds__(512, 1) void bert_qkv_attn_kernel(const f16* __restrict__ h16,
+                                                               const f16* __restrict__ wqkv,
+                                                               const float* __restrict__ bqkv,
+                                                               const int32_t* __restrict__ mask,
+                                                               f16* __restrict__ ctx, int nseq) {
+  __shared__ __attribute__((aligned(16))) f16 smem[2 * QA_STAGE];  // 2 GEMM stages, then Q/K/V images
+  __shared__ float sBias[ATT_L];
+  typedef __attribute__((address_space(3))) void* lds_p;
+  const int tid = threadIdx.x, lane = tid & 63;
+  const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int wm = wave >> 2, wn = wave & 3;
+  const int l16 = lane & 15, lq = lane >> 4;
+  // XCD-aware bijective remap: the 6 head pairs of a sequence (which share its 192-KB token
+  // rows) run on one XCD's L2
+  const int nwg = nseq * 6;
+  int bid = blockIdx.x;
+  {
+    const int xcd = bid & 7, q = nwg >> 3, r = nwg & 7;
+    bid = (xcd < r ? xcd * (q + 1) : r * (q + 1) + (xcd - r) * q) + (bid >> 3);
+  }
+  const int b = bid / 6, hp = bid - (bid / 6) * 6;
+
+  // stage loader: LDS row R < 128 = token row R of the sequence; R >= 128 = W row
+  // (R-128)/128 * 768 + hp*128 + (R-128)%128 (Q, K, V blocks of the two heads)
+  const int lrow = lane >> 3, pch = lane & 7;
+  const f16* src0[8];
+#pragma unroll
+  for (int it = 0; it < 8; ++it) {
+    const int R = (it * 8 + wave) * 8 + lrow;  // 64 rows per pass of the 8 waves
+    const int c = pch ^ ((R >> 1) & 7);
+    if (R < QA_BM) {
+      src0[it] = h16 + ((size_t)b * ATT_L + R) * BH + c * 8;
+    } else {
+      const int n = R - QA_BM, seg = n >> 7, j = n & 127;
+      src0[it] = wqkv + ((size_t)seg * BH + hp * 128 + j) * BH + c * 8;
+    }
+  }
+  auto issue = [&](int kt, int st) {
+    f16* base = smem + st * QA_STAGE;
+#pragma unroll
+    for (int it = 0; it < 8; ++it)
+      __builtin_amdgcn_global_load_lds((const void*)(src0[it] + kt * QA_BK), (lds_p)(base + (it * 8 + wave) * 8 * QA_BK),
+                                       16, 0, 0);
+  };
+
+  floatx4 acc[4][6];
+#pragma unroll
+  for (int i = 0; i < 4; ++i)
+#pragma unroll
+    for (int j = 0; j < 6; ++j) acc[i][j] = floatx4{0.f, 0.f, 0.f, 0.f};
+  issue(0, 0);
+  issue(1, 1);
+#pragma unroll 1
+  for (int kt = 0; kt < QA_NK; ++kt) {
+    if (kt + 1 < QA_NK)
+      asm volatile("s_waitcnt vmcnt(8)" ::: "memory");
+    else
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    __builtin_amdgcn_s_barrier();  // stage kt landed for every wave
+    const f16* sA = smem + (kt & 1) * QA_STAGE;
+    const f16* sB = sA + QA_BM * QA_BK;
+    half8 af[2][4], bf[2][6];
+#pragma unroll
+    for (int s2 = 0; s2 < 2; ++s2) {
+      const int kc = 4 * s2 + lq;
+#pragma unroll
+      for (int i = 0; i < 4; ++i) {
+        const int r = 64 * wm + 16 * i + l16;
+        af[s2][i] = *reinterpret_cast<const half8*>(sA + r * QA_BK + (kc ^ ((r >> 1) & 7)) * 8);
+      }
+#pragma unroll
+      for (int j = 0; j < 6; ++j) {
+        const int r = 96 * wn + 16 * j + l16;  // B row (feature); its LDS row is QA_BM + r
+        const int rr = QA_BM + r;
+        bf[s2][j] = *reinterpret_cast<const half8*>(sB + r * QA_BK + (kc ^ ((rr >> 1) & 7)) * 8);
+      }
+    }
+    // the stage is free as soon as every wave holds its fragments: restage it for kt + 2
+    // BEFORE the MFMAs, so the DMA has two K steps of MFMAs to land
+    __builtin_amdgcn_sched_barrier(0);
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+    __builtin_amdgcn_s_barrier();  // every wave is done reading stage kt
+    if (kt + 2 < QA_NK) issue(kt + 2, kt & 1);
+    __builtin_amdgcn_sched_barrier(0);
+#pragma unroll
+    for (int s2 = 0; s2 < 2; ++s2)
+#pragma unroll
+      for (int i = 0; i < 4; ++i)
+#pragma unroll
+        for (int j = 0; j < 6; ++j)
+          acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_f16(bf[s2][j], af[s2][i], acc[i][j], 0, 0, 0);
+  }
+
+  // ---- epilogue: (acc + bias) + 0 -> f16 -> the attention's Q / K / V LDS images
+  if (tid < ATT_L) sBias[tid] = mask[(size_t)b * ATT_L + tid] ? 0.f : -3.4028234663852886e38f;  // finfo(f32).min
+  f16* img = smem;  // [Q0 Q1 K0 K1 V0 V1], each [128][64]
+#pragma unroll
+  for (int j = 0; j < 6; ++j) {
+    const int n = 96 * wn + 16 * j + 4 * lq;  // features n .. n+3 (one 128-block, one head)
+    const int seg = n >> 7, hh = (n >> 6) & 1, d = n & 63;
+    const float4 bv = *reinterpret_cast<const float4*>(bqkv + seg * BH + hp * 128 + (n & 127));
+    const float bb[4] = {bv.x, bv.y, bv.z, bv.w};
+    f16* dst = img + (seg * 2 + hh) * (ATT_L * BDH);
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+      const int m = 64 * wm + 16 * i + l16;  // token
+      half4 hv;
+#pragma unroll
+      for (int e = 0; e < 4; ++e) {
+        float v = acc[i][j][e] + bb[e];
+        v += 0.f;
+        hv[e] = (f16)v;
+      }
+      const int ch = seg == 2 ? vswz(m, d >> 3) : aswz(m, d >> 3);
+      *reinterpret_cast<half4*>(dst + m * BDH + ch * 8 + (d & 7)) = hv;
+    }
+  }
+  __syncthreads();
+  const int hh = wave >> 2;
+  attn_head(img + hh * (ATT_L * BDH), img + (2 + hh) * (ATT_L * BDH), img + (4 + hh) * (ATT_L * BDH), sBias,
+            wave & 3, lane, ctx + (size_t)b * ATT_L * BH + (2 * hp + hh) * BDH);
+}
+
+int g_bert_qkv_attn = 1;  // fused QKV projection + attention (0: QKV GEMM, then attention kernel)
 
 // ----------------------------------------------------------------------------- model
 // prm layout per layer (floats): bqkv 2304 | bo 768 | ln1g 768 | ln1b 768 | bi 3072 | bo2 768 |
@@ -362,12 +510,19 @@ int TextModel::forward(const int32_t* ids, const int32_t* mask, int B, int L, fl
     const float *bqkv = pl, *bo = pl + 2304, *g1 = pl + 3072, *b1 = pl + 3840, *bi = pl + 4608,
                 *bo2 = pl + 7680, *g2 = pl + 8448, *b2 = pl + 9216;
     GemmParams g;
-    g.A = h16; g.B = wqkv; g.bias = bqkv; g.C16 = big16; g.M = M; g.N = 2304; g.K = BH;
-    MEC_TRY(launch_gemm(g, s, &prof, TAG_BERT_QKV));
-    MEC_TRY(prof.begin(TAG_BERT_ATTN, s));
-    hipLaunchKernelGGL(bert_attention_kernel, dim3(B * BHEADS), dim3(256), 0, s, big16, mask, ctx16);
-    MEC_LAUNCH_CHECK();
-    MEC_TRY(prof.end(TAG_BERT_ATTN, s));
+    if (g_bert_qkv_attn) {
+      MEC_TRY(prof.begin(TAG_BERT_ATTN, s));
+      hipLaunchKernelGGL(bert_qkv_attn_kernel, dim3(B * 6), dim3(512), 0, s, h16, wqkv, bqkv, mask, ctx16, B);
+      MEC_LAUNCH_CHECK();
+      MEC_TRY(prof.end(TAG_BERT_ATTN, s));
+    } else {
+      g.A = h16; g.B = wqkv; g.bias = bqkv; g.C16 = big16; g.M = M; g.N = 2304; g.K = BH;
+      MEC_TRY(launch_gemm(g, s, &prof, TAG_BERT_QKV));
+      MEC_TRY(prof.begin(TAG_BERT_ATTN, s));
+      hipLaunchKernelGGL(bert_attention_kernel, dim3(B * BHEADS), dim3(256), 0, s, big16, mask, ctx16);
+      MEC_LAUNCH_CHECK();
+      MEC_TRY(prof.end(TAG_BERT_ATTN, s));
+    }
     const bool first = l == 0, last = l == BLAYERS - 1;
     const float* pg2 = P + PRM_LAYER * (l - 1) + 8448;  // previous layer's LN2 (g2, b2)
     // f32 stream ping-pong: O-proj reads h32 and writes t32, FFN2 reads t32 and writes h32,

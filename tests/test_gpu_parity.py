@@ -163,3 +163,23 @@ def test_bad_shapes_raise(models, dev):
     with pytest.raises(ValueError):
         ids = torch.zeros(2, 64, dtype=torch.int32, device=dev)
         models['text'].forward(ids, ids)
+
+
+@pytest.mark.parametrize('B', [1, 3, 9])
+def test_text_qkv_attn_bit_identical(models, dev, B):
+    """BERT with the fused QKV-projection + attention kernel and with the QKV GEMM followed by
+    the attention kernel: identical CLS features, logits and probabilities (B = 9: 54
+    workgroups over the XCD remap with a remainder)."""
+    from mec import _lib
+    lib = _lib.load()
+    ids, mask = syn.text_inputs(B, 128, seed=300 + B, ragged=True)
+    args = (engine.to_device(ids, dev), engine.to_device(mask, dev))
+    outs = []
+    for fused in (1, 0):
+        _lib.check(lib.mec_set_option(b'bert_qkv_attn', fused), 'option')
+        try:
+            outs.append(_np(models['text'].forward(*args)))
+        finally:
+            lib.mec_set_option(b'bert_qkv_attn', 1)
+    for a, b in zip(*outs):
+        np.testing.assert_array_equal(a, b)
