@@ -102,8 +102,19 @@ int mec_gemm_f16(const void* A, const void* B, const float* bias, const void* R,
 int mec_conv_f16(const void* x, const void* w, const float* bias, const void* R, void* y, int n, int H, int W,
                  int C, int Cout, int ks, int stride, int pad, int act, void* stream);
 
-/* Process-wide tuning knobs (A/B benchmarking): "gemm_impl" 1|2, "gemm_bn" 0|64|128|256,
- * "gemm_autotune" 0|1 (time each GEMM tile width on the first launch of a shape; default 1). */
+/* Process-wide tuning knobs (A/B benchmarking; defaults in brackets). Every pair of
+ * settings of one knob gives bit-identical outputs, except the *_debug probe builds, which
+ * skip work to time its parts and return wrong results.
+ *   "gemm_impl" 1|[2]      register-staged / glds GEMM engine
+ *   "gemm_bn" [0]|id       force one GEMM tile (0 = autotune), "gemm_autotune" 0|[1]
+ *   "gemm_prefetch_r" 0|[1]  f16 residual prefetch in short-K GEMMs
+ *   "conv3x3_direct" 0|[1] layer1 3x3 conv on the halo-tile kernel (mec_conv_f16 too)
+ *   "pw_chain" 0|1|[2]     layer1 seam kernels (1: the 256->64 seams, 2: also 256->128)
+ *   "pw_chain_form" [0]|1|2  seam weight placement (LDS / registers)
+ *   "bert_qkv_attn" 0|[1]  fused BERT QKV projection + attention
+ *   "resnet_chunk" [0]|n   ResNet layers 1-2 over n-image chunks
+ *   "resnet_fused_tail" [0]|1, "mbv2_impl" [0]|1|2, "fusion_r" 1|[2]|4
+ *   "conv3x3_debug", "stem_debug", "gemm_debug": probe builds (wrong results). */
 int mec_set_option(const char* key, int value);
 
 /* Tile width the autotuner chose for a plain (amode 0) or conv (amode 1) GEMM shape; 0 = not yet seen. */
