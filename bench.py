@@ -54,6 +54,8 @@ def parse():
                     help="run each batch's fusion on the main stream (A/B of the cross-batch overlap)")
     ap.add_argument('--no-configs', action='store_true', help='skip the per-config (single-encoder) timings')
     ap.add_argument('--text-priority', type=int, default=1, help='0: BERT on the default-priority stream (A/B)')
+    ap.add_argument('--image-priority', type=int, default=0,
+                    help='1: speech + image stream at high priority, BERT at normal (A/B)')
     return ap.parse_args()
 
 
@@ -133,7 +135,7 @@ def main():
     from mec import engine, synthetic as syn
     B = a.batch
     pipe = engine.FusedPipeline(seed=1234, device=dev, concurrent=not a.serial, pipelined=not a.no_pipeline,
-                                text_priority=bool(a.text_priority))
+                                text_priority=bool(a.text_priority), image_priority=bool(a.image_priority))
     x = engine.to_device(syn.speech_inputs(B, seed=rank), dev)
     ids_np, mask_np = syn.text_inputs(B, 128, seed=rank, ragged=False)
     ids, mask = engine.to_device(ids_np, dev), engine.to_device(mask_np, dev)

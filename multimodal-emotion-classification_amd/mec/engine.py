@@ -235,7 +235,8 @@ class FusedPipeline:
     """
 
     def __init__(self, seed: int = 1234, device=None, weights=None, concurrent: bool = True,
-                 image_backbone: str = 'resnet50', pipelined: bool = True, text_priority: bool = True):
+                 image_backbone: str = 'resnet50', pipelined: bool = True, text_priority: bool = True,
+                 image_priority: bool = False):
         weights = weights or {}
         self.speech = SpeechEncoder(weights.get('speech'), seed, device)
         self.text = TextEncoder(weights.get('text'), seed, device)
@@ -244,11 +245,15 @@ class FusedPipeline:
         self.device = self.speech.device
         self.concurrent = concurrent
         self.pipelined = concurrent and pipelined
-        self._side = torch.cuda.Stream(device=self.device) if concurrent else None
+        # image_priority (A/B): the speech + image stream at high priority instead, BERT on its
+        # own normal-priority stream
+        self._side = (torch.cuda.Stream(device=self.device, priority=-1 if image_priority else 0)
+                      if concurrent else None)
         self._tail = torch.cuda.Stream(device=self.device) if self.pipelined else None
         # text_priority: BERT on its own high-priority stream, so its workgroups are dispatched
         # ahead of the image stream's and the image kernels fill the CUs BERT leaves idle
-        self._text = torch.cuda.Stream(device=self.device, priority=-1) if (concurrent and text_priority) else None
+        self._text = (torch.cuda.Stream(device=self.device, priority=0 if image_priority else -1)
+                      if (concurrent and (text_priority or image_priority)) else None)
         self._tuned = False
 
     def forward(self, x_speech, ids, mask, gray, epilogue=None):
