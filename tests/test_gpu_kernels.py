@@ -46,7 +46,7 @@ TILE_IDS = [64, 128, 256, 1064, 1128, 10064, 10128, 10256, 11064, 11128, 20256, 
 
 
 def _forced(lib, tid, fn):
-    lib.mec_set_option(b'gemm_bn', tid)
+    assert lib.mec_set_option(b'gemm_bn', tid) == 0, f'tile id {tid} rejected'
     try:
         fn()
     finally:
@@ -67,7 +67,7 @@ def test_every_tile_bit_identical(dev, amode):
         bias = torch.rand(N, generator=g).to(dev)
         R = torch.rand(M, N, generator=g).to(dev)
         ref = torch.nn.functional.gelu(A.float() @ B.float().t() + bias + R)
-        for tid in TILE_IDS + [40256, 41256, 42256, 43256]:
+        for tid in TILE_IDS + [40256, 41256]:
             C16 = torch.empty(M, N, dtype=torch.float16, device=dev)
             C32 = torch.empty(M, N, device=dev)
             _forced(lib, tid, lambda: _lib.check(lib.mec_gemm_f16(_p(A), _p(B), _p(bias), _p(R), 1, _p(C16), _p(C32),
@@ -99,7 +99,7 @@ def test_every_tile_bit_identical(dev, amode):
 
 @pytest.mark.parametrize('M,K', [(256, 64), (300, 128), (513, 192), (1000, 3072), (4096, 768)])
 def test_pingpong_tile_k_tails(dev, M, K):
-    """The ping-pong tiles (40256..43256) at 1, 2, 3, 48 and 12 K tiles: their prologue /
+    """The ping-pong tiles (40256, 41256) at 1, 2, 3, 48 and 12 K tiles: their prologue /
     restage / vmcnt tails, against torch and bit-identical to the 10256 tile."""
     lib = _lib.load()
     N = 512
@@ -109,7 +109,7 @@ def test_pingpong_tile_k_tails(dev, M, K):
     bias = torch.rand(N, generator=g).to(dev)
     ref = A.float() @ B.float().t() + bias
     outs = []
-    for tid in (40256, 41256, 42256, 43256, 10256):
+    for tid in (40256, 41256, 10256):
         C32 = torch.empty(M, N, device=dev)
         _forced(lib, tid, lambda: _lib.check(lib.mec_gemm_f16(_p(A), _p(B), _p(bias), None, 0, None, _p(C32),
                                                               M, N, K, 0, _s()), f'gemm {tid}'))
