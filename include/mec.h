@@ -104,7 +104,8 @@ int mec_conv_f16(const void* x, const void* w, const float* bias, const void* R,
 
 /* Process-wide tuning knobs (A/B benchmarking; defaults in brackets). Every pair of
  * settings of one knob gives bit-identical outputs, except the *_debug probe builds, which
- * skip work to time its parts and return wrong results.
+ * skip work to time its parts and return wrong results, and "fusion_r" 4 vs 1|2 (ulp-level,
+ * fp32 reassociation in the compiled block code; both within the oracle tolerance).
  *   "gemm_impl" 1|[2]      register-staged / glds GEMM engine
  *   "gemm_bn" [0]|id       force one GEMM tile (0 = autotune), "gemm_autotune" 0|[1]
  *   "gemm_prefetch_r" 0|[1]  f16 residual prefetch in short-K GEMMs
@@ -113,7 +114,9 @@ int mec_conv_f16(const void* x, const void* w, const float* bias, const void* R,
  *   "pw_chain_form" [0]|1|2  seam weight placement (LDS / registers)
  *   "bert_qkv_attn" 0|[1]  fused BERT QKV projection + attention
  *   "resnet_chunk" [0]|n   ResNet layers 1-2 over n-image chunks
- *   "resnet_fused_tail" [0]|1, "mbv2_impl" [0]|1|2, "fusion_r" 1|[2]|4
+ *   "resnet_fused_tail" [0]|1, "mbv2_impl" [0]|1|2
+ *   "fusion_r" 1|2|[4]     samples per fusion workgroup
+ *   "fusion_split" 0|[1]   fusion as 3 launches (per-modality projection, cross-attention, head)
  *   "conv3x3_debug", "stem_debug", "gemm_debug": probe builds (wrong results). */
 int mec_set_option(const char* key, int value);
 

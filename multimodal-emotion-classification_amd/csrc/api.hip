@@ -9,6 +9,7 @@
 namespace mec {
 const char* last_error();
 extern int g_fusion_r;
+extern int g_fusion_split;
 
 size_t blob_floats(int kind) {
   switch (kind) {
@@ -233,6 +234,7 @@ int mec_set_option(const char* key, int value) {
   const std::string k = key ? key : "";
   if (k == "gemm_impl" && (value == 1 || value == 2)) { g_gemm_impl = value; return 0; }
   if (k == "fusion_r" && (value == 1 || value == 2 || value == 4)) { g_fusion_r = value; return 0; }
+  if (k == "fusion_split" && (value == 0 || value == 1)) { g_fusion_split = value; return 0; }
   if (k == "gemm_debug" && value >= 0 && value <= 2) { g_gemm_debug = value; return 0; }
   if (k == "gemm_autotune" && (value == 0 || value == 1)) { g_gemm_autotune = value; return 0; }
   if (k == "gemm_prefetch_r" && (value == 0 || value == 1)) { g_gemm_prefetch_r = value; return 0; }

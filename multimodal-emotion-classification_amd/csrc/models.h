@@ -29,6 +29,8 @@ struct SpeechModel : Model {
 struct FusionModel : Model {
   DevBuf w;  // fp32, transposed Linear weights ([in][out]) + biases + LN params
   std::vector<size_t> off;  // offsets by FusionParam index
+  DevBuf ws;  // split form: projected (P) and fusion-projected (T) features, f32 [B, 768] each
+  int ws_batch = 0;
   int create(const float* blob, size_t n);
   int forward(const float* sf, const float* tf, const float* imf, const float* sp, const float* tp,
               const float* ip, int B, float* logits, float* probs, float* attn_w, float* dec_w,

@@ -130,7 +130,9 @@ int SpeechModel::forward(const float* x, int B, float* feat, float* logits, floa
 constexpr int FUSION_NP = 70;
 struct FusionW { const float* p[FUSION_NP]; };
 
-int g_fusion_r = 2;  // samples per workgroup (mec_set_option "fusion_r": 1, 2, 4, 8)
+// samples per workgroup (mec_set_option "fusion_r": 1, 2, 4). B = 256 on MI355X: split form
+// 145 / 139 / 118 us at R = 1 / 2 / 4, the single kernel 174 us at R = 2.
+int g_fusion_r = 4;
 constexpr int F_LDIN = 1368, F_LDP = 768, F_LDT = 1280;
 
 template <int FUSION_R>
@@ -263,6 +265,153 @@ __global__ __launch_bounds__(512) void fusion_kernel(FusionW w, const float* __r
   }
 }
 
+// ---- split form: the same block_linear / block_layernorm calls as fusion_kernel (so the
+// same bits), over three launches. The three modality chains of the projection and
+// cross-attention stages are independent, so stages 1-2 run one block per (sample group,
+// modality): 3x the blocks and a third of the serial layer chain per block.
+//   fusion_proj_kernel   grid (groups, 3): P_m = ReLU(LN(Linear_m(x_m)))           -> Pg
+//   fusion_cross_kernel  grid (groups, 3): E_m = LN(P_m + CrossAttn_m(P_m; P_o1, P_o2)),
+//                                          T_m = ReLU(LN(Proj_m(E_m)))             -> Tg
+//   fusion_head_kernel   grid (groups):    attention over T, decision weights, classifier
+int g_fusion_split = 1;  // mec_set_option "fusion_split": 0 = the single fused kernel
+
+template <int R>
+__global__ __launch_bounds__(512) void fusion_proj_kernel(FusionW w, const float* __restrict__ sf,
+                                                          const float* __restrict__ tf, const float* __restrict__ imf,
+                                                          int B, float* __restrict__ Pg) {
+  __shared__ __attribute__((aligned(16))) float IN[R * 768], P[R * 256], red[4 * R * SF_THREADS];
+  const int tid = threadIdx.x, m = blockIdx.y;
+  const int r0 = blockIdx.x * R, nr = min(R, B - r0);
+  const int dim = m == 0 ? 64 : (m == 1 ? 768 : 512);
+  const float* src = m == 0 ? sf : (m == 1 ? tf : imf);
+  for (int idx = tid; idx < R * dim; idx += blockDim.x) {
+    const int r = idx / dim, k = idx - r * dim;
+    IN[r * 768 + k] = r < nr ? src[(size_t)(r0 + r) * dim + k] : 0.f;
+  }
+  __syncthreads();
+  block_linear<R>(IN, 768, dim, w.p[4 * m], 256, w.p[4 * m + 1], 256, P, 256, red, BACT_NONE);
+  block_layernorm<R>(P, 256, 256, w.p[4 * m + 2], w.p[4 * m + 3], 1e-5f, true);
+  for (int idx = tid; idx < nr * 256; idx += blockDim.x) {
+    const int r = idx >> 8, n = idx & 255;
+    Pg[(size_t)(r0 + r) * 768 + 256 * m + n] = P[r * 256 + n];
+  }
+}
+
+template <int R>
+__global__ __launch_bounds__(512) void fusion_cross_kernel(FusionW w, const float* __restrict__ Pg, int B,
+                                                           float* __restrict__ Tg) {
+  __shared__ __attribute__((aligned(16))) float P[R * F_LDP], E[R * 256], T[R * F_LDT], red[4 * R * SF_THREADS];
+  const int tid = threadIdx.x, m = blockIdx.y;
+  const int r0 = blockIdx.x * R, nr = min(R, B - r0);
+  for (int idx = tid; idx < R * 768; idx += blockDim.x) {
+    const int r = idx / 768, k = idx - r * 768;
+    P[r * F_LDP + k] = r < nr ? Pg[(size_t)(r0 + r) * 768 + k] : 0.f;
+  }
+  __syncthreads();
+  const int o0 = m == 0 ? 1 : 0, o1 = m == 2 ? 1 : 2;  // the other two modalities, in order
+  const float* const* c = w.p + 12 + 10 * m;
+  block_linear<R>(P + 256 * m, F_LDP, 256, c[0], 256, c[1], 256, T + 0, F_LDT, red, BACT_NONE);
+  block_linear<R>(P + 256 * o0, F_LDP, 256, c[2], 256, c[3], 256, T + 256, F_LDT, red, BACT_NONE);
+  block_linear<R>(P + 256 * o1, F_LDP, 256, c[2], 256, c[3], 256, T + 512, F_LDT, red, BACT_NONE);
+  block_linear<R>(P + 256 * o0, F_LDP, 256, c[4], 256, c[5], 256, T + 768, F_LDT, red, BACT_NONE);
+  block_linear<R>(P + 256 * o1, F_LDP, 256, c[4], 256, c[5], 256, T + 1024, F_LDT, red, BACT_NONE);
+  cross_attention_rows<R>(T, F_LDT, nr);
+  block_linear<R>(T, F_LDT, 256, c[6], 256, c[7], 256, E, 256, red, BACT_NONE);
+  for (int idx = tid; idx < R * 256; idx += blockDim.x) {
+    const int r = idx >> 8, n = idx & 255;
+    E[r * 256 + n] = P[r * F_LDP + 256 * m + n] + E[r * 256 + n];
+  }
+  __syncthreads();
+  block_layernorm<R>(E, 256, 256, c[8], c[9], 1e-5f, false);
+  block_linear<R>(E, 256, 256, w.p[42 + 4 * m], 256, w.p[43 + 4 * m], 256, T, F_LDT, red, BACT_NONE);
+  block_layernorm<R>(T, F_LDT, 256, w.p[44 + 4 * m], w.p[45 + 4 * m], 1e-5f, true);
+  for (int idx = tid; idx < nr * 256; idx += blockDim.x) {
+    const int r = idx >> 8, n = idx & 255;
+    Tg[(size_t)(r0 + r) * 768 + 256 * m + n] = T[r * F_LDT + n];
+  }
+}
+
+template <int R>
+__global__ __launch_bounds__(512) void fusion_head_kernel(FusionW w, const float* __restrict__ Tg,
+                                                          const float* __restrict__ sp, const float* __restrict__ tp,
+                                                          const float* __restrict__ ip, int B, float* logits,
+                                                          float* probs, float* attn_w, float* dec_w) {
+  constexpr int LDPR = 24;
+  __shared__ __attribute__((aligned(16))) float PR[R * LDPR], P[R * F_LDP], E[R * F_LDP], T[R * F_LDT], red[4 * R * SF_THREADS];
+  const int tid = threadIdx.x, T_ = blockDim.x;
+  const int r0 = blockIdx.x * R;
+  const int nr = min(R, B - r0);
+  for (int idx = tid; idx < R * 768; idx += T_) {
+    const int r = idx / 768, k = idx - r * 768;
+    T[r * F_LDT + k] = r < nr ? Tg[(size_t)(r0 + r) * 768 + k] : 0.f;
+  }
+  for (int idx = tid; idx < R * LDPR; idx += T_) {
+    const int r = idx / LDPR, k = idx - r * LDPR;
+    const size_t b = (size_t)(r0 + r);
+    float v = 0.f;
+    if (r < nr) {
+      if (k < 7) v = sp[b * 7 + k];
+      else if (k < 14) v = tp[b * 7 + (k - 7)];
+      else if (k < 21) v = ip[b * 7 + (k - 14)];
+    }
+    PR[idx] = v;
+  }
+  __syncthreads();
+  block_linear<R>(T, F_LDT, 768, w.p[54], 256, w.p[55], 256, T + 768, F_LDT, red, BACT_TANH);
+  block_linear<R>(T + 768, F_LDT, 256, w.p[56], 3, w.p[57], 3, P, F_LDP, red, BACT_NONE);
+  block_softmax_small<R>(P, F_LDP, 3, nullptr, 0);
+  for (int idx = tid; idx < R * 256; idx += T_) {  // fused = sum_j w_j * proj_j
+    const int r = idx >> 8, n = idx & 255;
+    const float* a = P + r * F_LDP;
+    const float* t = T + r * F_LDT;
+    E[r * F_LDP + n] = a[0] * t[n] + a[1] * t[256 + n] + a[2] * t[512 + n];
+  }
+  for (int idx = tid; idx < nr * 3; idx += T_) {
+    const int r = idx / 3, j = idx - r * 3;
+    attn_w[(size_t)(r0 + r) * 3 + j] = P[r * F_LDP + j];
+  }
+  __syncthreads();
+  block_linear<R>(PR, LDPR, 21, w.p[58], 64, w.p[59], 64, P + 256, F_LDP, red, BACT_RELU);
+  block_linear<R>(P + 256, F_LDP, 64, w.p[60], 3, w.p[61], 3, P + 384, F_LDP, red, BACT_NONE);
+  block_softmax_small<R>(P + 384, F_LDP, 3, nullptr, 0);
+  for (int idx = tid; idx < R * 7; idx += T_) {
+    const int r = idx / 7, c = idx - r * 7;
+    const float* d = P + r * F_LDP + 384;
+    const float* pr = PR + r * LDPR;
+    E[r * F_LDP + 256 + c] = pr[c] * d[0] + pr[7 + c] * d[1] + pr[14 + c] * d[2];
+  }
+  for (int idx = tid; idx < nr * 3; idx += T_) {
+    const int r = idx / 3, j = idx - r * 3;
+    dec_w[(size_t)(r0 + r) * 3 + j] = P[r * F_LDP + 384 + j];
+  }
+  __syncthreads();
+  block_linear<R>(E, F_LDP, 263, w.p[62], 256, w.p[63], 256, T, F_LDT, red, BACT_NONE);
+  block_layernorm<R>(T, F_LDT, 256, w.p[64], w.p[65], 1e-5f, true);
+  block_linear<R>(T, F_LDT, 256, w.p[66], 128, w.p[67], 128, T + 256, F_LDT, red, BACT_RELU);
+  block_linear<R>(T + 256, F_LDT, 128, w.p[68], 7, w.p[69], 7, T + 384, F_LDT, red, BACT_NONE);
+  for (int idx = tid; idx < nr * 7; idx += T_) {
+    const int r = idx / 7, c = idx - r * 7;
+    logits[(size_t)(r0 + r) * 7 + c] = T[r * F_LDT + 384 + c];
+  }
+  __syncthreads();
+  block_softmax_small<R>(T + 384, F_LDT, 7, nullptr, 0);
+  for (int idx = tid; idx < nr * 7; idx += T_) {
+    const int r = idx / 7, c = idx - r * 7;
+    probs[(size_t)(r0 + r) * 7 + c] = T[r * F_LDT + 384 + c];
+  }
+}
+
+template <int R>
+static void launch_fusion_split(const FusionW& p, const float* sf, const float* tf, const float* imf, const float* sp,
+                                const float* tp, const float* ip, int B, float* Pg, float* Tg, float* logits,
+                                float* probs, float* attn_w, float* dec_w, hipStream_t s) {
+  const int groups = (B + R - 1) / R;
+  hipLaunchKernelGGL((fusion_proj_kernel<R>), dim3(groups, 3), dim3(SF_THREADS), 0, s, p, sf, tf, imf, B, Pg);
+  hipLaunchKernelGGL((fusion_cross_kernel<R>), dim3(groups, 3), dim3(SF_THREADS), 0, s, p, Pg, B, Tg);
+  hipLaunchKernelGGL((fusion_head_kernel<R>), dim3(groups), dim3(SF_THREADS), 0, s, p, Tg, sp, tp, ip, B, logits, probs,
+                     attn_w, dec_w);
+}
+
 int FusionModel::create(const float* blob, size_t n) {
   BlobReader rd(blob, n);
   std::vector<float> h;
@@ -326,6 +475,22 @@ int FusionModel::forward(const float* sf, const float* tf, const float* imf, con
   MEC_TRY(prof.begin(TAG_FUSION, s));
   const int R = g_fusion_r;
   const dim3 grid((B + R - 1) / R), blk(SF_THREADS);
+  if (g_fusion_split) {
+    if (B > ws_batch) {
+      MEC_TRY(ws.ensure((size_t)B * 768 * 2 * sizeof(float)));
+      ws_batch = B;
+    }
+    float* Pg = ws.as<float>();
+    float* Tg = Pg + (size_t)B * 768;
+    switch (R) {
+      case 1: launch_fusion_split<1>(p, sf, tf, imf, sp, tp, ip, B, Pg, Tg, logits, probs, attn_w, dec_w, s); break;
+      case 4: launch_fusion_split<4>(p, sf, tf, imf, sp, tp, ip, B, Pg, Tg, logits, probs, attn_w, dec_w, s); break;
+      default: launch_fusion_split<2>(p, sf, tf, imf, sp, tp, ip, B, Pg, Tg, logits, probs, attn_w, dec_w, s); break;
+    }
+    MEC_LAUNCH_CHECK();
+    MEC_TRY(prof.end(TAG_FUSION, s));
+    return 0;
+  }
   switch (R) {
     case 1: hipLaunchKernelGGL((fusion_kernel<1>), grid, blk, 0, s, p, sf, tf, imf, sp, tp, ip, B, logits, probs, attn_w, dec_w); break;
     case 4: hipLaunchKernelGGL((fusion_kernel<4>), grid, blk, 0, s, p, sf, tf, imf, sp, tp, ip, B, logits, probs, attn_w, dec_w); break;

@@ -190,6 +190,32 @@ def test_fused_bottleneck_tail_bit_identical(dev):
         assert torch.equal(a, b)
 
 
+@pytest.mark.parametrize('B', [1, 7, 256])
+def test_fusion_split_bit_identical(dev, B):
+    """The three-launch fusion (projection / cross-attention per modality, then the head)
+    against the single fused kernel at the same samples-per-block value: bit-identical.
+    (R = 4 itself differs from R = 1 / 2 by an ulp in both forms: not compared across R.)"""
+    from mec import engine, synthetic as syn
+    lib = _lib.load()
+    m = engine.FusionHead(device=dev)
+    g = torch.Generator().manual_seed(B)
+    args = [torch.randn(B, d, generator=g).to(dev) for d in (64, 768, 512)]
+    args += [torch.softmax(torch.randn(B, 7, generator=g), 1).to(dev) for _ in range(3)]
+    outs = {}
+    try:
+        for split in (0, 1):
+            for r in (1, 2, 4):
+                _lib.check(lib.mec_set_option(b'fusion_split', split), 'option')
+                _lib.check(lib.mec_set_option(b'fusion_r', r), 'option')
+                outs[split, r] = [t.cpu() for t in m.forward(*args)]
+    finally:
+        lib.mec_set_option(b'fusion_split', 1)
+        lib.mec_set_option(b'fusion_r', 4)
+    for r in (1, 2, 4):
+        for a, b in zip(outs[1, r], outs[0, r]):
+            assert torch.equal(a, b), r
+
+
 @pytest.mark.parametrize('n', [1, 3, 37, 75])
 def test_conv3x3_c64_bit_identical(dev, n):
     """ResNet layer1's 3x3 conv (56x56, 64 -> 64) on the halo-tile kernel (conv3x3.hip) vs the

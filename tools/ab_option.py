@@ -20,7 +20,7 @@ from mec import _lib, engine, synthetic as syn  # noqa: E402
 
 def main():
     ap = argparse.ArgumentParser()
-    ap.add_argument('--enc', choices=['text', 'image', 'image_mbv2', 'pipeline'], required=True)
+    ap.add_argument('--enc', choices=['text', 'image', 'image_mbv2', 'pipeline', 'fusion'], required=True)
     ap.add_argument('--opt', required=True)
     ap.add_argument('--values', type=int, nargs='+', required=True)
     ap.add_argument('--iters', type=int, default=5)
@@ -33,6 +33,11 @@ def main():
         ids, mask = syn.text_inputs(256, 128, seed=0)
         args = tuple(engine.to_device(v, dev) for v in (syn.speech_inputs(256, seed=0), ids, mask,
                                                         syn.image_inputs(256, seed=0)))
+    elif a.enc == 'fusion':  # the attention-fusion head alone on B = 256 feature rows
+        m = engine.FusionHead(device=dev)
+        g = torch.Generator().manual_seed(0)
+        args = tuple(torch.randn(256, d, generator=g).to(dev) for d in (64, 768, 512))
+        args += tuple(torch.softmax(torch.randn(256, 7, generator=g), 1).to(dev) for _ in range(3))
     elif a.enc == 'text':
         m = engine.TextEncoder(device=dev)
         ids, mask = syn.text_inputs(256, 128, seed=0)
