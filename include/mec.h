@@ -108,6 +108,7 @@ int mec_conv_f16(const void* x, const void* w, const float* bias, const void* R,
  * fp32 reassociation in the compiled block code; both within the oracle tolerance).
  *   "gemm_impl" 1|[2]      register-staged / glds GEMM engine
  *   "gemm_bn" [0]|id       force one GEMM tile (0 = autotune), "gemm_autotune" 0|[1]
+ *   "gemm_bn_tag" tag*100000+id   force a tile for one launch class (e.g. 3 = BERT O-proj)
  *   "gemm_prefetch_r" 0|[1]  f16 residual prefetch in short-K GEMMs
  *   "conv3x3_direct" 0|[1] layer1 3x3 conv on the halo-tile kernel (mec_conv_f16 too)
  *   "pw_chain" 0|1|[2]     layer1 seam kernels (1: the 256->64 seams, 2: also 256->128)

@@ -10,6 +10,7 @@ namespace mec {
 const char* last_error();
 extern int g_fusion_r;
 extern int g_fusion_split;
+extern int g_gemm_bn_tag[TAG_COUNT];
 
 size_t blob_floats(int kind) {
   switch (kind) {
@@ -253,11 +254,19 @@ int mec_set_option(const char* key, int value) {
     g_conv3x3_debug = value;
     return 0;
   }
-  const int v = value % 10000;
-  const bool deep = value == 20256 || value == 30256 || value == 20128 || value == 40256 || value == 41256 || value == 50128 ||
-                    value == 60128 || value == 50256;
-  if (k == "gemm_bn" && (value == 0 || deep || (value < 20000 && (v == 64 || v == 128 || v == 256 || v == 1064 || v == 1128)))) {
+  auto tile_ok = [](int id) {
+    const int v = id % 10000;
+    const bool deep = id == 20256 || id == 30256 || id == 20128 || id == 40256 || id == 41256 || id == 50128 ||
+                      id == 60128 || id == 50256;
+    return id == 0 || deep || (id < 20000 && (v == 64 || v == 128 || v == 256 || v == 1064 || v == 1128));
+  };
+  if (k == "gemm_bn" && tile_ok(value)) {
     g_gemm_bn = value;
+    return 0;
+  }
+  // one launch class only: value = tag * 100000 + tile id (tags: mec_common.h KernelTag)
+  if (k == "gemm_bn_tag" && value >= 0 && value / 100000 > 0 && value / 100000 < TAG_COUNT && tile_ok(value % 100000)) {
+    g_gemm_bn_tag[value / 100000] = value % 100000;
     return 0;
   }
   set_error("mec_set_option: unknown key or bad value: " + k);

@@ -57,6 +57,7 @@ enum KernelTag : int {
   TAG_FUSION = 11,
   TAG_MBV2_BLOCK = 12,
   TAG_MBV2_LAST = 13,
+  TAG_COUNT = 14,
 };
 
 // hipEvent pairs recorded around every launch whose tag matches `tag`.
