@@ -113,7 +113,8 @@ int mec_conv_f16(const void* x, const void* w, const float* bias, const void* R,
  *   "conv3x3_direct" 0|[1] layer1 3x3 conv on the halo-tile kernel (mec_conv_f16 too)
  *   "pw_chain" 0|1|[2]     layer1 seam kernels (1: the 256->64 seams, 2: also 256->128)
  *   "pw_chain_form" [0]|1|2  seam weight placement (LDS / registers)
- *   "bert_qkv_attn" 0|[1]  fused BERT QKV projection + attention
+ *   "bert_qkv_attn" 0|[1]  fused BERT QKV projection + attention (2 / 3: probe builds,
+ *                          no attention / main loop only)
  *   "resnet_chunk" [0]|n   ResNet layers 1-2 over n-image chunks
  *   "resnet_fused_tail" [0]|1, "mbv2_impl" [0]|1|2
  *   "fusion_r" 1|2|[4]     samples per fusion workgroup

@@ -269,6 +269,7 @@ __global__ __launch_bounds__(256) void bert_attention_kernel(const f16* __restri
 constexpr int QA_BM = 128, QA_BN = 384, QA_BK = 64, QA_NK = BH / QA_BK;
 constexpr int QA_STAGE = (QA_BM + QA_BN) * QA_BK;  // halfs per stage (64 KB)
 
+template <int DBG = 0>  // probe builds (wrong results): 1 = no attention, 2 = main loop only
 __global__ __launch_bounds__(512, 1) void bert_qkv_attn_kernel(const f16* __restrict__ h16,
                                                                const f16* __restrict__ wqkv,
                                                                const float* __restrict__ bqkv,
@@ -362,6 +363,15 @@ __global__ __launch_bounds__(512, 1) void bert_qkv_attn_kernel(const f16* __rest
           acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_f16(bf[s2][j], af[s2][i], acc[i][j], 0, 0, 0);
   }
 
+  if constexpr (DBG == 2) {
+    float t = 0.f;
+#pragma unroll
+    for (int i = 0; i < 4; ++i)
+#pragma unroll
+      for (int j = 0; j < 6; ++j) t += acc[i][j][0] + acc[i][j][1] + acc[i][j][2] + acc[i][j][3];
+    if (t == 12345.678f) ctx[tid] = (f16)t;
+    return;
+  }
   // ---- epilogue: (acc + bias) + 0 -> f16 -> the attention's Q / K / V LDS images
   if (tid < ATT_L) sBias[tid] = mask[(size_t)b * ATT_L + tid] ? 0.f : -3.4028234663852886e38f;  // finfo(f32).min
   f16* img = smem;  // [Q0 Q1 K0 K1 V0 V1], each [128][64]
@@ -387,12 +397,17 @@ __global__ __launch_bounds__(512, 1) void bert_qkv_attn_kernel(const f16* __rest
     }
   }
   __syncthreads();
+  if constexpr (DBG == 1) {
+    if (img[tid] == (f16)12345.f) ctx[tid] = img[tid + 1];
+    return;
+  }
   const int hh = wave >> 2;
   attn_head(img + hh * (ATT_L * BDH), img + (2 + hh) * (ATT_L * BDH), img + (4 + hh) * (ATT_L * BDH), sBias,
             wave & 3, lane, ctx + (size_t)b * ATT_L * BH + (2 * hp + hh) * BDH);
 }
 
-int g_bert_qkv_attn = 1;  // fused QKV projection + attention (0: QKV GEMM, then attention kernel)
+int g_bert_qkv_attn = 1;  // fused QKV projection + attention (0: QKV GEMM, then attention kernel;
+                          // 2 / 3: probe builds without the attention / with the main loop only)
 
 // ----------------------------------------------------------------------------- model
 // prm layout per layer (floats): bqkv 2304 | bo 768 | ln1g 768 | ln1b 768 | bi 3072 | bo2 768 |
@@ -512,7 +527,12 @@ int TextModel::forward(const int32_t* ids, const int32_t* mask, int B, int L, fl
     GemmParams g;
     if (g_bert_qkv_attn) {
       MEC_TRY(prof.begin(TAG_BERT_ATTN, s));
-      hipLaunchKernelGGL(bert_qkv_attn_kernel, dim3(B * 6), dim3(512), 0, s, h16, wqkv, bqkv, mask, ctx16, B);
+      if (g_bert_qkv_attn == 2)
+        hipLaunchKernelGGL((bert_qkv_attn_kernel<1>), dim3(B * 6), dim3(512), 0, s, h16, wqkv, bqkv, mask, ctx16, B);
+      else if (g_bert_qkv_attn == 3)
+        hipLaunchKernelGGL((bert_qkv_attn_kernel<2>), dim3(B * 6), dim3(512), 0, s, h16, wqkv, bqkv, mask, ctx16, B);
+      else
+        hipLaunchKernelGGL((bert_qkv_attn_kernel<0>), dim3(B * 6), dim3(512), 0, s, h16, wqkv, bqkv, mask, ctx16, B);
       MEC_LAUNCH_CHECK();
       MEC_TRY(prof.end(TAG_BERT_ATTN, s));
     } else {
