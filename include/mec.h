@@ -119,7 +119,8 @@ int mec_conv_f16(const void* x, const void* w, const float* bias, const void* R,
  *   "resnet_fused_tail" [0]|1, "mbv2_impl" [0]|1|2
  *   "fusion_r" 1|2|[4]     samples per fusion workgroup
  *   "fusion_split" 0|[1]   fusion as 3 launches (per-modality projection, cross-attention, head)
- *   "conv3x3_debug", "stem_debug", "gemm_debug": probe builds (wrong results). */
+ *   "conv3x3_debug", "stem_debug", "gemm_debug": probe builds (wrong results); gemm_debug 4
+ *   records an s_memtime phase trace of the ping-pong tile (tools/pp_trace.py). */
 int mec_set_option(const char* key, int value);
 
 /* Tile width the autotuner chose for a plain (amode 0) or conv (amode 1) GEMM shape; 0 = not yet seen. */

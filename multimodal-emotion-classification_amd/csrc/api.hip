@@ -236,7 +236,7 @@ int mec_set_option(const char* key, int value) {
   if (k == "gemm_impl" && (value == 1 || value == 2)) { g_gemm_impl = value; return 0; }
   if (k == "fusion_r" && (value == 1 || value == 2 || value == 4)) { g_fusion_r = value; return 0; }
   if (k == "fusion_split" && (value == 0 || value == 1)) { g_fusion_split = value; return 0; }
-  if (k == "gemm_debug" && value >= 0 && value <= 2) { g_gemm_debug = value; return 0; }
+  if (k == "gemm_debug" && value >= 0 && value <= 4) { g_gemm_debug = value; return 0; }
   if (k == "gemm_autotune" && (value == 0 || value == 1)) { g_gemm_autotune = value; return 0; }
   if (k == "gemm_prefetch_r" && (value == 0 || value == 1)) { g_gemm_prefetch_r = value; return 0; }
   if (k == "resnet_fused_tail" && (value == 0 || value == 1)) { g_resnet_fused_tail = value; return 0; }

@@ -487,6 +487,8 @@ __global__ __launch_bounds__(64 * WM * WN, (WM * WN == 4) ? 2 : 1) void gemm_gld
 // MFMA section while its partner loads. ph3 waits vmcnt(6): everything but the three
 // pieces issued for tile t+2 has landed, i.e. all of tile t+1, read one phase later.
 // Same k order per output as every other tile, so results are bit-identical to them.
+// DBG = 4 (probe build, tools/pp_trace.py): s_memtime at four points of every phase of the
+// first 12 K tiles, per wave, kept in spare LDS and dumped by one block into C32.
 template <int AM, int DBG = 0, int BM = 256>
 __global__ __launch_bounds__(512) void gemm_pp_kernel(const GemmParams p) {
   static_assert(AM == A_PLAIN, "ping-pong tile: plain A only");
@@ -501,6 +503,16 @@ __global__ __launch_bounds__(512) void gemm_pp_kernel(const GemmParams p) {
   constexpr int VM = (2 * GA + GB) * 1;    // glds of the three pieces issued for tile t+2
   typedef float accv __attribute__((ext_vector_type(4)));
   __shared__ __attribute__((aligned(16))) f16 smem[2 * BUF];
+  constexpr int TRN = DBG == 4 ? 12 * 4 * 4 : 1;  // DBG 4 (probe): s_memtime phase trace
+  __shared__ unsigned long long trace[DBG == 4 ? 8 : 1][TRN];
+  int trk = 0;
+  auto tmark = [&]() {
+    if constexpr (DBG == 4) {
+      const unsigned long long t = __builtin_amdgcn_s_memtime();
+      if ((threadIdx.x & 63) == 0 && trk < TRN) trace[threadIdx.x >> 6][trk] = t;
+      ++trk;
+    }
+  };
 
   const int tid = threadIdx.x, lane = tid & 63;
   const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
@@ -589,8 +601,10 @@ __global__ __launch_bounds__(512) void gemm_pp_kernel(const GemmParams p) {
   auto mma = [&](const int qa, const int qb) {
     __builtin_amdgcn_sched_barrier(0);
     asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+    tmark();
     __builtin_amdgcn_s_barrier();
     __builtin_amdgcn_sched_barrier(0);
+    tmark();
     __builtin_amdgcn_s_setprio(1);
 #pragma unroll
     for (int k = 0; k < 2; ++k)
@@ -602,6 +616,7 @@ __global__ __launch_bounds__(512) void gemm_pp_kernel(const GemmParams p) {
               __builtin_amdgcn_mfma_f32_16x16x32_f16(af[k][i], bf[k][j], acc[qa * QI + i][qb * 2 + j], 0, 0, 0);
     __builtin_amdgcn_s_setprio(0);
     __builtin_amdgcn_sched_barrier(0);
+    tmark();
     __builtin_amdgcn_s_barrier();
     __builtin_amdgcn_sched_barrier(0);
   };
@@ -627,19 +642,23 @@ __global__ __launch_bounds__(512) void gemm_pp_kernel(const GemmParams p) {
     const int buf = t & 1;
     const bool n1 = t + 1 < nk, n2 = t + 2 < nk;
     // ph0 (A0, B0)
+    tmark();
     read_a(buf, 0);
     read_b(buf, 0);
     if (n1) issue(2, t + 1);
     mma(0, 0);
     // ph1 (A0, B1)
+    tmark();
     read_b(buf, 1);
     if (n2) issue(0, t + 2);
     mma(0, 1);
     // ph2 (A1, B1)
+    tmark();
     read_a(buf, 1);
     if (n2) issue(3, t + 2);
     mma(1, 1);
     // ph3 (A1, B0)
+    tmark();
     read_b(buf, 0);
     if (n2) {
       issue(1, t + 2);
@@ -651,6 +670,13 @@ __global__ __launch_bounds__(512) void gemm_pp_kernel(const GemmParams p) {
   }
   if (wm == 0) __builtin_amdgcn_s_barrier();  // re-align the two wave rows
   asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)" ::: "memory");
+  if constexpr (DBG == 4) {  // probe build: block gridDim.x / 2 dumps its trace into C32
+    __syncthreads();
+    if (blockIdx.x == gridDim.x / 2)
+      for (int i = tid; i < 8 * TRN; i += blockDim.x)
+        reinterpret_cast<unsigned long long*>(p.C32)[i] = trace[i / TRN][i % TRN];
+    return;
+  }
   if constexpr (DBG == 2) {  // probe build: no epilogue
     float s = 0.f;
 #pragma unroll
@@ -754,7 +780,9 @@ static int launch_bn(const GemmParams& p, hipStream_t s, int id) {
       const int nbn = p.N / 256;
       if (id == 40256) {
         const dim3 grd(((p.M + 255) / 256) * nbn);
-        if (dbg)
+        if (g_gemm_debug == 4)
+          hipLaunchKernelGGL((gemm_pp_kernel<A_PLAIN, 4, 256>), grd, blk, 0, s, p);
+        else if (dbg)
           hipLaunchKernelGGL((gemm_pp_kernel<A_PLAIN, 2, 256>), grd, blk, 0, s, p);
         else
           hipLaunchKernelGGL((gemm_pp_kernel<A_PLAIN, 0, 256>), grd, blk, 0, s, p);
