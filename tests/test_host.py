@@ -76,6 +76,29 @@ def test_c_abi_argument_errors_without_gpu():
     assert b'null model' in lib.mec_last_error()
 
 
+def test_option_validation_without_gpu():
+    """mec_set_option accepts each knob's documented values (include/mec.h) and rejects the
+    rest; it only sets process globals, so this runs without a GPU. Defaults restored."""
+    lib = _lib.load()
+    ok = [(b'fusion_r', 1), (b'fusion_r', 4), (b'fusion_split', 0), (b'fusion_split', 1),
+          (b'bert_qkv_attn', 0), (b'bert_qkv_attn', 1), (b'gemm_bn', 40256), (b'gemm_bn', 0),
+          (b'gemm_bn_tag', 3 * 100000 + 40256), (b'gemm_bn_tag', 3 * 100000 + 11128),
+          (b'gemm_debug', 0)]
+    bad = [(b'fusion_r', 3), (b'fusion_split', 2), (b'bert_qkv_attn', 4), (b'gemm_bn', 12345),
+           (b'gemm_bn', 42256), (b'gemm_bn_tag', 11128), (b'gemm_bn_tag', 14 * 100000 + 256),
+           (b'gemm_bn_tag', 3 * 100000 + 999), (b'gemm_bn_tag', -1), (b'gemm_debug', 5)]
+    try:
+        for k, v in ok:
+            assert lib.mec_set_option(k, v) == 0, (k, v)
+        for k, v in bad:
+            assert lib.mec_set_option(k, v) == -1, (k, v)
+            assert b'bad value' in lib.mec_last_error()
+    finally:  # the defaults
+        for k, v in [(b'fusion_r', 4), (b'fusion_split', 1), (b'bert_qkv_attn', 1), (b'gemm_bn', 0),
+                     (b'gemm_bn_tag', 3 * 100000 + 11128), (b'gemm_debug', 0)]:
+            lib.mec_set_option(k, v)
+
+
 @pytest.mark.parametrize('total,world', [(256, 1), (8192, 8), (10, 3), (2, 4), (0, 2)])
 def test_shards_partition_the_batch(total, world):
     spans = [mdist.shard(total, world, r) for r in range(world)]
