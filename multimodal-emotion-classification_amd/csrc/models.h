@@ -119,6 +119,7 @@ int launch_bneck_tail(const f16* t1, const f16* x, const f16* w2, const float* b
 extern int g_resnet_fused_tail;
 extern int g_resnet_chunk;
 extern int g_bert_qkv_attn;
+extern int g_bert_oproj_ln;
 extern int g_stem_debug;
 extern int g_pw_chain;
 extern int g_pw_chain_form;

@@ -81,10 +81,11 @@ def test_option_validation_without_gpu():
     rest; it only sets process globals, so this runs without a GPU. Defaults restored."""
     lib = _lib.load()
     ok = [(b'fusion_r', 1), (b'fusion_r', 4), (b'fusion_split', 0), (b'fusion_split', 1),
-          (b'bert_qkv_attn', 0), (b'bert_qkv_attn', 1), (b'gemm_bn', 40256), (b'gemm_bn', 0),
+          (b'bert_qkv_attn', 0), (b'bert_qkv_attn', 1), (b'bert_oproj_ln', 0), (b'bert_oproj_ln', 1),
+          (b'gemm_bn', 40256), (b'gemm_bn', 0),
           (b'gemm_bn_tag', 3 * 100000 + 40256), (b'gemm_bn_tag', 3 * 100000 + 11128),
           (b'gemm_debug', 0)]
-    bad = [(b'fusion_r', 3), (b'fusion_split', 2), (b'bert_qkv_attn', 4), (b'gemm_bn', 12345),
+    bad = [(b'fusion_r', 3), (b'fusion_split', 2), (b'bert_qkv_attn', 4), (b'bert_oproj_ln', 3), (b'gemm_bn', 12345),
            (b'gemm_bn', 42256), (b'gemm_bn_tag', 11128), (b'gemm_bn_tag', 14 * 100000 + 256),
            (b'gemm_bn_tag', 3 * 100000 + 999), (b'gemm_bn_tag', -1), (b'gemm_debug', 5)]
     try:
@@ -94,7 +95,8 @@ def test_option_validation_without_gpu():
             assert lib.mec_set_option(k, v) == -1, (k, v)
             assert b'bad value' in lib.mec_last_error()
     finally:  # the defaults
-        for k, v in [(b'fusion_r', 4), (b'fusion_split', 1), (b'bert_qkv_attn', 1), (b'gemm_bn', 0),
+        for k, v in [(b'fusion_r', 4), (b'fusion_split', 1), (b'bert_qkv_attn', 1), (b'bert_oproj_ln', 0),
+                     (b'gemm_bn', 0),
                      (b'gemm_bn_tag', 3 * 100000 + 11128), (b'gemm_debug', 0)]:
             lib.mec_set_option(k, v)
 
