@@ -115,8 +115,9 @@ int mec_conv_f16(const void* x, const void* w, const float* bias, const void* R,
  *   "pw_chain_form" [0]|1|2  seam weight placement (LDS / registers)
  *   "bert_qkv_attn" 0|[1]  fused BERT QKV projection + attention (2 / 3: probe builds,
  *                          no attention / main loop only)
- *   "bert_oproj_ln" [0]|1|2  BERT O-projection + residual + LayerNorm 1 in one full-row kernel
- *                          (measured slower; 2: main-loop-only probe build)
+ *   "bert_oproj_ln" [0]|1|3  BERT O-projection + residual + LayerNorm 1 in one full-row kernel
+ *                          (1: Wo staged in LDS, 3: Wo read into registers; both measured
+ *                          slower; 2 / 4: their main-loop-only probe builds)
  *   "resnet_chunk" [0]|n   ResNet layers 1-2 over n-image chunks
  *   "resnet_fused_tail" [0]|1, "mbv2_impl" [0]|1|2
  *   "fusion_r" 1|2|[4]     samples per fusion workgroup

@@ -244,7 +244,7 @@ int mec_set_option(const char* key, int value) {
   if (k == "conv3x3_direct" && (value == 0 || value == 1)) { g_conv3x3_direct = value; return 0; }
   if (k == "resnet_chunk" && value >= 0) { g_resnet_chunk = value; return 0; }
   if (k == "bert_qkv_attn" && value >= 0 && value <= 3) { g_bert_qkv_attn = value; return 0; }
-  if (k == "bert_oproj_ln" && value >= 0 && value <= 2) { g_bert_oproj_ln = value; return 0; }
+  if (k == "bert_oproj_ln" && value >= 0 && value <= 4) { g_bert_oproj_ln = value; return 0; }
   if (k == "stem_debug" && (value == 0 || value == 1 || value == 2 || value == 4 || value == 7)) {
     g_stem_debug = value;
     return 0;

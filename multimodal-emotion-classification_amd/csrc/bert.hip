@@ -441,7 +441,7 @@ __device__ __forceinline__ int olswz(int row, int kc) { return kc ^ ((row >> 1) 
 
 // RST: the residual is the previous layer's deferred LN2 (else h32 as is); DBG 1: probe build
 // that stops after the main loop (wrong results)
-template <bool RST, int DBG = 0>
+template <bool RST, int DBG = 0, bool BD = false>
 __global__ __launch_bounds__(512, 1) void bert_oproj_ln_kernel(const f16* __restrict__ ctx,
                                                                const f16* __restrict__ wo,
                                                                const float* __restrict__ bo,
@@ -453,7 +453,7 @@ __global__ __launch_bounds__(512, 1) void bert_oproj_ln_kernel(const f16* __rest
                                                                const float* __restrict__ b1,
                                                                float* __restrict__ t32, f16* __restrict__ h16,
                                                                float2* __restrict__ st1) {
-  __shared__ __attribute__((aligned(16))) f16 smem[2 * OL_STAGE];
+  __shared__ __attribute__((aligned(16))) f16 smem[BD ? 3 * OL_BM * 64 : 2 * OL_STAGE];
   __shared__ float red[8][OL_BM];
   __shared__ __attribute__((aligned(16))) float sPar[5][BH];  // bo, r_g, r_b, g1, b1
   typedef __attribute__((address_space(3))) void* lds_p;
@@ -471,71 +471,125 @@ __global__ __launch_bounds__(512, 1) void bert_oproj_ln_kernel(const f16* __rest
     *reinterpret_cast<float4*>(&sPar[a][c]) = v;
   }
 
-  // piece p = it * 8 + wave covers stage rows 16p .. 16p+15; lane -> (row lane>>2, chunk lane&3)
-  const int lrow = lane >> 2, pch = lane & 3;
-  const bool extra = wave < OL_PIECES - 48;  // 52 pieces: waves 0-3 load a 7th
-  // a 16-row piece is all A (pieces 0-3: it 0 on waves 0-3) or all B, so the source base is
-  // wave-uniform and each lane keeps a 32-bit element offset per piece (no 64-bit pointers)
-  const f16* src_it0 = wave < OL_BM / 16 ? ctx : wo;
-  uint32_t off[7];
-#pragma unroll
-  for (int it = 0; it < 7; ++it) {
-    const int Rw = (it * 8 + wave) * 16 + lrow;
-    const int c = olswz(Rw, pch);
-    off[it] = Rw < OL_BM ? (uint32_t)((m0 + Rw) * BH + c * 8)
-                         : (uint32_t)((Rw < OL_ROWS ? Rw - OL_BM : 0) * BH + c * 8);
-  }
-  auto issue = [&](int kt, int st) {
-    f16* base = smem + st * OL_STAGE;
-#pragma unroll
-    for (int it = 0; it < 6; ++it)
-      __builtin_amdgcn_global_load_lds((const void*)((it == 0 ? src_it0 : wo) + off[it] + kt * OL_BK),
-                                       (lds_p)(base + (it * 8 + wave) * 16 * OL_BK), 16, 0, 0);
-    if (extra)
-      __builtin_amdgcn_global_load_lds((const void*)(wo + off[6] + kt * OL_BK),
-                                       (lds_p)(base + (48 + wave) * 16 * OL_BK), 16, 0, 0);
-  };
-
   floatx4 acc[4][6];
 #pragma unroll
   for (int i = 0; i < 4; ++i)
 #pragma unroll
     for (int j = 0; j < 6; ++j) acc[i][j] = floatx4{0.f, 0.f, 0.f, 0.f};
-  issue(0, 0);
-  issue(1, 1);
-#pragma unroll 1
-  for (int kt = 0; kt < OL_NK; ++kt) {
-    if (kt + 1 < OL_NK) {
-      if (extra)
-        asm volatile("s_waitcnt vmcnt(7)" ::: "memory");
-      else
-        asm volatile("s_waitcnt vmcnt(6)" ::: "memory");
-    } else {
-      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-    }
-    __builtin_amdgcn_s_barrier();  // stage kt landed for every wave
-    const f16* sA = smem + (kt & 1) * OL_STAGE;
-    half8 af[4], bf[6];
-#pragma unroll
-    for (int i = 0; i < 4; ++i) {
-      const int r = 16 * i + l16;
-      af[i] = *reinterpret_cast<const half8*>(sA + r * OL_BK + olswz(r, lq) * 8);
-    }
-#pragma unroll
-    for (int j = 0; j < 6; ++j) {
-      const int rr = OL_BM + 96 * wave + 16 * j + l16;
-      bf[j] = *reinterpret_cast<const half8*>(sA + rr * OL_BK + olswz(rr, lq) * 8);
-    }
-    __builtin_amdgcn_sched_barrier(0);
-    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
-    __builtin_amdgcn_s_barrier();  // every wave is done reading stage kt
-    if (kt + 2 < OL_NK) issue(kt + 2, kt & 1);
-    __builtin_amdgcn_sched_barrier(0);
-#pragma unroll
-    for (int i = 0; i < 4; ++i)
+  if constexpr (BD) {
+    // Direct-B form: only the A tile (64 tokens x 64 k, 128-B rows, aswz chunks, 3 stages,
+    // one 1-KB DMA piece per wave) goes through LDS. Wave w's Wo rows 96w..96w+95 are private
+    // to it, so they go L2 -> VGPRs one K step ahead (two register sets), each lane reading
+    // 32 contiguous bytes per row (4 lanes = one 128-B line). The k order inside a 64-deep
+    // step is permuted (lane lq, half s2 <-> k 16lq + 8s2 .. +7) identically for A and B.
+    constexpr int NK = BH / 64;
+    const int arow = wave * 8 + (lane >> 3), ach = lane & 7;
+    const uint32_t aoff = (uint32_t)((m0 + arow) * BH + aswz(arow, ach) * 8);
+    auto issueA = [&](int kt, int st) {
+      __builtin_amdgcn_global_load_lds((const void*)(ctx + aoff + kt * 64), (lds_p)(smem + st * (OL_BM * 64) + wave * 512),
+                                       16, 0, 0);
+    };
+    const f16* wrow = wo + (size_t)(96 * wave + l16) * BH + lq * 16;
+    half8 bb[2][6][2];
+    auto loadB = [&](int set, int kt) {
 #pragma unroll
       for (int j = 0; j < 6; ++j)
-        acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_f16(bf[j], af[i], acc[i][j], 0, 0, 0);
+#pragma unroll
+        for (int s2 = 0; s2 < 2; ++s2)
+          bb[set][j][s2] = *reinterpret_cast<const half8*>(wrow + (size_t)j * 16 * BH + kt * 64 + s2 * 8);
+    };
+    issueA(0, 0);
+    loadB(0, 0);
+    issueA(1, 1);
+#pragma unroll
+    for (int kt = 0; kt < NK; ++kt) {
+      // outstanding in issue order: A(kt), B(kt) x12, A(kt+1)
+      if (kt + 1 < NK)
+        asm volatile("s_waitcnt vmcnt(1)" ::: "memory");
+      else
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+      __builtin_amdgcn_s_barrier();  // A stage kt landed for every wave; stage kt-1 is free
+      if (kt + 1 < NK) loadB((kt + 1) & 1, kt + 1);
+      if (kt + 2 < NK) issueA(kt + 2, (kt + 2) % 3);
+      const f16* sA = smem + (kt % 3) * (OL_BM * 64);
+#pragma unroll
+      for (int s2 = 0; s2 < 2; ++s2) {
+        half8 af[4];
+#pragma unroll
+        for (int i = 0; i < 4; ++i) {
+          const int r = 16 * i + l16;
+          af[i] = *reinterpret_cast<const half8*>(sA + r * 64 + aswz(r, 2 * lq + s2) * 8);
+        }
+#pragma unroll
+        for (int i = 0; i < 4; ++i)
+#pragma unroll
+          for (int j = 0; j < 6; ++j)
+            acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_f16(bb[kt & 1][j][s2], af[i], acc[i][j], 0, 0, 0);
+      }
+    }
+    __syncthreads();
+  } else {
+    // piece p = it * 8 + wave covers stage rows 16p .. 16p+15; lane -> (row lane>>2, chunk lane&3)
+    const int lrow = lane >> 2, pch = lane & 3;
+    const bool extra = wave < OL_PIECES - 48;  // 52 pieces: waves 0-3 load a 7th
+    // a 16-row piece is all A (pieces 0-3: it 0 on waves 0-3) or all B, so the source base is
+    // wave-uniform and each lane keeps a 32-bit element offset per piece (no 64-bit pointers)
+    const f16* src_it0 = wave < OL_BM / 16 ? ctx : wo;
+    uint32_t off[7];
+  #pragma unroll
+    for (int it = 0; it < 7; ++it) {
+      const int Rw = (it * 8 + wave) * 16 + lrow;
+      const int c = olswz(Rw, pch);
+      off[it] = Rw < OL_BM ? (uint32_t)((m0 + Rw) * BH + c * 8)
+                           : (uint32_t)((Rw < OL_ROWS ? Rw - OL_BM : 0) * BH + c * 8);
+    }
+    auto issue = [&](int kt, int st) {
+      f16* base = smem + st * OL_STAGE;
+  #pragma unroll
+      for (int it = 0; it < 6; ++it)
+        __builtin_amdgcn_global_load_lds((const void*)((it == 0 ? src_it0 : wo) + off[it] + kt * OL_BK),
+                                         (lds_p)(base + (it * 8 + wave) * 16 * OL_BK), 16, 0, 0);
+      if (extra)
+        __builtin_amdgcn_global_load_lds((const void*)(wo + off[6] + kt * OL_BK),
+                                         (lds_p)(base + (48 + wave) * 16 * OL_BK), 16, 0, 0);
+    };
+
+    issue(0, 0);
+    issue(1, 1);
+  #pragma unroll 1
+    for (int kt = 0; kt < OL_NK; ++kt) {
+      if (kt + 1 < OL_NK) {
+        if (extra)
+          asm volatile("s_waitcnt vmcnt(7)" ::: "memory");
+        else
+          asm volatile("s_waitcnt vmcnt(6)" ::: "memory");
+      } else {
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+      }
+      __builtin_amdgcn_s_barrier();  // stage kt landed for every wave
+      const f16* sA = smem + (kt & 1) * OL_STAGE;
+      half8 af[4], bf[6];
+  #pragma unroll
+      for (int i = 0; i < 4; ++i) {
+        const int r = 16 * i + l16;
+        af[i] = *reinterpret_cast<const half8*>(sA + r * OL_BK + olswz(r, lq) * 8);
+      }
+  #pragma unroll
+      for (int j = 0; j < 6; ++j) {
+        const int rr = OL_BM + 96 * wave + 16 * j + l16;
+        bf[j] = *reinterpret_cast<const half8*>(sA + rr * OL_BK + olswz(rr, lq) * 8);
+      }
+      __builtin_amdgcn_sched_barrier(0);
+      asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+      __builtin_amdgcn_s_barrier();  // every wave is done reading stage kt
+      if (kt + 2 < OL_NK) issue(kt + 2, kt & 1);
+      __builtin_amdgcn_sched_barrier(0);
+  #pragma unroll
+      for (int i = 0; i < 4; ++i)
+  #pragma unroll
+        for (int j = 0; j < 6; ++j)
+          acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_f16(bf[j], af[i], acc[i][j], 0, 0, 0);
+    }
   }
 
   if constexpr (DBG == 1) {
@@ -643,8 +697,8 @@ __global__ __launch_bounds__(512, 1) void bert_oproj_ln_kernel(const f16* __rest
   }
 }
 
-int g_bert_oproj_ln = 0;  // 1: O-projection + residual + LayerNorm 1 in one kernel (measured slower,
-                          // DESIGN.md §4); 2: its main-loop-only probe build
+int g_bert_oproj_ln = 0;  // 1 / 3: O-projection + residual + LayerNorm 1 in one kernel, Wo through LDS /
+                          // into registers (both measured slower); 2 / 4: probe builds
 
 // ----------------------------------------------------------------------------- model
 // prm layout per layer (floats): bqkv 2304 | bo 768 | ln1g 768 | ln1b 768 | bi 3072 | bo2 768 |
@@ -787,9 +841,18 @@ int TextModel::forward(const int32_t* ids, const int32_t* mask, int B, int L, fl
     // re-runs candidates on the same buffers)
     if (g_bert_oproj_ln && M % OL_BM == 0) {
       MEC_TRY(prof.begin(TAG_BERT_OPROJ, s));
-      if (first)
+      if (first && g_bert_oproj_ln == 3)
+        hipLaunchKernelGGL((bert_oproj_ln_kernel<false, 0, true>), dim3(M / OL_BM), dim3(512), 0, s, ctx16, wo, bo,
+                           h32, nullptr, nullptr, nullptr, g1, b1, t32, h16, st1);
+      else if (first)
         hipLaunchKernelGGL(bert_oproj_ln_kernel<false>, dim3(M / OL_BM), dim3(512), 0, s, ctx16, wo, bo, h32,
                            nullptr, nullptr, nullptr, g1, b1, t32, h16, st1);
+      else if (g_bert_oproj_ln == 3)
+        hipLaunchKernelGGL((bert_oproj_ln_kernel<true, 0, true>), dim3(M / OL_BM), dim3(512), 0, s, ctx16, wo, bo, h32,
+                           st2, pg2, pg2 + BH, g1, b1, t32, h16, st1);
+      else if (g_bert_oproj_ln == 4)
+        hipLaunchKernelGGL((bert_oproj_ln_kernel<true, 1, true>), dim3(M / OL_BM), dim3(512), 0, s, ctx16, wo, bo, h32,
+                           st2, pg2, pg2 + BH, g1, b1, t32, h16, st1);
       else if (g_bert_oproj_ln == 2)
         hipLaunchKernelGGL((bert_oproj_ln_kernel<true, 1>), dim3(M / OL_BM), dim3(512), 0, s, ctx16, wo, bo, h32, st2,
                            pg2, pg2 + BH, g1, b1, t32, h16, st1);

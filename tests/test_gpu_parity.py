@@ -185,8 +185,9 @@ def test_text_qkv_attn_bit_identical(models, dev, B):
         np.testing.assert_array_equal(a, b)
 
 
+@pytest.mark.parametrize('form', [1, 3])  # LDS-staged Wo / Wo read straight into registers
 @pytest.mark.parametrize('B', [1, 3, 9])
-def test_text_oproj_ln_fused_matches_unfused(models, dev, B):
+def test_text_oproj_ln_fused_matches_unfused(models, dev, B, form):
     """BERT with the O-projection + residual + LayerNorm-1 kernel against the O-proj GEMM
     followed by the LayerNorm kernel. The GEMM sums are accumulated in the same k order, but
     the row statistics are summed in another order, so the bar is rounding-level agreement
@@ -196,14 +197,14 @@ def test_text_oproj_ln_fused_matches_unfused(models, dev, B):
     ids, mask = syn.text_inputs(B, 128, seed=400 + B, ragged=True)
     args = (engine.to_device(ids, dev), engine.to_device(mask, dev))
     outs = []
-    for fused in (1, 0):
+    for fused in (form, 0):
         _lib.check(lib.mec_set_option(b'bert_oproj_ln', fused), 'option')
         try:
             outs.append(_np(models['text'].forward(*args)))
         finally:
             lib.mec_set_option(b'bert_oproj_ln', 0)  # the default
     (cf, lf, pf), (cu, lu, pu) = outs
-    print(f'B={B}: cls max|d| {np.abs(cf - cu).max():.3g}, probs max|d| {np.abs(pf - pu).max():.3g}')
+    print(f'form {form} B={B}: cls max|d| {np.abs(cf - cu).max():.3g}, probs max|d| {np.abs(pf - pu).max():.3g}')
     assert np.abs(cf - cu).max() <= 2e-3
     assert np.abs(pf - pu).max() <= 1e-3  # north_star's probs bar; the synthetic head has large logits
     assert (pf.argmax(1) == pu.argmax(1)).all()
