@@ -81,8 +81,11 @@ def load_checkpoint(kind: str):
 def resolve(kind: str, weights=None, seed=None):
     if weights is not None:
         return weights
-    if seed is None and Config.SYNTHETIC_SEED not in (None, ''):
-        seed = int(Config.SYNTHETIC_SEED)
+    if seed is None:
+        # the reference's own config.py (INTEGRATION.md path A) has no SYNTHETIC_SEED
+        env = getattr(Config, 'SYNTHETIC_SEED', None) or os.environ.get('MEC_SYNTHETIC_SEED')
+        if env not in (None, ''):
+            seed = int(env)
     if seed is not None:
         return synthetic.weights(kind, int(seed))
     try:

@@ -140,3 +140,46 @@ def test_text_save_pretrained_loaders(tmp_path, monkeypatch):
     torch.save(small, tmp_path / 'pytorch_model.bin')
     got = checkpoints.resolve('text')
     assert all(np.array_equal(got[k], ref[k]) for k in ref)
+
+
+class _RefConfig:
+    """The reference's config.py attribute set for the hot path (config.py:39-65): no
+    SYNTHETIC_SEED (INTEGRATION.md path A keeps the reference's own Config)."""
+    SPEECH_MODEL_PATH = '/nonexistent/models/speech_model.h5'
+    SPEECH_SCALER_PATH = '/nonexistent/models/speech_scaler.pkl'
+    TEXT_MODEL_PATH = '/nonexistent/models/text_model.h5'
+    IMAGE_MODEL_PATH = '/nonexistent/models/image_model.h5'
+    FUSION_MODEL_PATH = '/nonexistent/models/fusion_model.pkl'
+    BERT_MODEL_PATH = '/nonexistent/models/bert_model'
+    EMOTIONS = ['happy', 'sad', 'angry', 'fear', 'disgust', 'surprise', 'neutral']
+    NUM_EMOTIONS = 7
+    SAMPLE_RATE = 22050
+    AUDIO_DURATION = 3
+    N_MFCC = 40
+    MAX_TEXT_LENGTH = 128
+    IMAGE_SIZE = (224, 224)
+
+
+def test_inference_classes_under_reference_config(monkeypatch):
+    """Every drop-in class constructs with the reference's Config (no SYNTHETIC_SEED) and no
+    checkpoints: model = None and the heuristic fallbacks answer, as in the reference."""
+    import importlib
+    monkeypatch.delenv('MEC_SYNTHETIC_SEED', raising=False)
+    mods = {n: importlib.import_module(f'inference.{n}') for n in
+            ('speech_inference', 'text_inference', 'image_inference', 'multimodal_fusion')}
+    monkeypatch.setattr(checkpoints, 'Config', _RefConfig)
+    for m in mods.values():
+        monkeypatch.setattr(m, 'Config', _RefConfig)
+    s = mods['speech_inference'].SpeechInference()
+    t = mods['text_inference'].TextInference()
+    i = mods['image_inference'].ImageInference()
+    assert s.model is None and t.model is None and i.model is None
+    r = t.predict('I am so happy today')
+    assert r['emotion'] in _RefConfig.EMOTIONS and len(r['all_probabilities']) == 7
+    if torch.cuda.is_available():
+        f = mods['multimodal_fusion'].MultimodalFusion()
+        assert f.fuse_predictions(None, None, None)['emotion'] in _RefConfig.EMOTIONS
+    else:  # its weighted average runs on the GPU: no GPU is a MecError, never an AttributeError
+        from mec._lib import MecError
+        with pytest.raises(MecError):
+            mods['multimodal_fusion'].MultimodalFusion()
