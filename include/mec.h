@@ -46,6 +46,17 @@ long long mec_blob_size(int kind);
  *           (MEC_IMAGE_MBV2: the same with base = mobilenet_v2, base.classifier = the head)
  *   fusion  _build_fusion_model + load_state_dict        inference/multimodal_fusion.py:43-56 */
 int mec_create(int kind, const float* host_blob, size_t n, int device, mec_model** out);
+
+/* Arithmetic of a handle. MEC_PREC_F16 (mec_create's default, the fast path): BERT and the
+ * image backbones on f16 MFMA operands with fp32 accumulation, LayerNorm, softmax, GELU,
+ * residual stream and heads. MEC_PREC_FP32: every operand and product in fp32
+ * (v_mfma_f32_32x32x2_f32, an exact fmaf chain), the precision the reference computes in
+ * (inference/text_inference.py:91-93, inference/image_inference.py:116-118); not available
+ * for MEC_IMAGE_MBV2. Speech and fusion handles are fp32 at either setting. */
+enum { MEC_PREC_F16 = 0, MEC_PREC_FP32 = 1 };
+int mec_create_ex(int kind, const float* host_blob, size_t n, int device, int precision, mec_model** out);
+/* The handle's precision (MEC_PREC_*), -1 on a null handle. */
+int mec_precision(const mec_model* m);
 int mec_destroy(mec_model* m);
 
 /* Speech DNN. x: raw (pre-scaler) features f32[B,56]. Outputs feat f32[B,64] (block-5
@@ -101,6 +112,13 @@ int mec_gemm_f16(const void* A, const void* B, const float* bias, const void* R,
 /* Implicit-GEMM conv on NHWC f16: x[n,H,W,C], w[Cout][ks][ks][C], y[n,OH,OW,Cout]. */
 int mec_conv_f16(const void* x, const void* w, const float* bias, const void* R, void* y, int n, int H, int W,
                  int C, int Cout, int ks, int stride, int pad, int act, void* stream);
+/* fp32 engine (the MEC_PREC_FP32 path): C[M,N] = act(A[M,K] . B[N,K]^T + bias (+ R)), all f32;
+ * K % 32 == 0, N % 64 == 0; act 0 none, 1 relu, 4 gelu (libm erf). */
+int mec_gemm_f32(const float* A, const float* B, const float* bias, const float* R, float* C, int M, int N, int K,
+                 int act, void* stream);
+/* Implicit-GEMM conv on NHWC f32 (C % 32 == 0), same geometry as mec_conv_f16. */
+int mec_conv_f32(const float* x, const float* w, const float* bias, const float* R, float* y, int n, int H, int W,
+                 int C, int Cout, int ks, int stride, int pad, int act, void* stream);
 
 /* Process-wide tuning knobs (A/B benchmarking; defaults in brackets). Every pair of
  * settings of one knob gives bit-identical outputs, except the *_debug probe builds, which
@@ -128,6 +146,8 @@ int mec_set_option(const char* key, int value);
 
 /* Tile width the autotuner chose for a plain (amode 0) or conv (amode 1) GEMM shape; 0 = not yet seen. */
 int mec_gemm_query(int amode, int M, int N, int K);
+/* The same for the fp32 engine: tile id 1 = 256x128 (8 waves), 2 = 128x128, 3 = 128x64, 4 = 256x256. */
+int mec_gemm_f32_query(int amode, int M, int N, int K);
 
 /* hipEvent timing hook: time every launch of kernel class `tag`. */
 int mec_prof_enable(mec_model* m, int tag);

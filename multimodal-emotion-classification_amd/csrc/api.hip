@@ -116,8 +116,20 @@ long long mec_blob_size(int kind) {
 }
 
 int mec_create(int kind, const float* host_blob, size_t n, int device, mec_model** out) {
+  return mec_create_ex(kind, host_blob, n, device, MEC_PREC_F16, out);
+}
+
+int mec_create_ex(int kind, const float* host_blob, size_t n, int device, int precision, mec_model** out) {
   API_GUARD({
     if (!out) { set_error("mec_create: out is null"); return -1; }
+    if (precision != MEC_PREC_F16 && precision != MEC_PREC_FP32) {
+      set_error("mec_create: precision must be MEC_PREC_F16 or MEC_PREC_FP32");
+      return -1;
+    }
+    if (precision == MEC_PREC_FP32 && kind == KIND_IMAGE_MBV2) {
+      set_error("mec_create: MEC_PREC_FP32 is not implemented for the MobileNetV2 backbone");
+      return -1;
+    }
     *out = nullptr;
     const size_t want = blob_floats(kind);
     if (!want) { set_error("mec_create: unknown kind"); return -1; }
@@ -129,15 +141,17 @@ int mec_create(int kind, const float* host_blob, size_t n, int device, mec_model
     Model* impl = nullptr;
     int rc = -1;
     switch (kind) {
+      // speech and fusion are fp32 at either precision
       case KIND_SPEECH: { auto* p = new SpeechModel(); impl = p; rc = p->create(host_blob, n); break; }
-      case KIND_TEXT: { auto* p = new TextModel(); impl = p; rc = p->create(host_blob, n); break; }
-      case KIND_IMAGE: { auto* p = new ImageModel(); impl = p; rc = p->create(host_blob, n); break; }
+      case KIND_TEXT: { auto* p = new TextModel(); p->prec = precision; impl = p; rc = p->create(host_blob, n); break; }
+      case KIND_IMAGE: { auto* p = new ImageModel(); p->prec = precision; impl = p; rc = p->create(host_blob, n); break; }
       case KIND_FUSION: { auto* p = new FusionModel(); impl = p; rc = p->create(host_blob, n); break; }
       case KIND_IMAGE_MBV2: { auto* p = new MobileNetModel(); impl = p; rc = p->create(host_blob, n); break; }
     }
     if (rc != 0) { delete impl; return -1; }
     impl->kind = kind;
     impl->device = device;
+    impl->prec = (kind == KIND_SPEECH || kind == KIND_FUSION) ? MEC_PREC_FP32 : precision;
     *out = new mec_model{impl};
     return 0;
   })
@@ -238,6 +252,7 @@ int mec_set_option(const char* key, int value) {
   if (k == "fusion_split" && (value == 0 || value == 1)) { g_fusion_split = value; return 0; }
   if (k == "gemm_debug" && value >= 0 && value <= 4) { g_gemm_debug = value; return 0; }
   if (k == "gemm_autotune" && (value == 0 || value == 1)) { g_gemm_autotune = value; return 0; }
+  if (k == "gemm_f32_tile" && value >= 0 && value <= 4) { g_gemm_f32_tile = value; return 0; }
   if (k == "gemm_prefetch_r" && (value == 0 || value == 1)) { g_gemm_prefetch_r = value; return 0; }
   if (k == "resnet_fused_tail" && (value == 0 || value == 1)) { g_resnet_fused_tail = value; return 0; }
   if (k == "mbv2_impl" && value >= 0 && value <= 2) { g_mbv2_impl = value; return 0; }
@@ -275,6 +290,34 @@ int mec_set_option(const char* key, int value) {
 }
 
 int mec_gemm_query(int amode, int M, int N, int K) { return gemm_tuned_bn(amode, M, N, K); }
+
+int mec_gemm_f32_query(int amode, int M, int N, int K) { return gemm_f32_tuned(amode, M, N, K); }
+
+int mec_precision(const mec_model* m) {
+  if (!m || !m->impl) { set_error("null model handle"); return -1; }
+  return m->impl->prec;
+}
+
+int mec_gemm_f32(const float* A, const float* B, const float* bias, const float* R, float* C, int M, int N, int K,
+                 int act, void* stream) {
+  API_GUARD({
+    GemmParams g;
+    g.A = A; g.B32 = B; g.bias = bias; g.R = R; g.r_f32 = 1; g.C32 = C; g.M = M; g.N = N; g.K = K; g.act = act;
+    return launch_gemm_f32(g, S(stream), nullptr, TAG_NONE);
+  })
+}
+
+int mec_conv_f32(const float* x, const float* w, const float* bias, const float* R, float* y, int n, int H, int W,
+                 int C, int Cout, int ks, int stride, int pad, int act, void* stream) {
+  API_GUARD({
+    GemmParams g;
+    g.amode = A_CONV; g.A = x; g.B32 = w; g.bias = bias; g.R = R; g.r_f32 = 1; g.C32 = y; g.act = act;
+    g.H = H; g.W = W; g.C = C; g.ks = ks; g.stride = stride; g.pad = pad;
+    g.OH = (H + 2 * pad - ks) / stride + 1; g.OW = (W + 2 * pad - ks) / stride + 1;
+    g.M = n * g.OH * g.OW; g.N = Cout; g.K = ks * ks * C;
+    return launch_gemm_f32(g, S(stream), nullptr, TAG_NONE);
+  })
+}
 
 int mec_prof_enable(mec_model* m, int tag) {
   if (!m || !m->impl) { set_error("null model handle"); return -1; }

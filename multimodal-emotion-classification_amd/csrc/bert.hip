@@ -69,8 +69,10 @@ __global__ __launch_bounds__(256) void bert_embed_ln_kernel(const int32_t* __res
     o.z = (v[4 * j + 2] - mean) * rstd * g[c + 2] + b[c + 2];
     o.w = (v[4 * j + 3] - mean) * rstd * g[c + 3] + b[c + 3];
     *reinterpret_cast<float4*>(h32 + (size_t)row * BH + c) = o;
-    half4 hh = {(f16)o.x, (f16)o.y, (f16)o.z, (f16)o.w};
-    *reinterpret_cast<half4*>(h16 + (size_t)row * BH + c) = hh;
+    if (h16) {  // null on the fp32 path
+      half4 hh = {(f16)o.x, (f16)o.y, (f16)o.z, (f16)o.w};
+      *reinterpret_cast<half4*>(h16 + (size_t)row * BH + c) = hh;
+    }
   }
 }
 
@@ -116,9 +118,31 @@ __global__ __launch_bounds__(256) void bert_layernorm_kernel(const float* x, int
     o.z = __builtin_fmaf((v[4 * j + 2] - mean) * rstd, gg[j].z, bb[j].z);
     o.w = __builtin_fmaf((v[4 * j + 3] - mean) * rstd, gg[j].w, bb[j].w);
     if (h32) *reinterpret_cast<float4*>(h32 + (size_t)row * BH + c) = o;
-    half4 hh = {(f16)o.x, (f16)o.y, (f16)o.z, (f16)o.w};
-    *reinterpret_cast<half4*>(h16 + (size_t)row * BH + c) = hh;
+    if (h16) {  // null on the fp32 path
+      half4 hh = {(f16)o.x, (f16)o.y, (f16)o.z, (f16)o.w};
+      *reinterpret_cast<half4*>(h16 + (size_t)row * BH + c) = hh;
+    }
   }
+}
+
+// Host launchers (also used by the fp32 path, bert_f32.hip). One wave per token row.
+int launch_bert_embed_ln(const int32_t* ids, int M, int L, const float* emb, float* h32, f16* h16, hipStream_t s) {
+  const float* word = emb;
+  const float* pos = word + (size_t)BVOCAB * BH;
+  const float* type = pos + (size_t)BMAXPOS * BH;
+  const float* lng = type + 2 * BH;
+  const float* lnb = lng + BH;
+  hipLaunchKernelGGL(bert_embed_ln_kernel, dim3((M + 3) / 4), dim3(256), 0, s, ids, M, L, word, pos, type, lng, lnb,
+                     h32, h16);
+  MEC_LAUNCH_CHECK();
+  return 0;
+}
+
+int launch_bert_layernorm(const float* x, int M, const float* g, const float* b, float* h32, f16* h16, float2* stats,
+                          hipStream_t s) {
+  hipLaunchKernelGGL(bert_layernorm_kernel, dim3((M + 3) / 4), dim3(256), 0, s, x, M, g, b, h32, h16, stats);
+  MEC_LAUNCH_CHECK();
+  return 0;
 }
 
 // ----------------------------------------------------------------------------- attention
@@ -724,7 +748,14 @@ int TextModel::create(const float* blob, size_t n) {
   e.insert(e.end(), type, type + 2 * BH);
   e.insert(e.end(), lg, lg + BH);
   e.insert(e.end(), lb, lb + BH);
-  std::vector<f16> w(WT_LAYER * BLAYERS);
+  // f16 path: GEMM weights in f16 (wts); fp32 path: the same layout in f32 (wts32)
+  const bool f32 = prec == PREC_FP32;
+  std::vector<f16> w(f32 ? 0 : WT_LAYER * BLAYERS);
+  std::vector<float> w32(f32 ? WT_LAYER * BLAYERS : 0);
+  auto put = [&](size_t off, const float* src, size_t cnt) {
+    if (f32) std::copy(src, src + cnt, w32.begin() + off);
+    else to_f16(w, off, src, cnt);
+  };
   std::vector<float> pr(PRM_LAYER * BLAYERS + (size_t)BH * BH + BH + BH * 7 + 7);
   for (int l = 0; l < BLAYERS; ++l) {
     f16* dummy = nullptr;
@@ -733,17 +764,17 @@ int TextModel::create(const float* blob, size_t n) {
     const size_t po = PRM_LAYER * l;
     // Wqkv rows: query | key | value (torch Linear weight [out,in] = GEMM B [N,K])
     for (int q = 0; q < 3; ++q) {
-      to_f16(w, wo + (size_t)q * BH * BH, rd.take((size_t)BH * BH), (size_t)BH * BH);
+      put(wo + (size_t)q * BH * BH, rd.take((size_t)BH * BH), (size_t)BH * BH);
       const float* bb = rd.take(BH);
       std::copy(bb, bb + BH, pr.begin() + po + q * BH);
     }
-    to_f16(w, wo + (size_t)2304 * BH, rd.take((size_t)BH * BH), (size_t)BH * BH);
+    put(wo + (size_t)2304 * BH, rd.take((size_t)BH * BH), (size_t)BH * BH);
     { const float* x = rd.take(BH); std::copy(x, x + BH, pr.begin() + po + 2304); }
     { const float* x = rd.take(BH); std::copy(x, x + BH, pr.begin() + po + 2304 + 768); }
     { const float* x = rd.take(BH); std::copy(x, x + BH, pr.begin() + po + 2304 + 1536); }
-    to_f16(w, wo + (size_t)2304 * BH + BH * BH, rd.take((size_t)BI * BH), (size_t)BI * BH);
+    put(wo + (size_t)2304 * BH + BH * BH, rd.take((size_t)BI * BH), (size_t)BI * BH);
     { const float* x = rd.take(BI); std::copy(x, x + BI, pr.begin() + po + 2304 + 2304); }
-    to_f16(w, wo + (size_t)2304 * BH + BH * BH + (size_t)BI * BH, rd.take((size_t)BH * BI), (size_t)BH * BI);
+    put(wo + (size_t)2304 * BH + BH * BH + (size_t)BI * BH, rd.take((size_t)BH * BI), (size_t)BH * BI);
     { const float* x = rd.take(BH); std::copy(x, x + BH, pr.begin() + po + 2304 + 2304 + 3072); }
     { const float* x = rd.take(BH); std::copy(x, x + BH, pr.begin() + po + 2304 + 2304 + 3072 + 768); }
     { const float* x = rd.take(BH); std::copy(x, x + BH, pr.begin() + po + 2304 + 2304 + 3072 + 1536); }
@@ -764,7 +795,8 @@ int TextModel::create(const float* blob, size_t n) {
   ho += (size_t)BH * 7;
   std::copy(bc, bc + 7, pr.begin() + ho);
   MEC_TRY(upload(emb, e.data(), e.size() * sizeof(float)));
-  MEC_TRY(upload(wts, w.data(), w.size() * sizeof(f16)));
+  if (f32) MEC_TRY(upload(wts32, w32.data(), w32.size() * sizeof(float)));
+  else MEC_TRY(upload(wts, w.data(), w.size() * sizeof(f16)));
   MEC_TRY(upload(prm, pr.data(), pr.size() * sizeof(float)));
   return 0;
 }
@@ -775,6 +807,7 @@ int TextModel::forward(const int32_t* ids, const int32_t* mask, int B, int L, fl
   if (B == 0) return 0;
   MEC_REQUIRE(L == ATT_L, "text: L must be 128 (padding='max_length', MAX_TEXT_LENGTH=128)");
   MEC_REQUIRE(ids && mask && cls && logits && probs, "text: null pointer");
+  if (prec == PREC_FP32) return forward_f32(ids, mask, B, L, cls, logits, probs, s);
   const int M = B * L;
   // workspace: h32 | t32 (f32 [M,768]) ; h16 | ctx16 (f16 [M,768]) ; qkv16 [M,2304] / i16 [M,3072]
   const size_t need = (size_t)M * BH * 4 * 2 + (size_t)M * BH * 2 * 2 + (size_t)M * BI * 2 + (size_t)B * BH * 4 +

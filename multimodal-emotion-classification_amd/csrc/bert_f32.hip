@@ -1,0 +1,183 @@
+// BERT-base in fp32 end to end (mec_create_ex(..., MEC_PREC_FP32)): the reference's own
+// precision (transformers BertForSequenceClassification in fp32, inference/text_inference.py:
+// 41, :92-93). Every GEMM runs on the fp32 engine (gemm_f32.hip, v_mfma_f32_32x32x2_f32) and
+// the attention on f32 MFMAs; LayerNorm, GELU (libm erff), softmax and the residual stream are
+// fp32 as on the f16 path. Per layer (M = B*L rows):
+//   qkv32 = h32 . Wqkv^T + b                   gemm_f32 (N = 2304)
+//   ctx32 = softmax(QK^T/8 + mask_bias) V      bert_attention_f32_kernel
+//   t32   = ctx32 . Wo^T + bo + h32            gemm_f32, residual fused
+//   h32   = LN(t32)                            bert_layernorm_kernel (f32 out only)
+//   i32   = GELU(h32 . Wi^T + bi)              gemm_f32 (N = 3072), exact erf
+//   t32   = i32 . Wo2^T + bo2 + h32            gemm_f32
+//   h32   = LN(t32)
+// Head as on the f16 path (pooler tanh + classifier + softmax, block_ops.h).
+#include "block_ops.h"
+#include "models.h"
+
+namespace mec {
+
+namespace {
+constexpr int H = 768, FF = 3072, NH = 12, DH = 64, NL = 12, AL = 128;
+constexpr size_t PRM_LAYER = 2304 + 768 * 3 + 3072 + 768 * 3;
+constexpr size_t WT_LAYER = (size_t)2304 * 768 + 768 * 768 + 3072 * 768 + 768 * 3072;
+}  // namespace
+
+// K rows in LDS: 16 chunks of 16 B per 256-B row, chunk c stored at c ^ (row & 15), so the 16
+// rows of a ds_read_b128 lane group cover all 64 banks.
+__device__ __forceinline__ int kswz(int row, int c) { return c ^ (row & 15); }
+
+// One workgroup per (sequence, head), 4 waves; wave w owns queries 32w .. 32w+31.
+// S^T = K Q^T on v_mfma_f32_32x32x2_f32 (A = K rows from LDS, B = Q^T from registers), so each
+// lane holds one query's scores over 64 keys (the other 64 in lane ^ 32): the row softmax is
+// lane-local plus one shuffle. O^T = V^T P^T: A = V[key][d] read as one f32 per lane (row-major
+// V, 32 consecutive d per half wave), B = the lane's own probabilities, in the k order the
+// score tile left them (two keys per MFMA: key f(e) + 4h of block t for lane half h).
+__global__ __launch_bounds__(256, 2) void bert_attention_f32_kernel(const float* __restrict__ qkv,
+                                                                    const int32_t* __restrict__ mask,
+                                                                    float* __restrict__ ctx) {
+  __shared__ __attribute__((aligned(16))) float sK[AL * DH];
+  __shared__ __attribute__((aligned(16))) float sV[AL * DH];
+  __shared__ float sBias[AL];
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int b = blockIdx.x / NH, h = blockIdx.x - (blockIdx.x / NH) * NH;
+  const float* base = qkv + (size_t)b * AL * (3 * H) + h * DH;
+#pragma unroll
+  for (int i = 0; i < 8; ++i) {
+    const int c = tid + 256 * i;
+    const int row = c >> 4, kc = c & 15;
+    const float* src = base + (size_t)row * (3 * H) + kc * 4;
+    const float4 k = *reinterpret_cast<const float4*>(src + H);
+    const float4 v = *reinterpret_cast<const float4*>(src + 2 * H);
+    *reinterpret_cast<float4*>(sK + row * DH + kswz(row, kc) * 4) = k;
+    *reinterpret_cast<float4*>(sV + row * DH + kc * 4) = v;
+  }
+  if (tid < AL) sBias[tid] = mask[(size_t)b * AL + tid] ? 0.f : -3.4028234663852886e38f;  // finfo(f32).min
+  const int lr = lane & 31, lh = lane >> 5;
+  const int q = 32 * wave + lr;
+  float4 qf[8];  // Q[q][8s + 4lh .. +3]
+#pragma unroll
+  for (int s = 0; s < 8; ++s) qf[s] = *reinterpret_cast<const float4*>(base + (size_t)q * (3 * H) + (2 * s + lh) * 4);
+  __syncthreads();
+
+  floatx16 st[4];  // st[t][e] = S[q][key 32t + (e&3) + 8(e>>2) + 4lh]
+#pragma unroll
+  for (int t = 0; t < 4; ++t) {
+#pragma unroll
+    for (int e = 0; e < 16; ++e) st[t][e] = 0.f;
+    const int rk = 32 * t + lr;
+#pragma unroll
+    for (int s = 0; s < 8; ++s) {
+      const float4 kf = *reinterpret_cast<const float4*>(sK + rk * DH + kswz(rk, 2 * s + lh) * 4);
+      st[t] = __builtin_amdgcn_mfma_f32_32x32x2f32(kf.x, qf[s].x, st[t], 0, 0, 0);
+      st[t] = __builtin_amdgcn_mfma_f32_32x32x2f32(kf.y, qf[s].y, st[t], 0, 0, 0);
+      st[t] = __builtin_amdgcn_mfma_f32_32x32x2f32(kf.z, qf[s].z, st[t], 0, 0, 0);
+      st[t] = __builtin_amdgcn_mfma_f32_32x32x2f32(kf.w, qf[s].w, st[t], 0, 0, 0);
+    }
+  }
+  // scores / sqrt(64) + additive mask (HF eager order), softmax over the 128 keys
+  float mx = -INFINITY;
+#pragma unroll
+  for (int t = 0; t < 4; ++t)
+#pragma unroll
+    for (int e = 0; e < 16; ++e) {
+      const int key = 32 * t + (e & 3) + 8 * (e >> 2) + 4 * lh;
+      const float v = st[t][e] * 0.125f + sBias[key];
+      st[t][e] = v;
+      mx = fmaxf(mx, v);
+    }
+  mx = fmaxf(mx, __shfl_xor(mx, 32, 64));
+  float sum = 0.f;
+#pragma unroll
+  for (int t = 0; t < 4; ++t)
+#pragma unroll
+    for (int e = 0; e < 16; ++e) {
+      const float p = expf(st[t][e] - mx);
+      st[t][e] = p;
+      sum += p;
+    }
+  sum += __shfl_xor(sum, 32, 64);
+  const float inv = 1.0f / sum;
+
+  floatx16 o[2];  // o[u][e] = O[q][d = 32u + (e&3) + 8(e>>2) + 4lh]
+#pragma unroll
+  for (int u = 0; u < 2; ++u)
+#pragma unroll
+    for (int e = 0; e < 16; ++e) o[u][e] = 0.f;
+#pragma unroll
+  for (int t = 0; t < 4; ++t)
+#pragma unroll
+    for (int e = 0; e < 16; ++e) {
+      const int key = 32 * t + (e & 3) + 8 * (e >> 2) + 4 * lh;
+      const float p = st[t][e] * inv;
+#pragma unroll
+      for (int u = 0; u < 2; ++u) o[u] = __builtin_amdgcn_mfma_f32_32x32x2f32(sV[key * DH + 32 * u + lr], p, o[u], 0, 0, 0);
+    }
+  float* out = ctx + ((size_t)b * AL + q) * H + h * DH;
+#pragma unroll
+  for (int u = 0; u < 2; ++u)
+#pragma unroll
+    for (int g = 0; g < 4; ++g)
+      *reinterpret_cast<float4*>(out + 32 * u + 8 * g + 4 * lh) =
+          make_float4(o[u][4 * g + 0], o[u][4 * g + 1], o[u][4 * g + 2], o[u][4 * g + 3]);
+}
+
+int TextModel::forward_f32(const int32_t* ids, const int32_t* mask, int B, int L, float* cls, float* logits,
+                           float* probs, hipStream_t s) {
+  MEC_REQUIRE(wts32.p, "text: fp32 weights missing (handle created at f16 precision)");
+  const int M = B * L;
+  // workspace: h32 | t32 | ctx32 (f32 [M,768]) ; big32 f32 [M,3072] (qkv [M,2304], then FFN) ; pooled [B,768]
+  const size_t need = (size_t)M * H * 4 * 3 + (size_t)M * FF * 4 + (size_t)B * H * 4;
+  if (ws.bytes < need) MEC_TRY(ws.ensure(need));
+  char* p = ws.as<char>();
+  float* h32 = reinterpret_cast<float*>(p); p += (size_t)M * H * 4;
+  float* t32 = reinterpret_cast<float*>(p); p += (size_t)M * H * 4;
+  float* ctx32 = reinterpret_cast<float*>(p); p += (size_t)M * H * 4;
+  float* big32 = reinterpret_cast<float*>(p); p += (size_t)M * FF * 4;
+  float* pooled = reinterpret_cast<float*>(p);
+
+  MEC_TRY(launch_bert_embed_ln(ids, M, L, emb.as<float>(), h32, nullptr, s));
+  const float* W = wts32.as<float>();
+  const float* P = prm.as<float>();
+  for (int l = 0; l < NL; ++l) {
+    const float* wqkv = W + WT_LAYER * l;
+    const float* wo = wqkv + (size_t)2304 * H;
+    const float* wi = wo + (size_t)H * H;
+    const float* wo2 = wi + (size_t)FF * H;
+    const float* pl = P + PRM_LAYER * l;
+    const float *bqkv = pl, *bo = pl + 2304, *g1 = pl + 3072, *b1 = pl + 3840, *bi = pl + 4608, *bo2 = pl + 7680,
+                *g2 = pl + 8448, *b2 = pl + 9216;
+    GemmParams g;
+    g.A = h32; g.B32 = wqkv; g.bias = bqkv; g.C32 = big32; g.M = M; g.N = 2304; g.K = H;
+    MEC_TRY(launch_gemm_f32(g, s, &prof, TAG_BERT_QKV));
+    MEC_TRY(prof.begin(TAG_BERT_ATTN, s));
+    hipLaunchKernelGGL(bert_attention_f32_kernel, dim3(B * NH), dim3(256), 0, s, big32, mask, ctx32);
+    MEC_LAUNCH_CHECK();
+    MEC_TRY(prof.end(TAG_BERT_ATTN, s));
+    g = GemmParams();
+    g.A = ctx32; g.B32 = wo; g.bias = bo; g.R = h32; g.r_f32 = 1; g.C32 = t32; g.M = M; g.N = H; g.K = H;
+    MEC_TRY(launch_gemm_f32(g, s, &prof, TAG_BERT_OPROJ));
+    MEC_TRY(prof.begin(TAG_BERT_LN, s));
+    MEC_TRY(launch_bert_layernorm(t32, M, g1, b1, h32, nullptr, nullptr, s));
+    MEC_TRY(prof.end(TAG_BERT_LN, s));
+    g = GemmParams();
+    g.A = h32; g.B32 = wi; g.bias = bi; g.act = ACT_GELU_EXACT; g.C32 = big32; g.M = M; g.N = FF; g.K = H;
+    MEC_TRY(launch_gemm_f32(g, s, &prof, TAG_BERT_FFN1));
+    g = GemmParams();
+    g.A = big32; g.B32 = wo2; g.bias = bo2; g.R = h32; g.r_f32 = 1; g.C32 = t32; g.M = M; g.N = H; g.K = FF;
+    MEC_TRY(launch_gemm_f32(g, s, &prof, TAG_BERT_FFN2));
+    MEC_TRY(prof.begin(TAG_BERT_LN, s));
+    MEC_TRY(launch_bert_layernorm(t32, M, g2, b2, h32, nullptr, nullptr, s));
+    MEC_TRY(prof.end(TAG_BERT_LN, s));
+  }
+  const float* head = P + PRM_LAYER * NL;
+  const float *WpT = head, *bp = WpT + (size_t)H * H, *WcT = bp + H, *bc = WcT + (size_t)H * 7;
+  hipLaunchKernelGGL((linear_rows_kernel<8, 768>), dim3((B + 7) / 8, H / 64), dim3(256), 0, s, h32, (size_t)L * H, B,
+                     H, WpT, bp, H, 64, pooled, H, (int)BACT_TANH, cls, H);
+  MEC_LAUNCH_CHECK();
+  hipLaunchKernelGGL((head_softmax_kernel<8, 768>), dim3((B + 7) / 8), dim3(256), 0, s, pooled, B, H, WcT, bc, logits,
+                     probs);
+  MEC_LAUNCH_CHECK();
+  return 0;
+}
+
+}  // namespace mec

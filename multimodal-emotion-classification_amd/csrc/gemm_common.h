@@ -1,0 +1,207 @@
+// Device helpers shared by the GEMM engines (gemm_glds.hip: f16 operands; gemm_f32.hip:
+// f32 operands): the LDS chunk swizzle, counted vmcnt waits, the erf-GELU and the
+// LDS-staged epilogue. The MFMA C/D layout is the same for the f16 and the f32-input
+// instructions (cdna_hip_programming.md), so one epilogue serves both engines.
+#pragma once
+#include "mec_common.h"
+
+namespace mec {
+
+typedef __attribute__((address_space(3))) void* lds_vptr;
+
+
+// LDS chunk swizzle (16-B chunks): BK=64 rows are 128 B, BK=32 rows are 64 B. Both make
+// every ds_read_b128 lane group of the 32x32x16 and 16x16x32 fragment reads cover the 16
+// slots of a 256-B bank row (MI355X_MICROARCH.md, LDS lane groups).
+template <int BK>
+__device__ __forceinline__ int sw(int row, int kc) {
+  if constexpr (BK == 64) return kc ^ ((row >> 1) & 7);
+  else return kc ^ ((4 - ((row >> 2) & 3)) & 3);
+}
+
+// GELU(x) = x/2 (1 + erf(x/sqrt2)) (HF "gelu"), erf by Abramowitz-Stegun 7.1.26
+// (|err| <= 1.5e-7 absolute over [-12, 12], far below the f16 rounding of FFN1's output).
+// With z = |x|/sqrt2: erf(z) = 1 - t P(t) exp(-z^2), t = 1/(1 + p z), so
+//   GELU(x) = 0.5 (x + |x| (1 - t P(t) exp2(-x^2 log2(e)/2)))      (no sign select)
+// evaluated on pairs with packed f32 math; v_rcp / v_exp are the raw instructions.
+typedef float f32x2 __attribute__((ext_vector_type(2)));
+__device__ __forceinline__ f32x2 gelu_erf_x2(f32x2 x) {
+  const f32x2 ax = {fabsf(x.x), fabsf(x.y)};
+  const f32x2 d = ax * 0.23164189f + 1.0f;                 // 1 + (0.3275911/sqrt2) |x|
+  const f32x2 t = {__builtin_amdgcn_rcpf(d.x), __builtin_amdgcn_rcpf(d.y)};
+  const f32x2 a = (x * x) * -0.72134752f;                  // -x^2 log2(e) / 2
+  const f32x2 e = {__builtin_amdgcn_exp2f(a.x), __builtin_amdgcn_exp2f(a.y)};
+  f32x2 p = t * 1.061405429f - 1.453152027f;
+  p = p * t + 1.421413741f;
+  p = p * t - 0.284496736f;
+  p = p * t + 0.254829592f;
+  const f32x2 q = 1.0f - (p * t) * e;
+  return (ax * q + x) * 0.5f;
+}
+
+template <int N>
+__device__ __forceinline__ void wait_vm() {
+  asm volatile("s_waitcnt vmcnt(%0)" ::"n"(N) : "memory");
+}
+
+// Shared epilogue: accumulators (16x16x32 or 32x32x16 layout, wave tile (BM/WM)x(BN/WN))
+// -> bias, residual, activation -> C16 / C32. `smem` must be free (all waves past the
+// main loop's last LDS read).
+// Epilogue geometry shared with the residual prefetch (gemm_glds_kernel, PRE): a lane covers 8
+// columns (16 B) of RPP-row passes through each 32-row slab of its wave tile.
+template <int BM, int BN, int WM, int WN>
+struct EpiGeom {
+  static constexpr int TM = BM / WM, TN = BN / WN;
+  static constexpr int CPR = TN / 8;      // lanes per row
+  static constexpr int RPP = 64 / CPR;    // rows per pass
+  static constexpr int SLABS = TM / 32;
+  static constexpr int NPS = 32 / RPP;    // passes per slab
+};
+
+template <int BM, int BN, int WM, int WN, int MF, typename accv, int TI, int TJ, int PRE = 0>
+__device__ __forceinline__ void gemm_epilogue(const GemmParams& p, accv (&acc)[TI][TJ], f16* smem, int m0, int n0,
+                                              int wm, int wn, int wave, int lane,
+                                              const half8 (*rpre)[EpiGeom<BM, BN, WM, WN>::NPS] = nullptr,
+                                              const float4 (*rpre32)[EpiGeom<BM, BN, WM, WN>::NPS][2] = nullptr) {
+  constexpr int TM = BM / WM, TN = BN / WN;
+  constexpr int EPI_LD = TN + 4;
+  const int M = p.M, N = p.N;
+  const int lr = lane & 31, lh = lane >> 5;
+  // ---- epilogue: per wave, 32-row slabs staged through LDS (f32), then written with
+  // 8-element chunks where consecutive lanes cover consecutive 16-B pieces of a row
+  // (CPR lanes per row), so every store / residual load instruction covers whole lines.
+  float* stg = reinterpret_cast<float*>(smem) + wave * 32 * EPI_LD;
+  constexpr int CPR = TN / 8;          // lanes per row (8 columns each)
+  constexpr int RPP = 64 / CPR;        // rows per pass
+  const int ech = lane % CPR, erow = lane / CPR;
+  const int col0 = n0 + wn * TN + ech * 8;
+  float bias[8];
+#pragma unroll
+  for (int q = 0; q < 8; ++q) bias[q] = 0.f;
+  if (p.bias) {
+    const float4 b0 = *reinterpret_cast<const float4*>(p.bias + col0);
+    const float4 b1 = *reinterpret_cast<const float4*>(p.bias + col0 + 4);
+    bias[0] = b0.x; bias[1] = b0.y; bias[2] = b0.z; bias[3] = b0.w;
+    bias[4] = b1.x; bias[5] = b1.y; bias[6] = b1.z; bias[7] = b1.w;
+  }
+  float lng[8], lnb[8];
+  if (p.r_stats) {
+#pragma unroll
+    for (int q = 0; q < 8; ++q) { lng[q] = p.r_g[col0 + q]; lnb[q] = p.r_b[col0 + q]; }
+  }
+  constexpr int SLABS = TM / 32;
+#pragma unroll
+  for (int i = 0; i < SLABS; ++i) {
+    if constexpr (MF == 32) {
+#pragma unroll
+      for (int j = 0; j < TJ; ++j)
+#pragma unroll
+        for (int e = 0; e < 16; ++e) {
+          const int rr = (e & 3) + 8 * (e >> 2) + 4 * lh;
+          stg[rr * EPI_LD + j * 32 + lr] = acc[i][j][e];
+        }
+    } else {  // 16x16 D layout: col = lane&15, row = 4(lane>>4) + e
+#pragma unroll
+      for (int a = 0; a < 2; ++a)
+#pragma unroll
+        for (int j = 0; j < TJ; ++j)
+#pragma unroll
+          for (int e = 0; e < 4; ++e)
+            stg[(16 * a + 4 * (lane >> 4) + e) * EPI_LD + j * 16 + (lane & 15)] = acc[2 * i + a][j][e];
+    }
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+    constexpr int NPS = 32 / RPP;
+    float rv[NPS][8];
+    if (PRE == 1) {  // f16 residual already in registers (loaded before the main loop)
+#pragma unroll
+      for (int ps = 0; ps < NPS; ++ps)
+#pragma unroll
+        for (int q = 0; q < 8; ++q) rv[ps][q] = (float)rpre[i][ps][q];
+    } else if (PRE == 2) {  // f32 residual already in registers; deferred LayerNorm applied here
+#pragma unroll
+      for (int ps = 0; ps < NPS; ++ps) {
+        const float4 r0 = rpre32[i][ps][0], r1 = rpre32[i][ps][1];
+        rv[ps][0] = r0.x; rv[ps][1] = r0.y; rv[ps][2] = r0.z; rv[ps][3] = r0.w;
+        rv[ps][4] = r1.x; rv[ps][5] = r1.y; rv[ps][6] = r1.z; rv[ps][7] = r1.w;
+        if (p.r_stats) {
+          const int row = min(m0 + wm * TM + i * 32 + ps * RPP + erow, M - 1);
+          const float2 st = p.r_stats[row];
+#pragma unroll
+          for (int q = 0; q < 8; ++q) rv[ps][q] = __builtin_fmaf((rv[ps][q] - st.x) * st.y, lng[q], lnb[q]);
+        }
+      }
+    } else if (p.R) {  // issue every residual load of the slab before any is consumed
+#pragma unroll
+      for (int ps = 0; ps < NPS; ++ps) {
+        const int row = min(m0 + wm * TM + i * 32 + ps * RPP + erow, M - 1);
+        const size_t base = (size_t)row * N + col0;
+        if (p.r_f32) {
+          const float* R = reinterpret_cast<const float*>(p.R) + base;
+          const float4 r0 = *reinterpret_cast<const float4*>(R);
+          const float4 r1 = *reinterpret_cast<const float4*>(R + 4);
+          rv[ps][0] = r0.x; rv[ps][1] = r0.y; rv[ps][2] = r0.z; rv[ps][3] = r0.w;
+          rv[ps][4] = r1.x; rv[ps][5] = r1.y; rv[ps][6] = r1.z; rv[ps][7] = r1.w;
+          if (p.r_stats) {
+            const float2 st = p.r_stats[row];
+#pragma unroll
+            for (int q = 0; q < 8; ++q) rv[ps][q] = __builtin_fmaf((rv[ps][q] - st.x) * st.y, lng[q], lnb[q]);
+          }
+        } else {
+          const half8 r8 = *reinterpret_cast<const half8*>(reinterpret_cast<const f16*>(p.R) + base);
+#pragma unroll
+          for (int q = 0; q < 8; ++q) rv[ps][q] = (float)r8[q];
+        }
+      }
+    } else {
+#pragma unroll
+      for (int ps = 0; ps < NPS; ++ps)
+#pragma unroll
+        for (int q = 0; q < 8; ++q) rv[ps][q] = 0.f;
+    }
+#pragma unroll
+    for (int ps = 0; ps < NPS; ++ps) {
+      const int sr = ps * RPP + erow;
+      const int row = m0 + wm * TM + i * 32 + sr;
+      float v[8];
+      const float4 x0 = *reinterpret_cast<const float4*>(stg + sr * EPI_LD + ech * 8);
+      const float4 x1 = *reinterpret_cast<const float4*>(stg + sr * EPI_LD + ech * 8 + 4);
+      v[0] = x0.x + bias[0]; v[1] = x0.y + bias[1]; v[2] = x0.z + bias[2]; v[3] = x0.w + bias[3];
+      v[4] = x1.x + bias[4]; v[5] = x1.y + bias[5]; v[6] = x1.z + bias[6]; v[7] = x1.w + bias[7];
+#pragma unroll
+      for (int q = 0; q < 8; ++q) v[q] += rv[ps][q];
+      if (p.act == ACT_RELU) {
+#pragma unroll
+        for (int q = 0; q < 8; ++q) v[q] = fmaxf(v[q], 0.f);
+      } else if (p.act == ACT_RELU6) {
+#pragma unroll
+        for (int q = 0; q < 8; ++q) v[q] = fminf(fmaxf(v[q], 0.f), 6.f);
+      } else if (p.act == ACT_GELU) {
+#pragma unroll
+        for (int q = 0; q < 8; q += 2) {
+          const f32x2 r = gelu_erf_x2(f32x2{v[q], v[q + 1]});
+          v[q] = r.x;
+          v[q + 1] = r.y;
+        }
+      } else if (p.act == ACT_GELU_EXACT) {
+#pragma unroll
+        for (int q = 0; q < 8; ++q) v[q] = (v[q] * 0.5f) * (1.0f + erff(v[q] * 0.70710678118654752f));
+      }
+      if (row < M) {
+        const size_t base = (size_t)row * N + col0;
+        if (p.C16) {
+          half8 h;
+#pragma unroll
+          for (int q = 0; q < 8; ++q) h[q] = (f16)v[q];
+          *reinterpret_cast<half8*>(p.C16 + base) = h;
+        }
+        if (p.C32) {
+          *reinterpret_cast<float4*>(p.C32 + base) = make_float4(v[0], v[1], v[2], v[3]);
+          *reinterpret_cast<float4*>(p.C32 + base + 4) = make_float4(v[4], v[5], v[6], v[7]);
+        }
+      }
+    }
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+  }
+}
+
+}  // namespace mec

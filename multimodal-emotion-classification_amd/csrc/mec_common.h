@@ -102,11 +102,14 @@ struct BlobReader {
 // C[M,N] = epilogue( A'[M,K] . B[N,K]^T ), A' = A (plain) or the im2col view of an NHWC
 // tensor (conv).
 enum AMode : int { A_PLAIN = 0, A_CONV = 1, A_DUAL = 2 };
-enum Act : int { ACT_NONE = 0, ACT_RELU = 1, ACT_GELU = 2, ACT_RELU6 = 3 };
+// ACT_GELU: the packed A&S erf form (f16 path, |err| <= 2.1e-7); ACT_GELU_EXACT: libm erff,
+// x * 0.5 * (1 + erf(x / sqrt2)) as torch's CPU gelu kernel orders it (fp32 path)
+enum Act : int { ACT_NONE = 0, ACT_RELU = 1, ACT_GELU = 2, ACT_RELU6 = 3, ACT_GELU_EXACT = 4 };
 
 struct GemmParams {
   const void* A = nullptr;   // f16 [M,K] | f16 NHWC [n,H,W,C]
   const f16* B = nullptr;    // f16 [N,K], K contiguous
+  const float* B32 = nullptr;   // f32 [N,K] (fp32 engine, gemm_f32.hip; A is then f32 too)
   const float* bias = nullptr;  // [N]
   const void* R = nullptr;      // residual [M,N] (f16 or f32) or null
   int r_f32 = 0;
@@ -140,5 +143,9 @@ int launch_conv3x3_c64(const f16* x, const f16* w, const float* bias, f16* y, in
 extern int g_conv3x3_direct;
 extern int g_conv3x3_debug;
 int gemm_tuned_bn(int amode, int M, int N, int K);
+// fp32 engine (gemm_f32.hip): f32 A (plain or NHWC conv) and B32, v_mfma_f32_32x32x2_f32
+int launch_gemm_f32(const GemmParams& p, hipStream_t s, Prof* prof, int tag);
+int gemm_f32_tuned(int amode, int M, int N, int K);
+extern int g_gemm_f32_tile;
 
 }  // namespace mec

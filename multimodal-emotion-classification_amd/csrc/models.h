@@ -10,9 +10,15 @@ enum ModelKind : int { KIND_SPEECH = 0, KIND_TEXT = 1, KIND_IMAGE = 2, KIND_FUSI
 
 size_t blob_floats(int kind);
 
+// Arithmetic of a handle (mec_create_ex): PREC_F16 = f16 MFMA operands with fp32
+// accumulation / LayerNorm / softmax / residual stream (the fast path); PREC_FP32 = every
+// operand and product in fp32 (v_mfma_f32_32x32x2_f32), the reference's own precision.
+enum Precision : int { PREC_F16 = 0, PREC_FP32 = 1 };
+
 struct Model {
   int kind = -1;
   int device = 0;
+  int prec = PREC_F16;
   Prof prof;
   virtual ~Model() {}
 };
@@ -45,12 +51,18 @@ struct TextModel : Model {
   DevBuf emb;      // fp32 word | pos | type | ln_g | ln_b
   DevBuf wts;      // f16 per layer: Wqkv[2304x768] Wo[768x768] Wi[3072x768] Wo2[768x3072]
   DevBuf prm;      // fp32 per layer: bqkv bo ln1g ln1b bi bo2 ln2g ln2b ; head: WpT bp WcT bc
+  DevBuf wts32;    // fp32 path: the same GEMM weights in f32
   DevBuf ws;       // workspace
   int ws_tokens = 0;
   int create(const float* blob, size_t n);
   int forward(const int32_t* ids, const int32_t* mask, int B, int L, float* cls, float* logits,
               float* probs, hipStream_t s);
+  int forward_f32(const int32_t* ids, const int32_t* mask, int B, int L, float* cls, float* logits,
+                  float* probs, hipStream_t s);  // bert_f32.hip
 };
+int launch_bert_embed_ln(const int32_t* ids, int M, int L, const float* emb, float* h32, f16* h16, hipStream_t s);
+int launch_bert_layernorm(const float* x, int M, const float* g, const float* b, float* h32, f16* h16, float2* stats,
+                          hipStream_t s);
 
 // ---------------------------------------------------------------- image encoders
 // Both backbones take the same u8 inputs and produce the same (512-d feature, logits, probs).
@@ -84,9 +96,15 @@ struct ImageModel : ImageNet {
   size_t stem_corr_off = 0;  // f32 [16 border classes][64] -mean/std term
   std::vector<Bottleneck> blocks;
   size_t fc1_off = 0, fc1b_off = 0, fc2_off = 0, fc2b_off = 0;
+  // fp32 path (resnet_f32.hip): f32 weights, same [Cout][kh][kw][Cin] layout; the stem is a
+  // [64][160] GEMM over an explicit im2col of the normalized image (k = c*49 + kh*7 + kw)
+  DevBuf wts32;
   int create(const float* blob, size_t n);
+  int create_f32(const float* blob, size_t n);
   int forward_u8(const uint8_t* img, int B, int H, int W, int C, float* feat, float* logits, float* probs,
                  hipStream_t s) override;
+  int forward_f32(const uint8_t* img, int B, int H, int W, int C, float* feat, float* logits, float* probs,
+                  hipStream_t s);
 };
 
 // ---------------------------------------------------------------- MobileNetV2 + head

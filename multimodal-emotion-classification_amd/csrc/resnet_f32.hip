@@ -1,0 +1,267 @@
+// ResNet50 image path in fp32 end to end (mec_create_ex(..., MEC_PREC_FP32)), the reference's
+// own precision (inference/image_inference.py:28-32 transform, :55-65 network + head):
+//   resize      PIL-exact u8 bilinear 48 -> 224 (resnet.hip, shared with the f16 path)
+//   stem        explicit im2col of ToTensor + Normalize (x / 255 - mean) / std, exactly as
+//               torchvision computes it, k = c*49 + kh*7 + kw (the torch weight order), K
+//               padded 147 -> 160; then one fp32 GEMM [B*112*112, 160] x [64, 160]^T + BN + ReLU
+//   maxpool     3x3/2 pad 1, NHWC f32
+//   bottlenecks conv1 / conv2 (3x3, stride on the 3x3: v1.5) / conv3 + residual (identity or
+//               the 1x1/s downsample GEMM) + ReLU, all on gemm_f32 (A_PLAIN / A_CONV), BN
+//               folded into f32 weights and bias
+//   avgpool     NHWC f32 -> [B, 2048]; head as on the f16 path (fc1 + ReLU = 512-d feature,
+//               fc2, softmax; block_ops.h)
+#include <algorithm>
+#include <cmath>
+
+#include "block_ops.h"
+#include "models.h"
+
+namespace mec {
+
+namespace {
+constexpr int STEM_K = 160;  // 3 * 49 = 147 taps, zero-padded to a multiple of 32
+const int kLayers32[4][3] = {{64, 3, 1}, {128, 4, 2}, {256, 6, 2}, {512, 3, 2}};
+}  // namespace
+
+// One thread per 4 consecutive k of one output pixel's im2col row. img: u8 [B,224,224,C]
+// (C = 1: the gray image replicated to RGB by convert('RGB'); C = 3: RGB).
+__global__ __launch_bounds__(256) void stem_im2col_f32_kernel(const uint8_t* __restrict__ img, int B, int C,
+                                                              float* __restrict__ A) {
+  const size_t idx = (size_t)blockIdx.x * 256 + threadIdx.x;
+  const size_t total = (size_t)B * 112 * 112 * (STEM_K / 4);
+  if (idx >= total) return;
+  const int q = (int)(idx % (STEM_K / 4));
+  const size_t m = idx / (STEM_K / 4);
+  const int ow = (int)(m % 112), oh = (int)((m / 112) % 112);
+  const size_t b = m / (112 * 112);
+  const float mean[3] = {0.485f, 0.456f, 0.406f}, stdv[3] = {0.229f, 0.224f, 0.225f};
+  float v[4];
+#pragma unroll
+  for (int j = 0; j < 4; ++j) {
+    const int k = 4 * q + j;
+    float x = 0.f;
+    if (k < 147) {
+      const int c = k / 49, tap = k - c * 49, kh = tap / 7, kw = tap - kh * 7;
+      const int ih = 2 * oh - 3 + kh, iw = 2 * ow - 3 + kw;
+      if (ih >= 0 && ih < 224 && iw >= 0 && iw < 224) {
+        const uint8_t px = img[((b * 224 + ih) * 224 + iw) * C + (C == 3 ? c : 0)];
+        x = ((float)px / 255.0f - mean[c]) / stdv[c];  // ToTensor, then Normalize (sub_, div_)
+      }
+    }
+    v[j] = x;
+  }
+  *reinterpret_cast<float4*>(A + m * STEM_K + 4 * q) = make_float4(v[0], v[1], v[2], v[3]);
+}
+
+// MaxPool2d(3, 2, 1) on NHWC f32 [B,H,H,C] -> [B,OH,OH,C]; one thread per 4 channels.
+__global__ __launch_bounds__(256) void maxpool_f32_kernel(const float* __restrict__ x, int B, int Hin, int C, int OH,
+                                                          float* __restrict__ y) {
+  const size_t idx = (size_t)blockIdx.x * 256 + threadIdx.x;
+  const int C4 = C / 4;
+  const size_t total = (size_t)B * OH * OH * C4;
+  if (idx >= total) return;
+  const int c4 = (int)(idx % C4);
+  const size_t pix = idx / C4;
+  const int ow = (int)(pix % OH), oh = (int)((pix / OH) % OH);
+  const size_t b = pix / ((size_t)OH * OH);
+  float4 m = make_float4(-INFINITY, -INFINITY, -INFINITY, -INFINITY);
+  for (int dy = 0; dy < 3; ++dy) {
+    const int ih = 2 * oh - 1 + dy;
+    if (ih < 0 || ih >= Hin) continue;
+    for (int dx = 0; dx < 3; ++dx) {
+      const int iw = 2 * ow - 1 + dx;
+      if (iw < 0 || iw >= Hin) continue;
+      const float4 v = *reinterpret_cast<const float4*>(x + ((b * Hin + ih) * Hin + iw) * C + 4 * c4);
+      m.x = fmaxf(m.x, v.x); m.y = fmaxf(m.y, v.y); m.z = fmaxf(m.z, v.z); m.w = fmaxf(m.w, v.w);
+    }
+  }
+  *reinterpret_cast<float4*>(y + idx * 4) = m;
+}
+
+// AdaptiveAvgPool2d(1) on NHWC f32 [B, HW, C] -> [B, C]; grid (B, C / 256).
+__global__ __launch_bounds__(256) void avgpool_f32_kernel(const float* __restrict__ x, int HW, int C,
+                                                          float* __restrict__ y) {
+  const int b = blockIdx.x, c = blockIdx.y * 256 + threadIdx.x;
+  if (c >= C) return;
+  const float* p = x + (size_t)b * HW * C + c;
+  float s = 0.f;
+  for (int q = 0; q < HW; ++q) s += p[(size_t)q * C];
+  y[(size_t)b * C + c] = s / (float)HW;
+}
+
+int ImageModel::create_f32(const float* blob, size_t n) {
+  BlobReader rd(blob, n);
+  std::vector<float> w;
+  std::vector<float> pr;
+  auto bn_fold = [&](int c, std::vector<float>& scale) {
+    const float* g = rd.take(c);
+    const float* b = rd.take(c);
+    const float* rm = rd.take(c);
+    const float* rv = rd.take(c);
+    scale.resize(c);
+    const size_t off = pr.size();
+    for (int i = 0; i < c; ++i) {
+      const double sc = (double)g[i] / std::sqrt((double)rv[i] + 1e-5);
+      scale[i] = (float)sc;
+      pr.push_back((float)((double)b[i] - (double)rm[i] * sc));
+    }
+    return off;
+  };
+  auto conv = [&](int cout, int cin, int ks, int stride, int pad) {
+    ConvLayer L;
+    L.cin = cin; L.cout = cout; L.ks = ks; L.stride = stride; L.pad = pad;
+    const float* src = rd.take((size_t)cout * cin * ks * ks);
+    std::vector<float> scale;
+    L.b_off = bn_fold(cout, scale);
+    L.w_off = w.size();
+    w.resize(w.size() + (size_t)cout * cin * ks * ks);
+    if (!rd.ok) return L;
+    for (int o = 0; o < cout; ++o)
+      for (int kh = 0; kh < ks; ++kh)
+        for (int kw = 0; kw < ks; ++kw)
+          for (int c = 0; c < cin; ++c)
+            w[L.w_off + (((size_t)o * ks + kh) * ks + kw) * cin + c] =
+                (float)((double)src[(((size_t)o * cin + c) * ks + kh) * ks + kw] * scale[o]);
+    return L;
+  };
+  {  // stem: [64][160], k = c*49 + kh*7 + kw (torch [64][3][7][7] order), BN scale folded
+    const float* src = rd.take((size_t)64 * 3 * 49);
+    std::vector<float> scale;
+    stem.b_off = bn_fold(64, scale);
+    stem.cin = 3; stem.cout = 64; stem.ks = 7; stem.stride = 2; stem.pad = 3;
+    stem.w_off = w.size();
+    w.resize(w.size() + (size_t)64 * STEM_K, 0.f);
+    if (rd.ok)
+      for (int o = 0; o < 64; ++o)
+        for (int k = 0; k < 147; ++k) w[stem.w_off + (size_t)o * STEM_K + k] = (float)((double)src[o * 147 + k] * scale[o]);
+  }
+  blocks.clear();
+  int cin = 64;
+  for (int li = 0; li < 4; ++li) {
+    const int wd = kLayers32[li][0], nb = kLayers32[li][1], st = kLayers32[li][2];
+    for (int b = 0; b < nb; ++b) {
+      Bottleneck bk;
+      const int s = b == 0 ? st : 1;
+      bk.c1 = conv(wd, cin, 1, 1, 0);
+      bk.c2 = conv(wd, wd, 3, s, 1);
+      bk.c3 = conv(4 * wd, wd, 1, 1, 0);
+      if (b == 0) {
+        bk.has_ds = true;
+        bk.ds = conv(4 * wd, cin, 1, s, 0);
+      }
+      blocks.push_back(bk);
+      cin = 4 * wd;
+    }
+  }
+  const float* f1w = rd.take((size_t)512 * 2048);
+  const float* f1b = rd.take(512);
+  const float* f2w = rd.take((size_t)7 * 512);
+  const float* f2b = rd.take(7);
+  MEC_REQUIRE(rd.ok && rd.off == n, "image blob size mismatch");
+  fc1_off = pr.size();
+  pr.resize(pr.size() + (size_t)2048 * 512);
+  for (int i = 0; i < 2048; ++i)
+    for (int j = 0; j < 512; ++j) pr[fc1_off + (size_t)i * 512 + j] = f1w[(size_t)j * 2048 + i];
+  fc1b_off = pr.size();
+  pr.insert(pr.end(), f1b, f1b + 512);
+  fc2_off = pr.size();
+  pr.resize(pr.size() + 512 * 7);
+  for (int i = 0; i < 512; ++i)
+    for (int j = 0; j < 7; ++j) pr[fc2_off + (size_t)i * 7 + j] = f2w[(size_t)j * 512 + i];
+  fc2b_off = pr.size();
+  pr.insert(pr.end(), f2b, f2b + 7);
+  MEC_TRY(upload(wts32, w.data(), w.size() * sizeof(float)));
+  MEC_TRY(upload(prm, pr.data(), pr.size() * sizeof(float)));
+  return 0;
+}
+
+int ImageModel::forward_f32(const uint8_t* img, int B, int H, int W, int C, float* feat, float* logits, float* probs,
+                            hipStream_t s) {
+  MEC_REQUIRE(wts32.p, "image: fp32 weights missing (handle created at f16 precision)");
+  const bool fer = (H == 48 && W == 48 && C == 1);
+  // per image (floats): im2col 12544 x 160; X, Y, DS 56*56*256 (also the 112*112*64 stem
+  // output); T1 56*56*128; T2 56*56*64; pooled 2048
+  const size_t big = (size_t)56 * 56 * 256;
+  const size_t per_img = 224 * 224 + ((size_t)12544 * STEM_K + 3 * big + 56 * 56 * 128 + 56 * 56 * 64 + 2048) * 4;
+  const size_t need = per_img * (size_t)B + 8192;
+  if (ws.bytes < need) MEC_TRY(ws.ensure(need));
+  char* p = ws.as<char>();
+  uint8_t* resized = reinterpret_cast<uint8_t*>(p);
+  p += ((size_t)B * 224 * 224 + 255) / 256 * 256;
+  float* A0 = reinterpret_cast<float*>(p); p += (size_t)B * 12544 * STEM_K * 4;
+  float* X = reinterpret_cast<float*>(p); p += (size_t)B * big * 4;
+  float* Y = reinterpret_cast<float*>(p); p += (size_t)B * big * 4;
+  float* DS = reinterpret_cast<float*>(p); p += (size_t)B * big * 4;
+  float* T1 = reinterpret_cast<float*>(p); p += (size_t)B * 56 * 56 * 128 * 4;
+  float* T2 = reinterpret_cast<float*>(p); p += (size_t)B * 56 * 56 * 64 * 4;
+  float* pooled = reinterpret_cast<float*>(p);
+
+  const float* Wt = wts32.as<float>();
+  const float* P = prm.as<float>();
+  const uint8_t* stem_in = img;
+  int Cin = C;
+  if (fer) {
+    MEC_TRY(resize_u8(img, B, 48, 48, resized, 224, 224, s));
+    stem_in = resized;
+    Cin = 1;
+  }
+  MEC_TRY(prof.begin(TAG_RESNET_STEM, s));
+  {
+    const size_t total = (size_t)B * 112 * 112 * (STEM_K / 4);
+    hipLaunchKernelGGL(stem_im2col_f32_kernel, dim3((unsigned)((total + 255) / 256)), dim3(256), 0, s, stem_in, B, Cin,
+                       A0);
+    MEC_LAUNCH_CHECK();
+  }
+  MEC_TRY(prof.end(TAG_RESNET_STEM, s));
+  GemmParams g;
+  g.A = A0; g.B32 = Wt + stem.w_off; g.bias = P + stem.b_off; g.act = ACT_RELU; g.C32 = Y;
+  g.M = B * 112 * 112; g.N = 64; g.K = STEM_K;
+  MEC_TRY(launch_gemm_f32(g, s, &prof, TAG_RESNET_STEM));
+  {
+    const size_t total = (size_t)B * 56 * 56 * 16;
+    hipLaunchKernelGGL(maxpool_f32_kernel, dim3((unsigned)((total + 255) / 256)), dim3(256), 0, s, Y, B, 112, 64, 56, X);
+    MEC_LAUNCH_CHECK();
+  }
+  float* cur = X;
+  float* other = Y;
+  int Hc = 56;
+  for (const Bottleneck& bk : blocks) {
+    const int wd = bk.c1.cout, cin = bk.c1.cin, st = bk.c2.stride;
+    const int OH = (Hc + 2 - 3) / st + 1;
+    g = GemmParams();
+    g.A = cur; g.B32 = Wt + bk.c1.w_off; g.bias = P + bk.c1.b_off; g.act = ACT_RELU; g.C32 = T1;
+    g.M = B * Hc * Hc; g.N = wd; g.K = cin;
+    MEC_TRY(launch_gemm_f32(g, s, &prof, TAG_RESNET_CONV1X1));
+    g = GemmParams();
+    g.amode = A_CONV; g.A = T1; g.B32 = Wt + bk.c2.w_off; g.bias = P + bk.c2.b_off; g.act = ACT_RELU; g.C32 = T2;
+    g.M = B * OH * OH; g.N = wd; g.K = 9 * wd;
+    g.H = Hc; g.W = Hc; g.C = wd; g.OH = OH; g.OW = OH; g.ks = 3; g.stride = st; g.pad = 1;
+    MEC_TRY(launch_gemm_f32(g, s, &prof, TAG_RESNET_CONV3X3));
+    const float* idn = cur;
+    if (bk.has_ds) {  // downsample = BN(conv1x1/s(x)), no activation
+      g = GemmParams();
+      g.amode = A_CONV; g.A = cur; g.B32 = Wt + bk.ds.w_off; g.bias = P + bk.ds.b_off; g.C32 = DS;
+      g.M = B * OH * OH; g.N = 4 * wd; g.K = cin;
+      g.H = Hc; g.W = Hc; g.C = cin; g.OH = OH; g.OW = OH; g.ks = 1; g.stride = st; g.pad = 0;
+      MEC_TRY(launch_gemm_f32(g, s, &prof, TAG_RESNET_CONV1X1));
+      idn = DS;
+    }
+    g = GemmParams();  // relu(bn3(conv3(t2)) + identity)
+    g.A = T2; g.B32 = Wt + bk.c3.w_off; g.bias = P + bk.c3.b_off; g.R = idn; g.r_f32 = 1; g.act = ACT_RELU;
+    g.C32 = other; g.M = B * OH * OH; g.N = 4 * wd; g.K = wd;
+    MEC_TRY(launch_gemm_f32(g, s, &prof, TAG_RESNET_CONV1X1));
+    std::swap(cur, other);
+    Hc = OH;
+  }
+  hipLaunchKernelGGL(avgpool_f32_kernel, dim3(B, 2048 / 256), dim3(256), 0, s, cur, Hc * Hc, 2048, pooled);
+  MEC_LAUNCH_CHECK();
+  hipLaunchKernelGGL((linear_rows_kernel<8, 2048>), dim3((B + 7) / 8, 512 / 64), dim3(256), 0, s, pooled, (size_t)2048,
+                     B, 2048, P + fc1_off, P + fc1b_off, 512, 64, feat, 512, (int)BACT_RELU, (float*)nullptr, 0);
+  MEC_LAUNCH_CHECK();
+  hipLaunchKernelGGL((head_softmax_kernel<8, 768>), dim3((B + 7) / 8), dim3(256), 0, s, feat, B, 512, P + fc2_off,
+                     P + fc2b_off, logits, probs);
+  MEC_LAUNCH_CHECK();
+  return 0;
+}
+
+}  // namespace mec

@@ -21,6 +21,8 @@ SIGNATURES = {
     'mec_last_error': (ctypes.c_char_p, []),
     'mec_blob_size': (ctypes.c_longlong, [c_int]),
     'mec_create': (c_int, [c_int, c_fp, ctypes.c_size_t, c_int, ctypes.POINTER(c_vp)]),
+    'mec_create_ex': (c_int, [c_int, c_fp, ctypes.c_size_t, c_int, c_int, ctypes.POINTER(c_vp)]),
+    'mec_precision': (c_int, [c_vp]),
     'mec_destroy': (c_int, [c_vp]),
     'mec_speech_fwd': (c_int, [c_vp, c_vp, c_int, c_vp, c_vp, c_vp, c_vp]),
     'mec_text_fwd': (c_int, [c_vp, c_vp, c_vp, c_int, c_int, c_vp, c_vp, c_vp, c_vp]),
@@ -33,8 +35,12 @@ SIGNATURES = {
     'mec_gemm_f16': (c_int, [c_vp, c_vp, c_vp, c_vp, c_int, c_vp, c_vp, c_int, c_int, c_int, c_int, c_vp]),
     'mec_conv_f16': (c_int, [c_vp, c_vp, c_vp, c_vp, c_vp, c_int, c_int, c_int, c_int, c_int, c_int, c_int,
                              c_int, c_int, c_vp]),
+    'mec_gemm_f32': (c_int, [c_vp, c_vp, c_vp, c_vp, c_vp, c_int, c_int, c_int, c_int, c_vp]),
+    'mec_conv_f32': (c_int, [c_vp, c_vp, c_vp, c_vp, c_vp, c_int, c_int, c_int, c_int, c_int, c_int, c_int,
+                             c_int, c_int, c_vp]),
     'mec_set_option': (c_int, [ctypes.c_char_p, c_int]),
     'mec_gemm_query': (c_int, [c_int, c_int, c_int, c_int]),
+    'mec_gemm_f32_query': (c_int, [c_int, c_int, c_int, c_int]),
     'mec_prof_enable': (c_int, [c_vp, c_int]),
     'mec_prof_read': (c_int, [c_vp, c_dp, ctypes.POINTER(c_int)]),
 }
@@ -43,6 +49,11 @@ SIGNATURES = {
 TAGS = {'bert_qkv': 1, 'bert_attn': 2, 'bert_oproj': 3, 'bert_ffn1': 4, 'bert_ffn2': 5, 'bert_ln': 6,
         'resnet_conv3x3': 7, 'resnet_conv1x1': 8, 'resnet_stem': 9, 'speech': 10, 'fusion': 11,
         'mbv2_blocks': 12, 'mbv2_last': 13}
+
+
+# Handle precision (include/mec.h MEC_PREC_*): 'f16' = f16 MFMA operands with fp32
+# accumulation / LayerNorm / softmax / residual (the fast path), 'fp32' = fp32 throughout.
+PRECISIONS = {'f16': 0, 'fp32': 1}
 
 
 class MecError(RuntimeError):

@@ -56,9 +56,12 @@ class HipModel:
 
     kind: str = ''
 
-    def __init__(self, weights=None, seed: int = 1234, device=None):
+    def __init__(self, weights=None, seed: int = 1234, device=None, precision: str = 'f16'):
+        if precision not in _lib.PRECISIONS:
+            raise ValueError(f"precision must be one of {sorted(_lib.PRECISIONS)}, got {precision!r}")
         self.lib = _lib.load()
         self.device = require_gpu(device)
+        self.precision = precision
         w = weights if weights is not None else synthetic.weights(self.kind, seed)
         blob = synthetic.pack(self.kind, w)
         want = self.lib.mec_blob_size(KINDS[self.kind])
@@ -66,8 +69,9 @@ class HipModel:
             raise MecError(f'{self.kind}: blob has {blob.size} floats, library expects {want}')
         h = ctypes.c_void_p()
         torch.cuda.set_device(self.device)
-        _lib.check(self.lib.mec_create(KINDS[self.kind], blob.ctypes.data_as(_lib.c_fp), blob.size,
-                                       self.device.index, ctypes.byref(h)), f'mec_create({self.kind})')
+        _lib.check(self.lib.mec_create_ex(KINDS[self.kind], blob.ctypes.data_as(_lib.c_fp), blob.size,
+                                          self.device.index, _lib.PRECISIONS[precision], ctypes.byref(h)),
+                   f'mec_create({self.kind}, {precision})')
         self.handle = h
         self._lock = threading.Lock()
 
@@ -236,11 +240,12 @@ class FusedPipeline:
 
     def __init__(self, seed: int = 1234, device=None, weights=None, concurrent: bool = True,
                  image_backbone: str = 'resnet50', pipelined: bool = True, text_priority: bool = True,
-                 image_priority: bool = False):
+                 image_priority: bool = False, precision: str = 'f16'):
         weights = weights or {}
+        self.precision = precision
         self.speech = SpeechEncoder(weights.get('speech'), seed, device)
-        self.text = TextEncoder(weights.get('text'), seed, device)
-        self.image = IMAGE_BACKBONES[image_backbone](weights.get('image'), seed, device)
+        self.text = TextEncoder(weights.get('text'), seed, device, precision)
+        self.image = IMAGE_BACKBONES[image_backbone](weights.get('image'), seed, device, precision)
         self.fusion = FusionHead(weights.get('fusion'), seed, device)
         self.device = self.speech.device
         self.concurrent = concurrent

@@ -1,0 +1,193 @@
+"""fp32 path (mec_create_ex(..., MEC_PREC_FP32)): the precision the reference computes in
+(inference/text_inference.py:91-93, inference/image_inference.py:116-118 — torch fp32).
+
+Every BERT and ResNet50 GEMM runs on v_mfma_f32_32x32x2_f32 (an exact f32 fmaf chain);
+the only deviation from the oracle is the summation order, so the bar is far tighter than
+the f16 path's 1e-3: softmax probabilities within FP32_PROB_TOL of the oracle and argmax
+exact on every row, with no near-tie exclusion.
+"""
+import ctypes
+
+import numpy as np
+import pytest
+import torch
+
+from mec import _lib, engine, synthetic as syn
+from oracle import fusion as o_f, image as o_i, speech as o_s, text as o_t
+
+pytestmark = pytest.mark.gpu
+
+FP32_PROB_TOL = 1e-5   # probs, fp32 path vs the fp32 oracle (order of summation only)
+FP32_FEAT_RTOL = 1e-4  # features, max |d| / max |ref|
+
+
+def _np(ts):
+    torch.cuda.synchronize()
+    return [t.cpu().numpy() for t in ts]
+
+
+def _report(name, got, ref):
+    err = float(np.abs(got - ref).max())
+    agree = int((got.argmax(1) == ref.argmax(1)).sum())
+    s = np.sort(ref, axis=1)
+    print(f'{name}: rows {len(got)}, probs max|d| {err:.3g}, argmax {agree}/{len(got)}, '
+          f'min top-2 margin {(s[:, -1] - s[:, -2]).min():.3g}')
+    return err, agree
+
+
+def _ptr(t):
+    return ctypes.c_void_p(t.data_ptr()) if t is not None else ctypes.c_void_p(0)
+
+
+def _stream(dev):
+    return ctypes.c_void_p(torch.cuda.current_stream(dev).cuda_stream)
+
+
+@pytest.fixture
+def tile_option():
+    lib = _lib.load()
+    yield lib
+    assert lib.mec_set_option(b'gemm_f32_tile', 0) == 0
+
+
+@pytest.mark.parametrize('M,N,K,act,res', [(300, 192, 256, 1, True), (256, 128, 768, 4, False),
+                                           (1000, 256, 96, 0, True), (64, 64, 32, 0, False)])
+def test_gemm_f32_vs_fp64(dev, tile_option, M, N, K, act, res):
+    """mec_gemm_f32 against an fp64 reference; every tile that fits N gives bit-identical
+    results (each output is the same k-ordered fmaf chain)."""
+    lib = tile_option
+    g = torch.Generator().manual_seed(M + N + K)
+    A = torch.randn(M, K, generator=g)
+    B = torch.randn(N, K, generator=g) / np.sqrt(K)
+    bias = torch.randn(N, generator=g)
+    R = torch.randn(M, N, generator=g) if res else None
+    ref = A.double() @ B.double().T + bias.double()
+    if res:
+        ref = ref + R.double()
+    if act == 1:
+        ref = ref.clamp_min(0)
+    elif act == 4:
+        ref = torch.nn.functional.gelu(ref)
+    outs = []
+    for tile in (1, 2, 3, 4):
+        if N % (64 if tile == 3 else (256 if tile == 4 else 128)):
+            continue
+        assert lib.mec_set_option(b'gemm_f32_tile', tile) == 0
+        dA, dB, db = A.to(dev), B.to(dev), bias.to(dev)
+        dR = R.to(dev) if res else None
+        C = torch.empty(M, N, device=dev)
+        _lib.check(lib.mec_gemm_f32(_ptr(dA), _ptr(dB), _ptr(db), _ptr(dR), _ptr(C), M, N, K, act, _stream(dev)),
+                   'mec_gemm_f32')
+        torch.cuda.synchronize()
+        outs.append((tile, C.cpu()))
+    scale = float((A.abs().double() @ B.abs().double().T).max()) + 1.0
+    for tile, C in outs:
+        err = float((C.double() - ref).abs().max())
+        print(f'tile {tile}: max|d| {err:.3g} (scale {scale:.3g})')
+        assert err <= 2e-6 * scale
+        assert torch.equal(C, outs[0][1]), f'tile {tile} differs from tile {outs[0][0]}'
+
+
+@pytest.mark.parametrize('H,C,Cout,ks,stride,pad', [(14, 64, 128, 3, 2, 1), (7, 128, 64, 3, 1, 1),
+                                                    (8, 32, 64, 1, 2, 0)])
+def test_conv_f32_vs_fp64(dev, H, C, Cout, ks, stride, pad):
+    lib = _lib.load()
+    g = torch.Generator().manual_seed(H * C)
+    n = 3
+    x = torch.randn(n, C, H, H, generator=g)
+    w = torch.randn(Cout, C, ks, ks, generator=g) / np.sqrt(C * ks * ks)
+    b = torch.randn(Cout, generator=g)
+    ref = torch.nn.functional.conv2d(x.double(), w.double(), b.double(), stride=stride, padding=pad).clamp_min(0)
+    OH = ref.shape[2]
+    xn = x.permute(0, 2, 3, 1).contiguous().to(dev)
+    wn = w.permute(0, 2, 3, 1).contiguous().to(dev)
+    y = torch.empty(n, OH, OH, Cout, device=dev)
+    _lib.check(lib.mec_conv_f32(_ptr(xn), _ptr(wn), _ptr(b.to(dev)), None, _ptr(y), n, H, H, C, Cout, ks, stride, pad,
+                                1, _stream(dev)), 'mec_conv_f32')
+    torch.cuda.synchronize()
+    err = float((y.cpu().permute(0, 3, 1, 2).double() - ref).abs().max())
+    print(f'conv f32 max|d| {err:.3g}')
+    assert err <= 1e-5
+
+
+def test_precision_query(dev):
+    t = engine.TextEncoder(device=dev, precision='fp32')
+    assert t.lib.mec_precision(t.handle) == 1
+    s = engine.SpeechEncoder(device=dev)
+    assert s.lib.mec_precision(s.handle) == 1  # speech is fp32 at either setting
+    with pytest.raises(ValueError):
+        engine.TextEncoder(device=dev, precision='bf16')
+    with pytest.raises(_lib.MecError):
+        engine.MobileNetImageEncoder(device=dev, precision='fp32')
+
+
+def test_text_fp32_golden(dev, golden):
+    """BERT fp32 against the fixture pinned to HF BertForSequenceClassification (eager)."""
+    gd = golden('text_bert.npz')
+    enc = engine.TextEncoder(device=dev, precision='fp32')
+    cls, logits, probs = _np(enc.forward(engine.to_device(gd['ids'], dev), engine.to_device(gd['mask'], dev)))
+    err, agree = _report('text fp32 golden', probs, gd['probs'])
+    ferr = float(np.abs(cls - gd['cls']).max() / np.abs(gd['cls']).max())
+    print(f'  cls rel err {ferr:.3g}, logits max|d| {np.abs(logits - gd["logits"]).max():.3g}')
+    assert agree == len(probs) and err <= FP32_PROB_TOL and ferr <= FP32_FEAT_RTOL
+
+
+@pytest.mark.parametrize('B,ragged', [(16, True), (128, False)])
+def test_text_fp32_vs_oracle(dev, B, ragged):
+    ids, mask = syn.text_inputs(B, 128, seed=40 + B, ragged=ragged)
+    enc = engine.TextEncoder(device=dev, precision='fp32')
+    cls, logits, probs = _np(enc.forward(engine.to_device(ids, dev), engine.to_device(mask, dev)))
+    sub = np.unique(np.r_[0, 1, np.arange(0, B, max(1, B // 12)), B - 1])
+    rc, rl, rp = o_t.forward(syn.weights('text'), ids[sub], mask[sub])
+    err, agree = _report(f'text fp32 B={B}', probs[sub], rp)
+    ferr = float(np.abs(cls[sub] - rc).max() / np.abs(rc).max())
+    print(f'  cls rel err {ferr:.3g}, logits max|d| {np.abs(logits[sub] - rl).max():.3g}')
+    assert agree == len(sub) and err <= FP32_PROB_TOL and ferr <= FP32_FEAT_RTOL
+
+
+@pytest.mark.parametrize('B', [3, 32])
+def test_image_fp32_vs_oracle(dev, B):
+    gray = syn.image_inputs(B, seed=50 + B)
+    enc = engine.ImageEncoder(device=dev, precision='fp32')
+    feat, logits, probs = _np(enc.forward(engine.to_device(gray, dev)))
+    sub = np.unique(np.r_[0, np.arange(0, B, max(1, B // 6)), B - 1])
+    rf, rl, rp = o_i.forward(syn.weights('image'), gray[sub])
+    err, agree = _report(f'image fp32 B={B}', probs[sub], rp)
+    ferr = float(np.abs(feat[sub] - rf).max() / np.abs(rf).max())
+    print(f'  feat rel err {ferr:.3g}, logits max|d| {np.abs(logits[sub] - rl).max():.3g}')
+    assert agree == len(sub) and err <= FP32_PROB_TOL and ferr <= FP32_FEAT_RTOL
+
+
+def test_image_fp32_rgb_and_gray224(dev):
+    """The already-resized entry points (mec_image_fwd_u8: [B,224,224,1] and RGB [B,224,224,3])."""
+    rng = np.random.default_rng(5)
+    enc = engine.ImageEncoder(device=dev, precision='fp32')
+    for C in (1, 3):
+        img = rng.integers(0, 256, (2, 224, 224, C), dtype=np.uint8)
+        feat, logits, probs = _np(enc.forward_u8(engine.to_device(img, dev)))
+        rf, rl, rp = o_i.forward_resized(syn.weights('image'), img[..., 0] if C == 1 else img)
+        err, agree = _report(f'image fp32 224x224x{C}', probs, rp)
+        assert agree == 2 and err <= FP32_PROB_TOL
+
+
+def test_fused_fp32_end_to_end(dev):
+    """Fused probs of the fp32 pipeline against the oracle chain o_f(o_s, o_t, o_i)
+    (inference/multimodal_fusion.py:271-278), B = 24 with ragged text."""
+    B = 24
+    x = syn.speech_inputs(B, seed=61)
+    ids, mask = syn.text_inputs(B, 128, seed=61, ragged=True)
+    gray = syn.image_inputs(B, seed=61)
+    pipe = engine.FusedPipeline(device=dev, precision='fp32')
+    args = [engine.to_device(a, dev) for a in (x, ids, mask, gray)]
+    pipe.forward(*args)
+    out = pipe.forward(*args)
+    pipe.wait()
+    got = {k: _np(v) for k, v in out.items()}
+    rs = o_s.forward(syn.weights('speech'), x)
+    rt = o_t.forward(syn.weights('text'), ids, mask)
+    ri = o_i.forward(syn.weights('image'), gray)
+    rf = o_f.forward(syn.weights('fusion'), rs[0], rt[0], ri[0], rs[2], rt[2], ri[2])
+    for name, g, r in (('speech', got['speech'][2], rs[2]), ('text', got['text'][2], rt[2]),
+                       ('image', got['image'][2], ri[2]), ('fused', got['fusion'][1], rf[1])):
+        err, agree = _report(f'fp32 pipeline {name}', g, r)
+        assert agree == B and err <= FP32_PROB_TOL, name
