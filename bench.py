@@ -206,7 +206,11 @@ def per_config(pipe, dev, precision, iters=10):
 
 def run(a, precision, B, world, rank, dev):
     """Time K pipelined steps at one precision; returns the result line (rank 0) or None."""
-    from mec import dist as mdist, engine, synthetic as syn
+    from mec import _lib, dist as mdist, engine, synthetic as syn
+    # the product library: no probe build (probe option values skip work and return wrong
+    # results), and every knob of the pipeline's handles at its default (handles own their knobs)
+    if _lib.load().mec_build_flags() != 0:
+        raise SystemExit(f'bench.py: {_lib.LIB_PATH} is a probe build (MEC_PROBES); use the product library')
     pipe = engine.FusedPipeline(seed=1234, device=dev, concurrent=not a.serial, pipelined=not a.no_pipeline,
                                 text_priority=bool(a.text_priority), image_priority=bool(a.image_priority),
                                 precision=precision)
@@ -272,13 +276,11 @@ def run(a, precision, B, world, rank, dev):
     avg_s = (ffn_ms / max(ffn_n, 1)) / 1e3
     achieved = ffn_flop / avg_s / 1e12 if ffn_n else None
     iso = ffn_flop / ((iso_ms / max(iso_n, 1)) / 1e3) / 1e12 if iso_n else None
-    lib = pipe.text.lib
+    tile = pipe.text.gemm_tile(M, 3072, 768)  # the text handle's own autotune choice
     if precision == 'f16':
-        tile = lib.mec_gemm_query(0, M, 3072, 768)
         kname = tile_name(tile, M) + ' + GELU'
         ebytes, tfile = 2, 'ffn1_traffic.json'
     else:
-        tile = lib.mec_gemm_f32_query(0, M, 3072, 768)
         kname = tile_name_f32(tile, M) + ' + erf-GELU'
         ebytes, tfile = 4, 'ffn1_f32_traffic.json'
     traffic, tsrc = None, None

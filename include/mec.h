@@ -120,34 +120,45 @@ int mec_gemm_f32(const float* A, const float* B, const float* bias, const float*
 int mec_conv_f32(const float* x, const float* w, const float* bias, const float* R, float* y, int n, int H, int W,
                  int C, int Cout, int ks, int stride, int pad, int act, void* stream);
 
-/* Process-wide tuning knobs (A/B benchmarking; defaults in brackets). Every pair of
- * settings of one knob gives bit-identical outputs, except the *_debug probe builds, which
- * skip work to time its parts and return wrong results, and "fusion_r" 4 vs 1|2 (ulp-level,
- * fp32 reassociation in the compiled block code; both within the oracle tolerance).
+/* Tuning knobs (A/B benchmarking; defaults in brackets). Every handle owns its own copy of
+ * the knobs and its own GEMM autotune cache, so two handles in one process never perturb
+ * each other: mec_model_set_option sets one handle's knob; mec_set_option sets the process
+ * default that handles created AFTERWARDS copy (and that the handle-less kernel entry points
+ * use). Every pair of settings of one knob gives bit-identical outputs, except "fusion_r" 4 vs
+ * 1|2 (ulp-level fp32 reassociation, both within the oracle tolerance).
  *   "gemm_impl" 1|[2]      register-staged / glds GEMM engine
- *   "gemm_bn" [0]|id       force one GEMM tile (0 = autotune), "gemm_autotune" 0|[1]
+ *   "gemm_bn" [0]|id       force one f16 GEMM tile (0 = autotune), "gemm_autotune" 0|[1]
  *   "gemm_bn_tag" tag*100000+id   force a tile for one launch class (e.g. 3 = BERT O-proj)
+ *   "gemm_f32_tile" [0]|1..4  force one fp32 GEMM tile (0 = autotune)
  *   "gemm_prefetch_r" 0|[1]  f16 residual prefetch in short-K GEMMs
  *   "conv3x3_direct" 0|[1] layer1 3x3 conv on the halo-tile kernel (mec_conv_f16 too)
  *   "pw_chain" 0|1|[2]     layer1 seam kernels (1: the 256->64 seams, 2: also 256->128)
  *   "pw_chain_form" [0]|1|2  seam weight placement (LDS / registers)
- *   "bert_qkv_attn" 0|[1]  fused BERT QKV projection + attention (2 / 3: probe builds,
- *                          no attention / main loop only)
+ *   "bert_qkv_attn" 0|[1]  fused BERT QKV projection + attention
  *   "bert_oproj_ln" [0]|1|3  BERT O-projection + residual + LayerNorm 1 in one full-row kernel
- *                          (1: Wo staged in LDS, 3: Wo read into registers; both measured
- *                          slower; 2 / 4: their main-loop-only probe builds)
+ *                          (1: Wo staged in LDS, 3: Wo read into registers; both measured slower)
  *   "resnet_chunk" [0]|n   ResNet layers 1-2 over n-image chunks
  *   "resnet_fused_tail" [0]|1, "mbv2_impl" [0]|1|2
  *   "fusion_r" 1|2|[4]     samples per fusion workgroup
  *   "fusion_split" 0|[1]   fusion as 3 launches (per-modality projection, cross-attention, head)
- *   "conv3x3_debug", "stem_debug", "gemm_debug": probe builds (wrong results); gemm_debug 4
- *   records an s_memtime phase trace of the ping-pong tile (tools/pp_trace.py). */
+ * Probe values, which skip work to time a kernel's parts and return WRONG results, exist only
+ * in the -DMEC_PROBES build (libmec_hip_probes.so, `make probes`; tools/ only): "gemm_debug"
+ * 1..4, "conv3x3_debug" / "stem_debug" 1|2|4|7, "bert_qkv_attn" 2|3, "bert_oproj_ln" 2|4. The
+ * product library rejects them (-1). */
 int mec_set_option(const char* key, int value);
+int mec_model_set_option(mec_model* m, const char* key, int value);
+
+/* Build flags of the loaded library: MEC_BUILD_PROBES set = probe values accepted. */
+enum { MEC_BUILD_PROBES = 1 };
+int mec_build_flags(void);
 
 /* Tile width the autotuner chose for a plain (amode 0) or conv (amode 1) GEMM shape; 0 = not yet seen. */
 int mec_gemm_query(int amode, int M, int N, int K);
-/* The same for the fp32 engine: tile id 1 = 256x128 (8 waves), 2 = 128x128, 3 = 128x64, 4 = 256x256. */
+/* The same for the fp32 engine: tile id 1 = 256x128 (8 waves), 2 = 128x128, 3 = 128x64, 4 = 256x256.
+ * Both query the process-default cache of the handle-less entry points (mec_gemm_f16/f32). */
 int mec_gemm_f32_query(int amode, int M, int N, int K);
+/* The tile a handle's own autotuner chose for a shape it ran (its precision's engine); 0 = not seen. */
+int mec_model_gemm_query(mec_model* m, int amode, int M, int N, int K);
 
 /* hipEvent timing hook: time every launch of kernel class `tag`. */
 int mec_prof_enable(mec_model* m, int tag);

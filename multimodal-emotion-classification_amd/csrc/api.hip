@@ -169,6 +169,7 @@ int mec_speech_fwd(mec_model* m, const float* x, int B, float* feat, float* logi
   API_GUARD({
     auto* p = as<SpeechModel>(m, KIND_SPEECH);
     if (!p) return -1;
+    OptScope sc(&p->opts, &p->tune);
     return p->forward(x, B, feat, logits, probs, S(stream));
   })
 }
@@ -178,6 +179,7 @@ int mec_text_fwd(mec_model* m, const int32_t* ids, const int32_t* mask, int B, i
   API_GUARD({
     auto* p = as<TextModel>(m, KIND_TEXT);
     if (!p) return -1;
+    OptScope sc(&p->opts, &p->tune);
     return p->forward(ids, mask, B, L, cls, logits, probs, S(stream));
   })
 }
@@ -187,6 +189,7 @@ int mec_image_fwd(mec_model* m, const uint8_t* gray, int B, float* feat, float* 
   API_GUARD({
     auto* p = image_net(m);
     if (!p) return -1;
+    OptScope sc(&p->opts, &p->tune);
     return p->forward(gray, B, feat, logits, probs, S(stream));
   })
 }
@@ -196,6 +199,7 @@ int mec_image_fwd_u8(mec_model* m, const uint8_t* img, int B, int H, int W, int 
   API_GUARD({
     auto* p = image_net(m);
     if (!p) return -1;
+    OptScope sc(&p->opts, &p->tune);
     return p->forward_u8(img, B, H, W, C, feat, logits, probs, S(stream));
   })
 }
@@ -206,6 +210,7 @@ int mec_fusion_fwd(mec_model* m, const float* s_feat, const float* t_feat, const
   API_GUARD({
     auto* p = as<FusionModel>(m, KIND_FUSION);
     if (!p) return -1;
+    OptScope sc(&p->opts, &p->tune);
     return p->forward(s_feat, t_feat, i_feat, s_pred, t_pred, i_pred, B, logits, probs, attn_w, dec_w, S(stream));
   })
 }
@@ -245,29 +250,40 @@ int mec_conv_f16(const void* x, const void* w, const float* bias, const void* R,
   })
 }
 
-int mec_set_option(const char* key, int value) {
-  const std::string k = key ? key : "";
-  if (k == "gemm_impl" && (value == 1 || value == 2)) { g_gemm_impl = value; return 0; }
-  if (k == "fusion_r" && (value == 1 || value == 2 || value == 4)) { g_fusion_r = value; return 0; }
-  if (k == "fusion_split" && (value == 0 || value == 1)) { g_fusion_split = value; return 0; }
-  if (k == "gemm_debug" && value >= 0 && value <= 4) { g_gemm_debug = value; return 0; }
-  if (k == "gemm_autotune" && (value == 0 || value == 1)) { g_gemm_autotune = value; return 0; }
-  if (k == "gemm_f32_tile" && value >= 0 && value <= 4) { g_gemm_f32_tile = value; return 0; }
-  if (k == "gemm_prefetch_r" && (value == 0 || value == 1)) { g_gemm_prefetch_r = value; return 0; }
-  if (k == "resnet_fused_tail" && (value == 0 || value == 1)) { g_resnet_fused_tail = value; return 0; }
-  if (k == "mbv2_impl" && value >= 0 && value <= 2) { g_mbv2_impl = value; return 0; }
-  if (k == "conv3x3_direct" && (value == 0 || value == 1)) { g_conv3x3_direct = value; return 0; }
-  if (k == "resnet_chunk" && value >= 0) { g_resnet_chunk = value; return 0; }
-  if (k == "bert_qkv_attn" && value >= 0 && value <= 3) { g_bert_qkv_attn = value; return 0; }
-  if (k == "bert_oproj_ln" && value >= 0 && value <= 4) { g_bert_oproj_ln = value; return 0; }
-  if (k == "stem_debug" && (value == 0 || value == 1 || value == 2 || value == 4 || value == 7)) {
-    g_stem_debug = value;
+}  // extern "C"
+
+namespace mec {
+// One knob of `o` (include/mec.h lists them). The probe-build values (*_debug, bert_qkv_attn
+// 2 | 3, bert_oproj_ln 2 | 4) return wrong results and exist only in -DMEC_PROBES builds.
+int set_option(Options& o, const std::string& k, int value) {
+  const bool probe = kProbes;
+  if (k == "gemm_impl" && (value == 1 || value == 2)) { o.gemm_impl = value; return 0; }
+  if (k == "fusion_r" && (value == 1 || value == 2 || value == 4)) { o.fusion_r = value; return 0; }
+  if (k == "fusion_split" && (value == 0 || value == 1)) { o.fusion_split = value; return 0; }
+  if (k == "gemm_debug" && (value == 0 || (probe && value >= 1 && value <= 4))) { o.gemm_debug = value; return 0; }
+  if (k == "gemm_autotune" && (value == 0 || value == 1)) { o.gemm_autotune = value; return 0; }
+  if (k == "gemm_f32_tile" && value >= 0 && value <= 4) { o.gemm_f32_tile = value; return 0; }
+  if (k == "gemm_prefetch_r" && (value == 0 || value == 1)) { o.gemm_prefetch_r = value; return 0; }
+  if (k == "resnet_fused_tail" && (value == 0 || value == 1)) { o.resnet_fused_tail = value; return 0; }
+  if (k == "mbv2_impl" && value >= 0 && value <= 2) { o.mbv2_impl = value; return 0; }
+  if (k == "conv3x3_direct" && (value == 0 || value == 1)) { o.conv3x3_direct = value; return 0; }
+  if (k == "resnet_chunk" && value >= 0) { o.resnet_chunk = value; return 0; }
+  if (k == "bert_qkv_attn" && (value == 0 || value == 1 || (probe && (value == 2 || value == 3)))) {
+    o.bert_qkv_attn = value;
     return 0;
   }
-  if (k == "pw_chain" && (value >= 0 && value <= 2)) { g_pw_chain = value; return 0; }
-  if (k == "pw_chain_form" && (value >= 0 && value <= 2)) { g_pw_chain_form = value; return 0; }
-  if (k == "conv3x3_debug" && (value == 0 || value == 1 || value == 2 || value == 4 || value == 7)) {
-    g_conv3x3_debug = value;
+  if (k == "bert_oproj_ln" && (value == 0 || value == 1 || value == 3 || (probe && (value == 2 || value == 4)))) {
+    o.bert_oproj_ln = value;
+    return 0;
+  }
+  if (k == "stem_debug" && (value == 0 || (probe && (value == 1 || value == 2 || value == 4 || value == 7)))) {
+    o.stem_debug = value;
+    return 0;
+  }
+  if (k == "pw_chain" && (value >= 0 && value <= 2)) { o.pw_chain = value; return 0; }
+  if (k == "pw_chain_form" && (value >= 0 && value <= 2)) { o.pw_chain_form = value; return 0; }
+  if (k == "conv3x3_debug" && (value == 0 || (probe && (value == 1 || value == 2 || value == 4 || value == 7)))) {
+    o.conv3x3_debug = value;
     return 0;
   }
   auto tile_ok = [](int id) {
@@ -277,16 +293,35 @@ int mec_set_option(const char* key, int value) {
     return id == 0 || deep || (id < 20000 && (v == 64 || v == 128 || v == 256 || v == 1064 || v == 1128));
   };
   if (k == "gemm_bn" && tile_ok(value)) {
-    g_gemm_bn = value;
+    o.gemm_bn = value;
     return 0;
   }
   // one launch class only: value = tag * 100000 + tile id (tags: mec_common.h KernelTag)
   if (k == "gemm_bn_tag" && value >= 0 && value / 100000 > 0 && value / 100000 < TAG_COUNT && tile_ok(value % 100000)) {
-    g_gemm_bn_tag[value / 100000] = value % 100000;
+    o.gemm_bn_tag[value / 100000] = value % 100000;
     return 0;
   }
-  set_error("mec_set_option: unknown key or bad value: " + k);
+  set_error("mec_set_option: unknown key or bad value: " + k + " = " + std::to_string(value) +
+            (probe ? "" : " (probe values need a -DMEC_PROBES build)"));
   return -1;
+}
+}  // namespace mec
+
+extern "C" {
+
+int mec_set_option(const char* key, int value) { return set_option(default_options(), key ? key : "", value); }
+
+int mec_model_set_option(mec_model* m, const char* key, int value) {
+  if (!m || !m->impl) { set_error("null model handle"); return -1; }
+  return set_option(m->impl->opts, key ? key : "", value);
+}
+
+int mec_build_flags(void) { return kProbes ? MEC_BUILD_PROBES : 0; }
+
+int mec_model_gemm_query(mec_model* m, int amode, int M, int N, int K) {
+  if (!m || !m->impl) { set_error("null model handle"); return -1; }
+  OptScope sc(&m->impl->opts, &m->impl->tune);
+  return m->impl->prec == PREC_FP32 ? gemm_f32_tuned(amode, M, N, K) : gemm_tuned_bn(amode, M, N, K);
 }
 
 int mec_gemm_query(int amode, int M, int N, int K) { return gemm_tuned_bn(amode, M, N, K); }

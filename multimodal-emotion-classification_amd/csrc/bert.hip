@@ -438,8 +438,6 @@ __global__ __launch_bounds__(512, 1) void bert_qkv_attn_kernel(const f16* __rest
             wave & 3, lane, ctx + (size_t)b * ATT_L * BH + (2 * hp + hh) * BDH);
 }
 
-int g_bert_qkv_attn = 1;  // fused QKV projection + attention (0: QKV GEMM, then attention kernel;
-                          // 2 / 3: probe builds without the attention / with the main loop only)
 
 // ----------------------------------------------------------------------------- O-proj + LN1
 // The attention output projection, its residual add and LayerNorm 1 in one kernel: a
@@ -721,8 +719,6 @@ __global__ __launch_bounds__(512, 1) void bert_oproj_ln_kernel(const f16* __rest
   }
 }
 
-int g_bert_oproj_ln = 0;  // 1 / 3: O-projection + residual + LayerNorm 1 in one kernel, Wo through LDS /
-                          // into registers (both measured slower); 2 / 4: probe builds
 
 // ----------------------------------------------------------------------------- model
 // prm layout per layer (floats): bqkv 2304 | bo 768 | ln1g 768 | ln1b 768 | bi 3072 | bo2 768 |
@@ -849,13 +845,15 @@ int TextModel::forward(const int32_t* ids, const int32_t* mask, int B, int L, fl
     const float *bqkv = pl, *bo = pl + 2304, *g1 = pl + 3072, *b1 = pl + 3840, *bi = pl + 4608,
                 *bo2 = pl + 7680, *g2 = pl + 8448, *b2 = pl + 9216;
     GemmParams g;
-    if (g_bert_qkv_attn) {
+    if (opt().bert_qkv_attn) {
       MEC_TRY(prof.begin(TAG_BERT_ATTN, s));
-      if (g_bert_qkv_attn == 2)
+#ifdef MEC_PROBES
+      if (opt().bert_qkv_attn == 2)
         hipLaunchKernelGGL((bert_qkv_attn_kernel<1>), dim3(B * 6), dim3(512), 0, s, h16, wqkv, bqkv, mask, ctx16, B);
-      else if (g_bert_qkv_attn == 3)
+      else if (opt().bert_qkv_attn == 3)
         hipLaunchKernelGGL((bert_qkv_attn_kernel<2>), dim3(B * 6), dim3(512), 0, s, h16, wqkv, bqkv, mask, ctx16, B);
       else
+#endif
         hipLaunchKernelGGL((bert_qkv_attn_kernel<0>), dim3(B * 6), dim3(512), 0, s, h16, wqkv, bqkv, mask, ctx16, B);
       MEC_LAUNCH_CHECK();
       MEC_TRY(prof.end(TAG_BERT_ATTN, s));
@@ -872,23 +870,25 @@ int TextModel::forward(const int32_t* ids, const int32_t* mask, int B, int L, fl
     // f32 stream ping-pong: O-proj reads h32 and writes t32, FFN2 reads t32 and writes h32,
     // so no GEMM reads its own output (a launch stays idempotent: the tile autotuner
     // re-runs candidates on the same buffers)
-    if (g_bert_oproj_ln && M % OL_BM == 0) {
+    if (opt().bert_oproj_ln && M % OL_BM == 0) {
       MEC_TRY(prof.begin(TAG_BERT_OPROJ, s));
-      if (first && g_bert_oproj_ln == 3)
+      if (first && opt().bert_oproj_ln == 3)
         hipLaunchKernelGGL((bert_oproj_ln_kernel<false, 0, true>), dim3(M / OL_BM), dim3(512), 0, s, ctx16, wo, bo,
                            h32, nullptr, nullptr, nullptr, g1, b1, t32, h16, st1);
       else if (first)
         hipLaunchKernelGGL(bert_oproj_ln_kernel<false>, dim3(M / OL_BM), dim3(512), 0, s, ctx16, wo, bo, h32,
                            nullptr, nullptr, nullptr, g1, b1, t32, h16, st1);
-      else if (g_bert_oproj_ln == 3)
+      else if (opt().bert_oproj_ln == 3)
         hipLaunchKernelGGL((bert_oproj_ln_kernel<true, 0, true>), dim3(M / OL_BM), dim3(512), 0, s, ctx16, wo, bo, h32,
                            st2, pg2, pg2 + BH, g1, b1, t32, h16, st1);
-      else if (g_bert_oproj_ln == 4)
+#ifdef MEC_PROBES
+      else if (opt().bert_oproj_ln == 4)
         hipLaunchKernelGGL((bert_oproj_ln_kernel<true, 1, true>), dim3(M / OL_BM), dim3(512), 0, s, ctx16, wo, bo, h32,
                            st2, pg2, pg2 + BH, g1, b1, t32, h16, st1);
-      else if (g_bert_oproj_ln == 2)
+      else if (opt().bert_oproj_ln == 2)
         hipLaunchKernelGGL((bert_oproj_ln_kernel<true, 1>), dim3(M / OL_BM), dim3(512), 0, s, ctx16, wo, bo, h32, st2,
                            pg2, pg2 + BH, g1, b1, t32, h16, st1);
+#endif
       else
         hipLaunchKernelGGL(bert_oproj_ln_kernel<true>, dim3(M / OL_BM), dim3(512), 0, s, ctx16, wo, bo, h32, st2,
                            pg2, pg2 + BH, g1, b1, t32, h16, st1);

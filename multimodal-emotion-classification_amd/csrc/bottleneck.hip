@@ -15,7 +15,7 @@
 // the residual), the block output once. Accumulation is fp32 over the same (tap, ci) k order
 // as the A_CONV GEMM, with the same f16 rounding of the conv2 output: the outputs are bit-
 // identical to the unfused GEMMs. MEASURED SLOWER (315 us per block vs 275 us for the two
-// GEMMs, see g_resnet_fused_tail in resnet.hip), so it is opt-in: at one 4-wave workgroup
+// GEMMs, see opt().resnet_fused_tail in resnet.hip), so it is opt-in: at one 4-wave workgroup
 // per CU the per-k-step LDS reads and the barriers are not hidden; two waves per SIMD (the
 // q-tiles split over 8 waves) is the next form to try.
 #include <algorithm>

@@ -215,7 +215,6 @@ __global__ __launch_bounds__(256, 1) void conv3x3_c64_kernel(const f16* __restri
   }
 }
 
-int g_conv3x3_debug = 0;
 
 int launch_conv3x3_c64(const f16* x, const f16* w, const float* bias, f16* y, int B, int H, int C, int Cout,
                        hipStream_t s) {
@@ -229,12 +228,14 @@ int launch_conv3x3_c64(const f16* x, const f16* w, const float* bias, f16* y, in
   }
   const int ntiles = B * (C3_H / C3_TR);
   const dim3 grd(std::min(ntiles, ncu)), blk(256);
-  switch (g_conv3x3_debug) {  // probe builds (wrong results): 1 no next-tile DMA, 2 no stores, 4 no LDS reads
+  switch (opt().conv3x3_debug) {  // probe builds (wrong results): 1 no next-tile DMA, 2 no stores, 4 no LDS reads
     case 0: hipLaunchKernelGGL(conv3x3_c64_kernel<0>, grd, blk, 0, s, x, w, bias, y, ntiles); break;
+#ifdef MEC_PROBES
     case 1: hipLaunchKernelGGL(conv3x3_c64_kernel<1>, grd, blk, 0, s, x, w, bias, y, ntiles); break;
     case 2: hipLaunchKernelGGL(conv3x3_c64_kernel<2>, grd, blk, 0, s, x, w, bias, y, ntiles); break;
     case 4: hipLaunchKernelGGL(conv3x3_c64_kernel<4>, grd, blk, 0, s, x, w, bias, y, ntiles); break;
     case 7: hipLaunchKernelGGL(conv3x3_c64_kernel<7>, grd, blk, 0, s, x, w, bias, y, ntiles); break;
+#endif
     default: set_error("conv3x3_debug: bad value"); return -1;
   }
   MEC_LAUNCH_CHECK();

@@ -208,15 +208,11 @@ static int launch_mode(const GemmParams& p, hipStream_t s) {
   return 0;
 }
 
-int g_gemm_impl = 2;  // 1 = register-staged 128x128 kernel, 2 = glds pipelined (default)
-int g_gemm_bn = 0;    // 0 = auto tile width
 // Per launch class (profiling tag): forced tile id, 0 = autotune. The BERT O-projection
 // (32768 x 768 x 768, f32 deferred-LN residual) is pinned to 128 x 128: its candidates time
 // within 2% of each other alone, so the isolated autotune flips between them run to run, but
 // inside the encoder 128 x 128 is the fastest (text 8.22 ms vs 8.43 with 256 x 128 / 4 waves;
 // fused step 11.40 vs 11.48 ms).
-int g_gemm_bn_tag[TAG_COUNT] = {0, 0, 0, /*TAG_BERT_OPROJ*/ 11128};
-int g_conv3x3_direct = 1;  // ResNet layer1 conv2 on the halo-tile kernel (conv3x3.hip)
 
 int launch_gemm(const GemmParams& p, hipStream_t s, Prof* prof, int tag) {
   MEC_REQUIRE(p.M > 0 && p.N > 0 && p.K > 0, "gemm: empty shape");
@@ -230,17 +226,17 @@ int launch_gemm(const GemmParams& p, hipStream_t s, Prof* prof, int tag) {
   } else if (p.amode == A_DUAL) {
     MEC_REQUIRE(p.A2 && p.K1 > 0 && p.K1 % 64 == 0 && p.C % 64 == 0 && p.K == p.K1 + p.C && p.ks == 1 && p.pad == 0,
                 "dual gemm: need K = K1 + C, K1 % 64 == 0, C % 64 == 0, 1x1 unpadded second source");
-    MEC_REQUIRE(g_gemm_impl == 2, "dual gemm needs the glds engine");
+    MEC_REQUIRE(opt().gemm_impl == 2, "dual gemm needs the glds engine");
   } else {
     MEC_REQUIRE(p.amode == A_PLAIN, "gemm: unknown A mode");
   }
   if (prof) MEC_TRY(prof->begin(tag, s));
   int rc;
-  if (g_conv3x3_direct && !g_gemm_bn && p.amode == A_CONV && p.ks == 3 && p.stride == 1 && p.pad == 1 && p.H == 56 &&
+  if (opt().conv3x3_direct && !opt().gemm_bn && p.amode == A_CONV && p.ks == 3 && p.stride == 1 && p.pad == 1 && p.H == 56 &&
       p.W == 56 && p.C == 64 && p.N == 64 && p.act == ACT_RELU && !p.R && p.C16 && !p.C32 && p.M % (56 * 56) == 0)
     rc = launch_conv3x3_c64(reinterpret_cast<const f16*>(p.A), p.B, p.bias, p.C16, p.M / (56 * 56), 56, 64, 64, s);
-  else if (g_gemm_impl == 2)
-    rc = launch_gemm_glds(p, s, g_gemm_bn ? g_gemm_bn : (tag > 0 && tag < TAG_COUNT ? g_gemm_bn_tag[tag] : 0));
+  else if (opt().gemm_impl == 2)
+    rc = launch_gemm_glds(p, s, opt().gemm_bn ? opt().gemm_bn : (tag > 0 && tag < TAG_COUNT ? opt().gemm_bn_tag[tag] : 0));
   else
     rc = (p.N % 128 == 0) ? launch_mode<128, 128>(p, s) : launch_mode<128, 64>(p, s);
   if (rc) return rc;

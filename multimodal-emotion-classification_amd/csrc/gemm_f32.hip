@@ -209,19 +209,10 @@ static int launch_tile(const GemmParams& p, hipStream_t s, int id) {
   }
 }
 
-struct F32Key {
-  int amode, M, N, K, H, W, C, ks, stride, pad;
-  bool operator<(const F32Key& o) const {
-    const int a[10] = {amode, M, N, K, H, W, C, ks, stride, pad};
-    const int b[10] = {o.amode, o.M, o.N, o.K, o.H, o.W, o.C, o.ks, o.stride, o.pad};
-    for (int i = 0; i < 10; ++i)
-      if (a[i] != b[i]) return a[i] < b[i];
-    return false;
-  }
-};
-static std::map<F32Key, int> g_f32_tuned;
-int g_gemm_f32_tile = 0;  // mec_set_option("gemm_f32_tile"): 0 = autotune, 1..4 = force a tile
-static std::mutex g_f32_mu;
+// Cache key: engine 1 (this engine) + the shape, in the calling handle's tune_cache().
+static std::array<int, 11> f32_key(const GemmParams& p) {
+  return {1, p.amode, p.M, p.N, p.K, p.H, p.W, p.C, p.ks, p.stride, p.pad};
+}
 
 static int heuristic_tile(const GemmParams& p) {
   if (p.N % 128) return 3;
@@ -256,12 +247,7 @@ static int tune_tile(const GemmParams& p, hipStream_t s, int* out) {
   return 0;
 }
 
-int gemm_f32_tuned(int amode, int M, int N, int K) {
-  std::lock_guard<std::mutex> lk(g_f32_mu);
-  for (const auto& kv : g_f32_tuned)
-    if (kv.first.amode == amode && kv.first.M == M && kv.first.N == N && kv.first.K == K) return kv.second;
-  return 0;
-}
+int gemm_f32_tuned(int amode, int M, int N, int K) { return tune_cache().find_shape(1, amode, M, N, K); }
 
 int launch_gemm_f32(const GemmParams& p, hipStream_t s, Prof* prof, int tag) {
   MEC_REQUIRE(p.M > 0 && p.N > 0 && p.K > 0, "gemm_f32: empty shape");
@@ -276,24 +262,21 @@ int launch_gemm_f32(const GemmParams& p, hipStream_t s, Prof* prof, int tag) {
   } else {
     MEC_REQUIRE(p.amode == A_PLAIN, "gemm_f32: plain or conv A only");
   }
-  const F32Key key{p.amode, p.M, p.N, p.K, p.H, p.W, p.C, p.ks, p.stride, p.pad};
-  int id = g_gemm_f32_tile;
+  const auto key = f32_key(p);
+  int id = opt().gemm_f32_tile;
   if (id) {
     MEC_REQUIRE(id >= 1 && id <= 4 && p.N % tile_n(id) == 0, "gemm_f32: forced tile does not fit N");
   } else {
-    std::lock_guard<std::mutex> lk(g_f32_mu);
-    auto it = g_f32_tuned.find(key);
-    if (it != g_f32_tuned.end()) id = it->second;
+    id = tune_cache().find(key);
   }
   if (!id) {
     hipStreamCaptureStatus cs = hipStreamCaptureStatusNone;
-    if (g_gemm_autotune && hipStreamIsCapturing(s, &cs) == hipSuccess && cs == hipStreamCaptureStatusNone) {
+    if (opt().gemm_autotune && hipStreamIsCapturing(s, &cs) == hipSuccess && cs == hipStreamCaptureStatusNone) {
       MEC_TRY(tune_tile(p, s, &id));
     } else {
       id = heuristic_tile(p);
     }
-    std::lock_guard<std::mutex> lk(g_f32_mu);
-    g_f32_tuned[key] = id;
+    tune_cache().put(key, id);
     if (getenv("MEC_GEMM_TRACE"))
       fprintf(stderr, "MEC_GEMM_F32 amode=%d M=%d N=%d K=%d H=%d C=%d ks=%d stride=%d act=%d R=%d tile=%d\n", p.amode,
               p.M, p.N, p.K, p.H, p.C, p.ks, p.stride, p.act, p.R != nullptr, id);

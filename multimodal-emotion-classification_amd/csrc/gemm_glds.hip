@@ -497,19 +497,22 @@ __global__ __launch_bounds__(512) void gemm_pp_kernel(const GemmParams p) {
 }
 
 // BM=256 tiles: (BN, WM, WN, NS)
-int g_gemm_debug = 0;
-int g_gemm_prefetch_r = 1;
 
 template <int BM, int BN, int WM, int WN, int NS, int MF = 32, int BK = 64>
 static int launch_cfg(const GemmParams& p, hipStream_t s) {
   const int nwg = ((p.M + BM - 1) / BM) * (p.N / BN);
   const dim3 blk(64 * WM * WN);
-  if (g_gemm_debug && BN == 256 && BM == 256 && p.amode == A_PLAIN) {
-    if (g_gemm_debug == 1)
+#ifdef MEC_PROBES
+  if (opt().gemm_debug && BN == 256 && BM == 256 && p.amode == A_PLAIN) {
+    if (opt().gemm_debug == 1)
       hipLaunchKernelGGL((gemm_glds_kernel<BM, BN, WM, WN, NS, A_PLAIN, 1, MF, BK>), dim3(nwg), blk, 0, s, p);
     else
       hipLaunchKernelGGL((gemm_glds_kernel<BM, BN, WM, WN, NS, A_PLAIN, 2, MF, BK>), dim3(nwg), blk, 0, s, p);
-  } else if (BM * BN <= 128 * 128 && g_gemm_prefetch_r && p.amode == A_PLAIN && p.R && !p.r_f32 && p.K <= 512) {
+    MEC_LAUNCH_CHECK();
+    return 0;
+  }
+#endif
+  if (BM * BN <= 128 * 128 && opt().gemm_prefetch_r && p.amode == A_PLAIN && p.R && !p.r_f32 && p.K <= 512) {
     // f16 residual prefetch for ResNet's short-K conv3 GEMMs (small tiles only: no spills);
     // 225 -> 170 us on layer1's conv3. The f32 form (PRE = 2, BERT's O-projection, K = 768)
     // measured 10-15% slower than no prefetch, so it is not dispatched.
@@ -529,19 +532,11 @@ static int launch_cfg(const GemmParams& p, hipStream_t s) {
 // the choice changes speed only, never results. The first launch of each distinct shape
 // times every legal width on the caller's stream (hipEvents; skipped while the stream is
 // being captured into a graph) and caches the fastest; `gemm_bn` forces a width.
-struct GemmKey {
-  int amode, M, N, K, H, W, C, ks, stride, pad;
-  bool operator<(const GemmKey& o) const {
-    const int a[10] = {amode, M, N, K, H, W, C, ks, stride, pad};
-    const int b[10] = {o.amode, o.M, o.N, o.K, o.H, o.W, o.C, o.ks, o.stride, o.pad};
-    for (int i = 0; i < 10; ++i)
-      if (a[i] != b[i]) return a[i] < b[i];
-    return false;
-  }
-};
-static std::map<GemmKey, int> g_tuned;
-static std::mutex g_tuned_mu;
-int g_gemm_autotune = 1;
+// Cache key: engine 0 (this engine) + the shape; the cache is the calling handle's
+// (tune_cache(), mec_common.h).
+static std::array<int, 11> gemm_key(const GemmParams& p) {
+  return {0, p.amode, p.M, p.N, p.K, p.H, p.W, p.C, p.ks, p.stride, p.pad};
+}
 
 // Tile configs (id): 256 / 128 / 64 = 256 x BN with 8 waves; 1128 / 1064 = 128 x BN with
 // 4 waves (64 / 48 KB of LDS, so two blocks share a CU and one block's epilogue overlaps
@@ -583,23 +578,22 @@ static int launch_bn(const GemmParams& p, hipStream_t s, int id) {
       if (p0.amode != A_PLAIN) { set_error("gemm_glds: ping-pong tiles take a plain A only"); return -1; }
       const GemmParams& p = p0;
       const dim3 blk(512);
-      const bool dbg = g_gemm_debug == 2;
       const int nbn = p.N / 256;
-      if (id == 40256) {
-        const dim3 grd(((p.M + 255) / 256) * nbn);
-        if (g_gemm_debug == 4)
-          hipLaunchKernelGGL((gemm_pp_kernel<A_PLAIN, 4, 256>), grd, blk, 0, s, p);
-        else if (dbg)
-          hipLaunchKernelGGL((gemm_pp_kernel<A_PLAIN, 2, 256>), grd, blk, 0, s, p);
-        else
-          hipLaunchKernelGGL((gemm_pp_kernel<A_PLAIN, 0, 256>), grd, blk, 0, s, p);
-      } else {
-        const dim3 grd(((p.M + 127) / 128) * nbn);
-        if (dbg)
-          hipLaunchKernelGGL((gemm_pp_kernel<A_PLAIN, 2, 128>), grd, blk, 0, s, p);
-        else
-          hipLaunchKernelGGL((gemm_pp_kernel<A_PLAIN, 0, 128>), grd, blk, 0, s, p);
-      }
+      const dim3 grd(((p.M + (id == 40256 ? 255 : 127)) / (id == 40256 ? 256 : 128)) * nbn);
+#ifdef MEC_PROBES
+      const int dbg = opt().gemm_debug;
+      if (id == 40256 && dbg == 4)
+        hipLaunchKernelGGL((gemm_pp_kernel<A_PLAIN, 4, 256>), grd, blk, 0, s, p);
+      else if (id == 40256 && dbg == 2)
+        hipLaunchKernelGGL((gemm_pp_kernel<A_PLAIN, 2, 256>), grd, blk, 0, s, p);
+      else if (dbg == 2)
+        hipLaunchKernelGGL((gemm_pp_kernel<A_PLAIN, 2, 128>), grd, blk, 0, s, p);
+      else
+#endif
+      if (id == 40256)
+        hipLaunchKernelGGL((gemm_pp_kernel<A_PLAIN, 0, 256>), grd, blk, 0, s, p);
+      else
+        hipLaunchKernelGGL((gemm_pp_kernel<A_PLAIN, 0, 128>), grd, blk, 0, s, p);
       MEC_LAUNCH_CHECK();
       return 0;
     }
@@ -643,34 +637,23 @@ static int tune_bn(const GemmParams& p, hipStream_t s, int* out_bn) {
   return 0;
 }
 
-int gemm_tuned_bn(int amode, int M, int N, int K) {
-  std::lock_guard<std::mutex> lk(g_tuned_mu);
-  for (const auto& kv : g_tuned)
-    if (kv.first.amode == amode && kv.first.M == M && kv.first.N == N && kv.first.K == K) return kv.second;
-  return 0;
-}
+int gemm_tuned_bn(int amode, int M, int N, int K) { return tune_cache().find_shape(0, amode, M, N, K); }
 
 int launch_gemm_glds(const GemmParams& p, hipStream_t s, int force_bn) {
   if (force_bn) {
     MEC_REQUIRE(p.N % tile_bn(force_bn) == 0, "gemm_glds: forced tile width does not divide N");
     return launch_bn(p, s, force_bn);
   }
-  const GemmKey key{p.amode, p.M, p.N, p.K, p.H, p.W, p.C, p.ks, p.stride, p.pad};
-  int bn = 0;
-  {
-    std::lock_guard<std::mutex> lk(g_tuned_mu);
-    auto it = g_tuned.find(key);
-    if (it != g_tuned.end()) bn = it->second;
-  }
+  const auto key = gemm_key(p);
+  int bn = tune_cache().find(key);
   if (!bn) {
     hipStreamCaptureStatus cs = hipStreamCaptureStatusNone;
-    if (g_gemm_autotune && hipStreamIsCapturing(s, &cs) == hipSuccess && cs == hipStreamCaptureStatusNone) {
+    if (opt().gemm_autotune && hipStreamIsCapturing(s, &cs) == hipSuccess && cs == hipStreamCaptureStatusNone) {
       MEC_TRY(tune_bn(p, s, &bn));
     } else {
       bn = heuristic_bn(p);
     }
-    std::lock_guard<std::mutex> lk(g_tuned_mu);
-    g_tuned[key] = bn;
+    tune_cache().put(key, bn);
     if (getenv("MEC_GEMM_TRACE"))  // one line per distinct shape, at its first launch
       fprintf(stderr, "MEC_GEMM amode=%d M=%d N=%d K=%d H=%d C=%d ks=%d stride=%d act=%d R=%d r_f32=%d tile=%d\n",
               p.amode, p.M, p.N, p.K, p.H, p.C, p.ks, p.stride, p.act, p.R != nullptr, p.r_f32, bn);

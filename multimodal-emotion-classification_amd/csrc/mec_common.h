@@ -1,8 +1,11 @@
 // Shared definitions for the MI355X (gfx950) emotion-inference HIP library.
 #pragma once
 #include <hip/hip_runtime.h>
+#include <array>
 #include <cstddef>
 #include <cstdint>
+#include <map>
+#include <mutex>
 #include <string>
 #include <vector>
 
@@ -59,6 +62,73 @@ enum KernelTag : int {
   TAG_MBV2_LAST = 13,
   TAG_COUNT = 14,
 };
+
+// Tuning knobs (mec_set_option / mec_model_set_option, include/mec.h). Every model handle
+// owns a copy, taken from the process defaults when it is created, and kernels read the
+// options of the handle whose call they serve (opt()), so handles never perturb each other.
+// Every setting of a knob gives the same results, except the probe-build values (compiled only
+// with -DMEC_PROBES: they skip work to time a kernel's parts and return wrong results).
+struct Options {
+  int gemm_impl = 2;        // 1 = register-staged 128x128 engine, 2 = glds pipelined engine
+  int gemm_bn = 0;          // forced f16 GEMM tile id (0 = autotune)
+  int gemm_autotune = 1;
+  int gemm_prefetch_r = 1;  // f16 residual prefetch in short-K GEMMs
+  int gemm_f32_tile = 0;    // forced fp32 GEMM tile id (0 = autotune)
+  // per launch class (profiling tag): forced tile, 0 = autotune. The BERT O-projection is
+  // pinned to 128 x 128 (its candidates time within 2% alone; in the encoder 128 x 128 wins)
+  int gemm_bn_tag[TAG_COUNT] = {0, 0, 0, /*TAG_BERT_OPROJ*/ 11128};
+  int conv3x3_direct = 1;   // ResNet layer1 conv2 on the halo-tile kernel (conv3x3.hip)
+  int resnet_fused_tail = 0;
+  int resnet_chunk = 0;
+  int pw_chain = 2;         // layer1 seam kernels (pw_chain.hip)
+  int pw_chain_form = 0;
+  int bert_qkv_attn = 1;    // fused BERT QKV projection + attention
+  int bert_oproj_ln = 0;    // O-projection + residual + LayerNorm 1 in one kernel (1 | 3)
+  int mbv2_impl = 0;
+  int fusion_r = 4;         // samples per fusion workgroup
+  int fusion_split = 1;     // fusion as 3 launches
+  int gemm_debug = 0, conv3x3_debug = 0, stem_debug = 0;  // probe builds only
+};
+
+// GEMM autotuner results: tile id per (engine, shape), per handle.
+struct TuneCache {
+  std::map<std::array<int, 11>, int> m;
+  std::mutex mu;
+  int find(const std::array<int, 11>& k) {
+    std::lock_guard<std::mutex> lk(mu);
+    auto it = m.find(k);
+    return it == m.end() ? 0 : it->second;
+  }
+  void put(const std::array<int, 11>& k, int v) {
+    std::lock_guard<std::mutex> lk(mu);
+    m[k] = v;
+  }
+  int find_shape(int engine, int amode, int M, int N, int K) {  // any geometry
+    std::lock_guard<std::mutex> lk(mu);
+    for (const auto& kv : m)
+      if (kv.first[0] == engine && kv.first[1] == amode && kv.first[2] == M && kv.first[3] == N && kv.first[4] == K)
+        return kv.second;
+    return 0;
+  }
+};
+
+Options& default_options();      // process defaults (mec_set_option), copied into new handles
+TuneCache& default_tune_cache(); // for the handle-less kernel entry points
+const Options& opt();            // options of the handle the calling thread is serving
+TuneCache& tune_cache();         // its autotune cache
+struct OptScope {                // set for the duration of one C-ABI call on a handle
+  const Options* po;
+  TuneCache* pt;
+  OptScope(const Options* o, TuneCache* t);
+  ~OptScope();
+};
+int set_option(Options& o, const std::string& key, int value);  // 0 = ok, -1 = unknown key / bad value
+constexpr bool kProbes =
+#ifdef MEC_PROBES
+    true;
+#else
+    false;
+#endif
 
 // hipEvent pairs recorded around every launch whose tag matches `tag`.
 struct Prof {
@@ -131,21 +201,13 @@ struct GemmParams {
 
 int launch_gemm(const GemmParams& p, hipStream_t s, Prof* prof, int tag);
 int launch_gemm_glds(const GemmParams& p, hipStream_t s, int force_bn);
-extern int g_gemm_impl;
-extern int g_gemm_bn;
-extern int g_gemm_autotune;
-extern int g_gemm_debug;
-extern int g_gemm_prefetch_r;
 // 3x3/1 conv 64 -> 64 on 56x56 (+ BN shift + ReLU) as a halo-tile kernel (conv3x3.hip);
-// launch_gemm routes matching A_CONV shapes to it while g_conv3x3_direct is set
+// launch_gemm routes matching A_CONV shapes to it while opt().conv3x3_direct is set
 int launch_conv3x3_c64(const f16* x, const f16* w, const float* bias, f16* y, int B, int H, int C, int Cout,
                        hipStream_t s);
-extern int g_conv3x3_direct;
-extern int g_conv3x3_debug;
 int gemm_tuned_bn(int amode, int M, int N, int K);
 // fp32 engine (gemm_f32.hip): f32 A (plain or NHWC conv) and B32, v_mfma_f32_32x32x2_f32
 int launch_gemm_f32(const GemmParams& p, hipStream_t s, Prof* prof, int tag);
 int gemm_f32_tuned(int amode, int M, int N, int K);
-extern int g_gemm_f32_tile;
 
 }  // namespace mec

@@ -767,7 +767,6 @@ int MobileNetModel::create(const float* blob, size_t n) {
 // bit-identical, so the choice changes speed only). Measured at B=256: the wave form wins
 // the stride-2 blocks and the mid-size stride-1 ones, the workgroup form the stem block and
 // the wide late blocks (their depthwise weights no longer fit beside four waves' tiles).
-int g_mbv2_impl = 0;
 
 template <int S, int TO, int CINP, int HIDP, int COUTP, bool EXPAND, bool RES, int STEM>
 static int run_block(const MbArgs& a, int B, hipStream_t s, int impl) {
@@ -794,8 +793,10 @@ static int run_block(const MbArgs& a, int B, hipStream_t s, int impl) {
 
 template <int S, int TO, int CINP, int HIDP, int COUTP, bool EXPAND, bool RES, int STEM>
 static int launch_block(const MbArgs& a, int B, hipStream_t s) {
-  static int choice = 0;  // per block shape, once tuned
-  int impl = g_mbv2_impl;
+  // per block shape, once tuned (engine 2 of the handle's tune cache)
+  const std::array<int, 11> key = {2, S, TO, CINP, HIDP, COUTP, EXPAND, RES, STEM, 0, 0};
+  int choice = tune_cache().find(key);
+  int impl = opt().mbv2_impl;
   if (impl == 0) {
     hipStreamCaptureStatus cs = hipStreamCaptureStatusNone;
     if (!choice && hipStreamIsCapturing(s, &cs) == hipSuccess && cs == hipStreamCaptureStatusNone) {
@@ -817,6 +818,7 @@ static int launch_block(const MbArgs& a, int B, hipStream_t s) {
         if (t[REPS / 2] < best) { best = t[REPS / 2]; choice = cand; }
       }
       for (auto& e : ev) (void)hipEventDestroy(e);
+      tune_cache().put(key, choice);
     }
     impl = choice ? choice : 1;
   }

@@ -19,6 +19,8 @@ struct Model {
   int kind = -1;
   int device = 0;
   int prec = PREC_F16;
+  Options opts = default_options();  // this handle's knobs (mec_model_set_option)
+  TuneCache tune;                    // this handle's GEMM autotune results
   Prof prof;
   virtual ~Model() {}
 };
@@ -134,13 +136,6 @@ int resize_u8(const uint8_t* in, int B, int H, int W, uint8_t* out, int OH, int 
 // ResNet bottleneck conv2 + conv3 + residual + ReLU (stride-1 blocks, w = 64 @ 56 or 128 @ 28)
 int launch_bneck_tail(const f16* t1, const f16* x, const f16* w2, const float* b2, const f16* w3, const float* b3,
                       f16* y, int B, int H, int w, hipStream_t s);
-extern int g_resnet_fused_tail;
-extern int g_resnet_chunk;
-extern int g_bert_qkv_attn;
-extern int g_bert_oproj_ln;
-extern int g_stem_debug;
-extern int g_pw_chain;
-extern int g_pw_chain_form;
 // layer1 seam: conv3 (64 -> 256) + residual + ReLU, then the next block's conv1 (256 -> N2)
 int launch_pw_chain(const f16* t2, const f16* xin, const f16* w3, const float* b3, const f16* w1, const float* b1,
                     f16* xout, f16* t1, int M, int N2, hipStream_t s);
@@ -148,6 +143,5 @@ int launch_pw_chain(const f16* t2, const f16* xin, const f16* w3, const float* b
 int launch_pw_chain_dual(const f16* t2, const f16* x0, const f16* w3ds, const float* b3ds, const f16* w1,
                          const float* b1, f16* xout, f16* t1, int M, hipStream_t s);
 
-extern int g_mbv2_impl;
 
 }  // namespace mec

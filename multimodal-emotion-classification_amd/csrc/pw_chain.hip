@@ -418,7 +418,6 @@ __global__ __launch_bounds__(256, 1) void pw_chain2_kernel(const f16* __restrict
 // 0: per-N2 default (N2 = 64: LDS-weight form; N2 = 128: register-weight form), 1: LDS-weight
 // form, 2: register-weight form. At N2 = 64 the two forms time the same (3.826 / 3.828 ms for
 // the image encoder); at N2 = 128 the LDS-weight form holds only two tile buffers.
-int g_pw_chain_form = 0;
 
 int launch_pw_chain(const f16* t2, const f16* xin, const f16* w3, const float* b3, const f16* w1, const float* b1,
                     f16* xout, f16* t1, int M, int N2, hipStream_t s) {
@@ -432,7 +431,7 @@ int launch_pw_chain(const f16* t2, const f16* xin, const f16* w3, const float* b
   }
   const int ntiles = M / PC_BM;
   const dim3 grd(std::min(ntiles, ncu)), blk(256);
-  const int form = g_pw_chain_form ? g_pw_chain_form : (N2 == 64 ? 1 : 2);
+  const int form = opt().pw_chain_form ? opt().pw_chain_form : (N2 == 64 ? 1 : 2);
   if (N2 == 64 && form == 1)
     hipLaunchKernelGGL(pw_chain_kernel<64>, grd, blk, 0, s, t2, xin, w3, b3, w1, b1, xout, t1, ntiles);
   else if (N2 == 64)

@@ -15,16 +15,12 @@ namespace mec {
 // against 105 + 170 us for the conv2 and conv3 GEMMs (rocprofv3, tools/encoder_profile.py
 // --opt resnet_fused_tail=1). It moves fewer bytes (about 3 TB/s at 315 us) but runs one
 // 4-wave workgroup per CU, so LDS-read and barrier latency inside a tile is exposed.
-int g_resnet_fused_tail = 0;
 // Images per layer1-2 pass (0 = whole batch). Measured at B = 256 (tools/encoder_profile.py
 // --opt resnet_chunk=N): 0 -> 4.23-4.25 ms, 128 -> 4.38, 64 -> 4.44-4.49, 32 -> 5.08: the
 // smaller GEMMs lose more than the cache residency gains, so chunking is off.
-int g_resnet_chunk = 0;
-int g_stem_debug = 0;  // probe variants of stem_pool_kernel (wrong results), tools/ab_option.py
 // layer1 seam kernels (pw_chain.hip): 0 off, 1 the 256 -> 64 seams (block 1 -> 2, 2 -> 3),
 // 2 also the 256 -> 128 seam into layer2 (block 3 -> layer2 block 1). Image encoder at
 // B = 256 (tools/ab_option.py, one process): 4.03 / 3.83 / 3.75 ms for 0 / 1 / 2.
-int g_pw_chain = 2;
 
 // ----------------------------------------------------------------------------- resize
 // Pillow ImagingResample (bilinear, 8bpc): 22-bit fixed-point taps, horizontal pass into
@@ -554,16 +550,18 @@ int ImageModel::forward_u8(const uint8_t* img, int B, int H, int W, int C, float
     const float *sbias = P + st.b_off, *scorr = P + stem_corr_off;
     if (C == 3)
       hipLaunchKernelGGL(stem_pool_kernel<3>, sg, sb, 0, s, stem_in, ntiles, sw, sbias, scorr, X);
-    else if (g_stem_debug == 0)
-      hipLaunchKernelGGL(stem_pool_kernel<1>, sg, sb, 0, s, stem_in, ntiles, sw, sbias, scorr, X);
-    else if (g_stem_debug == 1)  // probe builds (wrong results): no MFMA / no pool / no prefetch
+#ifdef MEC_PROBES
+    else if (opt().stem_debug == 1)  // probe builds (wrong results): no MFMA / no pool / no prefetch
       hipLaunchKernelGGL((stem_pool_kernel<1, 1>), sg, sb, 0, s, stem_in, ntiles, sw, sbias, scorr, X);
-    else if (g_stem_debug == 2)
+    else if (opt().stem_debug == 2)
       hipLaunchKernelGGL((stem_pool_kernel<1, 2>), sg, sb, 0, s, stem_in, ntiles, sw, sbias, scorr, X);
-    else if (g_stem_debug == 4)
+    else if (opt().stem_debug == 4)
       hipLaunchKernelGGL((stem_pool_kernel<1, 4>), sg, sb, 0, s, stem_in, ntiles, sw, sbias, scorr, X);
-    else
+    else if (opt().stem_debug == 7)
       hipLaunchKernelGGL((stem_pool_kernel<1, 7>), sg, sb, 0, s, stem_in, ntiles, sw, sbias, scorr, X);
+#endif
+    else
+      hipLaunchKernelGGL(stem_pool_kernel<1>, sg, sb, 0, s, stem_in, ntiles, sw, sbias, scorr, X);
     MEC_LAUNCH_CHECK();
     MEC_TRY(prof.end(TAG_RESNET_STEM, s));
   }
@@ -587,7 +585,7 @@ int ImageModel::forward_u8(const uint8_t* img, int B, int H, int W, int C, float
         MEC_TRY(launch_gemm(g, s, &prof, TAG_RESNET_CONV1X1));
       }
       conv1_done = false;
-      if (!bk.has_ds && g_resnet_fused_tail && wd == 64 && H == 56) {
+      if (!bk.has_ds && opt().resnet_fused_tail && wd == 64 && H == 56) {
         // conv2 + conv3 + residual + ReLU in one kernel (bottleneck.hip)
         MEC_TRY(prof.begin(TAG_RESNET_CONV3X3, s));
         MEC_TRY(launch_bneck_tail(t1, in, Wt + bk.c2.w_off, P + bk.c2.b_off, Wt + bk.c3.w_off, P + bk.c3.b_off, out,
@@ -601,7 +599,7 @@ int ImageModel::forward_u8(const uint8_t* img, int B, int H, int W, int C, float
       g.M = nb * OH * OH; g.N = wd; g.K = 9 * wd;
       g.H = H; g.W = H; g.C = wd; g.OH = OH; g.OW = OH; g.ks = 3; g.stride = st; g.pad = 1;
       MEC_TRY(launch_gemm(g, s, &prof, TAG_RESNET_CONV3X3));
-      if (bk.has_ds && g_pw_chain && wd == 64 && st == 1 && cin == 64 && OH == 56 && bi + 1 < b1 &&
+      if (bk.has_ds && opt().pw_chain && wd == 64 && st == 1 && cin == 64 && OH == 56 && bi + 1 < b1 &&
           blocks[bi + 1].c1.cin == 256 && blocks[bi + 1].c1.cout == 64) {
         // layer1 block 1: conv3 + downsample + ReLU, then block 2's conv1 (pw_chain.hip)
         const Bottleneck& nx = blocks[bi + 1];
@@ -616,8 +614,8 @@ int ImageModel::forward_u8(const uint8_t* img, int B, int H, int W, int C, float
         g.act = ACT_RELU; g.C16 = out; g.M = nb * OH * OH; g.N = 4 * wd; g.K = wd + cin;
         g.H = H; g.W = H; g.C = cin; g.OH = OH; g.OW = OH; g.ks = 1; g.stride = st; g.pad = 0;
         MEC_TRY(launch_gemm(g, s, &prof, TAG_RESNET_CONV1X1));
-      } else if (g_pw_chain && wd == 64 && OH == 56 && bi + 1 < b1 && blocks[bi + 1].c1.cin == 256 &&
-                 (blocks[bi + 1].c1.cout == 64 || (g_pw_chain == 2 && blocks[bi + 1].c1.cout == 128))) {
+      } else if (opt().pw_chain && wd == 64 && OH == 56 && bi + 1 < b1 && blocks[bi + 1].c1.cin == 256 &&
+                 (blocks[bi + 1].c1.cout == 64 || (opt().pw_chain == 2 && blocks[bi + 1].c1.cout == 128))) {
         // conv3 + residual + ReLU, then the next block's conv1 on the rows just produced
         // (pw_chain.hip): the block output is not read back from HBM. Block 2 -> 3: 186 us
         // against 164 + 111 us for the two GEMMs; block 3 -> layer2 (N2 = 128) in the
@@ -640,14 +638,14 @@ int ImageModel::forward_u8(const uint8_t* img, int B, int H, int W, int C, float
     }
     return 0;
   };
-  // Layers 1-2 can run over chunks of g_resnet_chunk images, so that a chunk's activations
+  // Layers 1-2 can run over chunks of opt().resnet_chunk images, so that a chunk's activations
   // stay in the 256-MB Infinity Cache between a block's producer and consumer kernels (off by
-  // default: measured slower, see g_resnet_chunk). Every GEMM row and conv pixel is computed
+  // default: measured slower, see opt().resnet_chunk). Every GEMM row and conv pixel is computed
   // the same way at any batch split, so the outputs do not depend on the chunk size.
   constexpr size_t kL12 = 7;  // layer1 (3 blocks) + layer2 (4 blocks)
   f16* cur = X;
   f16* other = Y;
-  const int chunk = g_resnet_chunk > 0 ? std::min(g_resnet_chunk, B) : B;
+  const int chunk = opt().resnet_chunk > 0 ? std::min(opt().resnet_chunk, B) : B;
   for (int i0 = 0; i0 < B; i0 += chunk) {
     f16* c = X;
     f16* o = Y;

@@ -8,6 +8,29 @@ static thread_local std::string g_last_error;
 void set_error(const std::string& msg) { g_last_error = msg; }
 const char* last_error() { return g_last_error.c_str(); }
 
+// Options / tune cache of the handle the calling thread is serving (OptScope), else the
+// process defaults (handle-less kernel entry points such as mec_gemm_f16).
+Options& default_options() {
+  static Options o;
+  return o;
+}
+TuneCache& default_tune_cache() {
+  static TuneCache c;
+  return c;
+}
+static thread_local const Options* t_opts = nullptr;
+static thread_local TuneCache* t_tune = nullptr;
+const Options& opt() { return t_opts ? *t_opts : default_options(); }
+TuneCache& tune_cache() { return t_tune ? *t_tune : default_tune_cache(); }
+OptScope::OptScope(const Options* o, TuneCache* t) : po(t_opts), pt(t_tune) {
+  t_opts = o;
+  t_tune = t;
+}
+OptScope::~OptScope() {
+  t_opts = po;
+  t_tune = pt;
+}
+
 int DevBuf::ensure(size_t n) {
   if (n <= bytes) return 0;
   release();

@@ -132,7 +132,6 @@ struct FusionW { const float* p[FUSION_NP]; };
 
 // samples per workgroup (mec_set_option "fusion_r": 1, 2, 4). B = 256 on MI355X: split form
 // 145 / 139 / 118 us at R = 1 / 2 / 4, the single kernel 174 us at R = 2.
-int g_fusion_r = 4;
 constexpr int F_LDIN = 1368, F_LDP = 768, F_LDT = 1280;
 
 template <int FUSION_R>
@@ -273,7 +272,6 @@ __global__ __launch_bounds__(512) void fusion_kernel(FusionW w, const float* __r
 //   fusion_cross_kernel  grid (groups, 3): E_m = LN(P_m + CrossAttn_m(P_m; P_o1, P_o2)),
 //                                          T_m = ReLU(LN(Proj_m(E_m)))             -> Tg
 //   fusion_head_kernel   grid (groups):    attention over T, decision weights, classifier
-int g_fusion_split = 1;  // mec_set_option "fusion_split": 0 = the single fused kernel
 
 template <int R>
 __global__ __launch_bounds__(512) void fusion_proj_kernel(FusionW w, const float* __restrict__ sf,
@@ -473,9 +471,9 @@ int FusionModel::forward(const float* sf, const float* tf, const float* imf, con
   const float* base = w.as<float>();
   for (int i = 0; i < FUSION_NP; ++i) p.p[i] = base + off[i];
   MEC_TRY(prof.begin(TAG_FUSION, s));
-  const int R = g_fusion_r;
+  const int R = opt().fusion_r;
   const dim3 grid((B + R - 1) / R), blk(SF_THREADS);
-  if (g_fusion_split) {
+  if (opt().fusion_split) {
     if (B > ws_batch) {
       MEC_TRY(ws.ensure((size_t)B * 768 * 2 * sizeof(float)));
       ws_batch = B;

@@ -8,7 +8,10 @@ import os
 import threading
 
 _HERE = os.path.dirname(os.path.abspath(__file__))
-LIB_PATH = os.path.join(_HERE, 'libmec_hip.so')
+# MEC_LIB selects another build of the same ABI (tools/ only: libmec_hip_probes.so, the
+# -DMEC_PROBES build whose probe option values return wrong results).
+LIB_PATH = os.environ.get('MEC_LIB') or os.path.join(_HERE, 'libmec_hip.so')
+PROBES_LIB_PATH = os.path.join(_HERE, 'libmec_hip_probes.so')
 
 c_vp = ctypes.c_void_p
 c_int = ctypes.c_int
@@ -39,6 +42,9 @@ SIGNATURES = {
     'mec_conv_f32': (c_int, [c_vp, c_vp, c_vp, c_vp, c_vp, c_int, c_int, c_int, c_int, c_int, c_int, c_int,
                              c_int, c_int, c_vp]),
     'mec_set_option': (c_int, [ctypes.c_char_p, c_int]),
+    'mec_model_set_option': (c_int, [c_vp, ctypes.c_char_p, c_int]),
+    'mec_build_flags': (c_int, []),
+    'mec_model_gemm_query': (c_int, [c_vp, c_int, c_int, c_int, c_int]),
     'mec_gemm_query': (c_int, [c_int, c_int, c_int, c_int]),
     'mec_gemm_f32_query': (c_int, [c_int, c_int, c_int, c_int]),
     'mec_prof_enable': (c_int, [c_vp, c_int]),

@@ -86,6 +86,14 @@ class HipModel:
         except Exception:
             pass
 
+    def set_option(self, key: str, value: int):
+        """One tuning knob of THIS handle (mec_model_set_option; include/mec.h lists them)."""
+        _lib.check(self.lib.mec_model_set_option(self.handle, key.encode(), int(value)), f'set_option({key}={value})')
+
+    def gemm_tile(self, M: int, N: int, K: int, amode: int = 0) -> int:
+        """The tile this handle's autotuner chose for a GEMM shape it has run (0 = not seen)."""
+        return self.lib.mec_model_gemm_query(self.handle, amode, M, N, K)
+
     # hipEvent timing hook (DESIGN.md §Measurement)
     def prof_enable(self, tag: str | int):
         t = _lib.TAGS[tag] if isinstance(tag, str) else int(tag)
@@ -259,17 +267,23 @@ class FusedPipeline:
         # ahead of the image stream's and the image kernels fill the CUs BERT leaves idle
         self._text = (torch.cuda.Stream(device=self.device, priority=0 if image_priority else -1)
                       if (concurrent and (text_priority or image_priority)) else None)
-        self._tuned = False
+        self._tuned = set()  # batch sizes whose GEMM shapes were autotuned (serially)
 
     def forward(self, x_speech, ids, mask, gray, epilogue=None):
         """One batch through the path -> dict of per-modality and fusion outputs (and, with
         `epilogue`, ``(outputs, epilogue(outputs))``, the callable run on the fusion's stream)."""
         main = torch.cuda.current_stream(self.device)
-        if not self.concurrent or not self._tuned:
+        B = int(ids.shape[0])
+        if not self.concurrent or B not in self._tuned:
+            # a batch size not seen yet runs serially on one stream, so each new GEMM shape is
+            # autotuned alone (not against the other encoder's kernels)
+            for st in (self._side, self._text, self._tail):  # nothing else in flight while tuning
+                if st is not None:
+                    main.wait_stream(st)
             sf, sl, sp = self.speech.forward(x_speech)
             tf, tl, tp = self.text.forward(ids, mask)
             imf, il, ip = self.image.forward(gray)
-            self._tuned = True
+            self._tuned.add(B)
             fstream = main
         else:
             side = self._side
@@ -324,6 +338,11 @@ class FusedPipeline:
 
     def models(self):
         return [self.speech, self.text, self.image, self.fusion]
+
+    def set_option(self, key: str, value: int):
+        """Set a tuning knob on every handle of the pipeline that knows it."""
+        for m in self.models():
+            m.set_option(key, value)
 
 
 def to_device(a: np.ndarray, device) -> torch.Tensor:

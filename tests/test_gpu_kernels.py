@@ -183,9 +183,8 @@ def test_fused_bottleneck_tail_bit_identical(dev):
     g = engine.to_device(syn.image_inputs(5, seed=41), dev)
     outs = []
     for v in (0, 1):
-        _lib.check(lib.mec_set_option(b'resnet_fused_tail', v), 'set_option')
+        m.set_option('resnet_fused_tail', v)
         outs.append([t.cpu() for t in m.forward(g)])
-    lib.mec_set_option(b'resnet_fused_tail', 0)
     for a, b in zip(*outs):
         assert torch.equal(a, b)
 
@@ -202,15 +201,11 @@ def test_fusion_split_bit_identical(dev, B):
     args = [torch.randn(B, d, generator=g).to(dev) for d in (64, 768, 512)]
     args += [torch.softmax(torch.randn(B, 7, generator=g), 1).to(dev) for _ in range(3)]
     outs = {}
-    try:
-        for split in (0, 1):
-            for r in (1, 2, 4):
-                _lib.check(lib.mec_set_option(b'fusion_split', split), 'option')
-                _lib.check(lib.mec_set_option(b'fusion_r', r), 'option')
-                outs[split, r] = [t.cpu() for t in m.forward(*args)]
-    finally:
-        lib.mec_set_option(b'fusion_split', 1)
-        lib.mec_set_option(b'fusion_r', 4)
+    for split in (0, 1):
+        for r in (1, 2, 4):
+            m.set_option('fusion_split', split)
+            m.set_option('fusion_r', r)
+            outs[split, r] = [t.cpu() for t in m.forward(*args)]
     for r in (1, 2, 4):
         for a, b in zip(outs[1, r], outs[0, r]):
             assert torch.equal(a, b), r
@@ -256,15 +251,11 @@ def test_pw_chain_bit_identical(dev, B):
     gray = engine.to_device(syn.image_inputs(B, seed=77 + B), dev)
     outs = []
     for chain, form in ((0, 0), (1, 0), (2, 0), (2, 1), (2, 2)):
-        _lib.check(lib.mec_set_option(b'pw_chain', chain), 'option')
-        _lib.check(lib.mec_set_option(b'pw_chain_form', form), 'option')
-        try:
-            res = enc.forward(gray)
-            torch.cuda.synchronize()
-            outs.append([t.cpu() for t in res])
-        finally:
-            lib.mec_set_option(b'pw_chain', 1)
-            lib.mec_set_option(b'pw_chain_form', 0)
+        enc.set_option('pw_chain', chain)
+        enc.set_option('pw_chain_form', form)
+        res = enc.forward(gray)
+        torch.cuda.synchronize()
+        outs.append([t.cpu() for t in res])
     for o in outs[1:]:
         for a, b in zip(o, outs[0]):
             assert torch.equal(a, b)

@@ -82,14 +82,12 @@ def test_image_inference_mbv2(dev):
 @pytest.mark.parametrize('C', [1, 3])
 def test_mbv2_wave_and_workgroup_forms_bit_identical(mb, dev, C):
     """mbv2_impl 2 (wave-autonomous 4x4 tiles) == mbv2_impl 1 (workgroup 8x8 / 7x7 tiles)."""
-    from mec import _lib
-    lib = _lib.load()
     img = syn.randint(30 + C, 'in/mbv2_forms', (5, 224, 224, C), 0, 256).astype(np.uint8)
     x = engine.to_device(img, dev)
     outs = []
     for impl in (1, 2):
-        _lib.check(lib.mec_set_option(b'mbv2_impl', impl), 'set_option')
+        mb.set_option('mbv2_impl', impl)
         outs.append(_np(mb.forward_u8(x)))
-    lib.mec_set_option(b"mbv2_impl", 0)
+    mb.set_option('mbv2_impl', 0)
     for a, b in zip(*outs):
         np.testing.assert_array_equal(a, b)

@@ -170,17 +170,16 @@ def test_text_qkv_attn_bit_identical(models, dev, B):
     """BERT with the fused QKV-projection + attention kernel and with the QKV GEMM followed by
     the attention kernel: identical CLS features, logits and probabilities (B = 9: 54
     workgroups over the XCD remap with a remainder)."""
-    from mec import _lib
-    lib = _lib.load()
     ids, mask = syn.text_inputs(B, 128, seed=300 + B, ragged=True)
     args = (engine.to_device(ids, dev), engine.to_device(mask, dev))
+    enc = models['text']
     outs = []
     for fused in (1, 0):
-        _lib.check(lib.mec_set_option(b'bert_qkv_attn', fused), 'option')
+        enc.set_option('bert_qkv_attn', fused)
         try:
-            outs.append(_np(models['text'].forward(*args)))
+            outs.append(_np(enc.forward(*args)))
         finally:
-            lib.mec_set_option(b'bert_qkv_attn', 1)
+            enc.set_option('bert_qkv_attn', 1)
     for a, b in zip(*outs):
         np.testing.assert_array_equal(a, b)
 
@@ -190,21 +189,26 @@ def test_text_qkv_attn_bit_identical(models, dev, B):
 def test_text_oproj_ln_fused_matches_unfused(models, dev, B, form):
     """BERT with the O-projection + residual + LayerNorm-1 kernel against the O-proj GEMM
     followed by the LayerNorm kernel. The GEMM sums are accumulated in the same k order, but
-    the row statistics are summed in another order, so the bar is rounding-level agreement
-    (CLS |d| <= 2e-3 after 12 layers, probs <= 1e-3) and identical argmax, not bit identity."""
-    from mec import _lib
-    lib = _lib.load()
+    the row statistics are summed in another order, so the bar is relative to the unfused
+    path's own f16 error: against the oracle, the fused kernel's CLS and probs errors may be at
+    most 1.5x the unfused path's (plus an ulp-scale floor), with identical argmax."""
     ids, mask = syn.text_inputs(B, 128, seed=400 + B, ragged=True)
     args = (engine.to_device(ids, dev), engine.to_device(mask, dev))
+    enc = models['text']
     outs = []
     for fused in (form, 0):
-        _lib.check(lib.mec_set_option(b'bert_oproj_ln', fused), 'option')
+        enc.set_option('bert_oproj_ln', fused)
         try:
-            outs.append(_np(models['text'].forward(*args)))
+            outs.append(_np(enc.forward(*args)))
         finally:
-            lib.mec_set_option(b'bert_oproj_ln', 0)  # the default
+            enc.set_option('bert_oproj_ln', 0)  # the default
     (cf, lf, pf), (cu, lu, pu) = outs
-    print(f'form {form} B={B}: cls max|d| {np.abs(cf - cu).max():.3g}, probs max|d| {np.abs(pf - pu).max():.3g}')
-    assert np.abs(cf - cu).max() <= 2e-3
-    assert np.abs(pf - pu).max() <= 1e-3  # north_star's probs bar; the synthetic head has large logits
+    rc, rl, rp = o_t.forward(syn.weights('text'), ids, mask)
+    ec_f, ec_u = np.abs(cf - rc).max(), np.abs(cu - rc).max()
+    ep_f, ep_u = np.abs(pf - rp).max(), np.abs(pu - rp).max()
+    print(f'form {form} B={B}: vs oracle cls {ec_f:.3g} (unfused {ec_u:.3g}), probs {ep_f:.3g} (unfused {ep_u:.3g}); '
+          f'fused vs unfused cls {np.abs(cf - cu).max():.3g}')
+    assert ec_f <= 1.5 * ec_u + 1e-4
+    assert ep_f <= 1.5 * ep_u + 1e-5
+    assert ep_f <= 1e-3  # north_star's probs bar
     assert (pf.argmax(1) == pu.argmax(1)).all()

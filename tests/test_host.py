@@ -64,6 +64,14 @@ def test_blob_sizes_agree_with_library():
     assert lib.mec_blob_size(9) == -1
 
 
+def test_model_option_and_query_need_a_handle():
+    lib = _lib.load()
+    assert lib.mec_model_set_option(None, b'fusion_r', 2) == -1
+    assert b'null model' in lib.mec_last_error()
+    assert lib.mec_model_gemm_query(None, 0, 256, 256, 256) == -1
+    assert lib.mec_precision(None) == -1
+
+
 def test_c_abi_argument_errors_without_gpu():
     import ctypes
     lib = _lib.load()
@@ -78,14 +86,21 @@ def test_c_abi_argument_errors_without_gpu():
 
 def test_option_validation_without_gpu():
     """mec_set_option accepts each knob's documented values (include/mec.h) and rejects the
-    rest; it only sets process globals, so this runs without a GPU. Defaults restored."""
+    rest, including every probe value (the product library is not a -DMEC_PROBES build); it
+    only sets the process defaults, so this runs without a GPU. Defaults restored."""
     lib = _lib.load()
+    assert lib.mec_build_flags() == 0, 'the product library must not be a probe build'
+    probes = [(b'gemm_debug', 1), (b'gemm_debug', 2), (b'gemm_debug', 4), (b'stem_debug', 1), (b'conv3x3_debug', 2),
+              (b'bert_qkv_attn', 2), (b'bert_qkv_attn', 3), (b'bert_oproj_ln', 2), (b'bert_oproj_ln', 4)]
+    for k, v in probes:
+        assert lib.mec_set_option(k, v) == -1, (k, v)
+        assert b'MEC_PROBES' in lib.mec_last_error()
     ok = [(b'fusion_r', 1), (b'fusion_r', 4), (b'fusion_split', 0), (b'fusion_split', 1),
           (b'bert_qkv_attn', 0), (b'bert_qkv_attn', 1), (b'bert_oproj_ln', 0), (b'bert_oproj_ln', 1),
           (b'gemm_bn', 40256), (b'gemm_bn', 0),
           (b'gemm_bn_tag', 3 * 100000 + 40256), (b'gemm_bn_tag', 3 * 100000 + 11128),
-          (b'gemm_debug', 0)]
-    bad = [(b'fusion_r', 3), (b'fusion_split', 2), (b'bert_qkv_attn', 4), (b'bert_oproj_ln', 5), (b'gemm_bn', 12345),
+          (b'gemm_debug', 0), (b'gemm_f32_tile', 3), (b'gemm_f32_tile', 0), (b'bert_oproj_ln', 3)]
+    bad = [(b'gemm_f32_tile', 5), (b'fusion_r', 3), (b'fusion_split', 2), (b'bert_qkv_attn', 4), (b'bert_oproj_ln', 5), (b'gemm_bn', 12345),
            (b'gemm_bn', 42256), (b'gemm_bn_tag', 11128), (b'gemm_bn_tag', 14 * 100000 + 256),
            (b'gemm_bn_tag', 3 * 100000 + 999), (b'gemm_bn_tag', -1), (b'gemm_debug', 5)]
     try:
@@ -96,6 +111,7 @@ def test_option_validation_without_gpu():
             assert b'bad value' in lib.mec_last_error()
     finally:  # the defaults
         for k, v in [(b'fusion_r', 4), (b'fusion_split', 1), (b'bert_qkv_attn', 1), (b'bert_oproj_ln', 0),
+                     (b'gemm_f32_tile', 0),
                      (b'gemm_bn', 0),
                      (b'gemm_bn_tag', 3 * 100000 + 11128), (b'gemm_debug', 0)]:
             lib.mec_set_option(k, v)

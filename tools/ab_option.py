@@ -1,4 +1,4 @@
-"""Interleaved A/B of a library option (mec_set_option) on one encoder at B=256.
+"""Interleaved A/B of a library option (mec_model_set_option) on one encoder at B=256.
 
     python tools/ab_option.py --enc image --opt resnet_fused_tail --values 0 1
 
@@ -13,6 +13,10 @@ import sys
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 sys.path.insert(0, os.path.join(ROOT, 'multimodal-emotion-classification_amd'))
 
+if '--probes' in sys.argv:  # probe option values: the -DMEC_PROBES build (csrc: make probes)
+    os.environ.setdefault('MEC_LIB', os.path.join(ROOT, 'multimodal-emotion-classification_amd', 'mec',
+                                                  'libmec_hip_probes.so'))
+
 import torch  # noqa: E402
 
 from mec import _lib, engine, synthetic as syn  # noqa: E402
@@ -25,6 +29,7 @@ def main():
     ap.add_argument('--values', type=int, nargs='+', required=True)
     ap.add_argument('--iters', type=int, default=5)
     ap.add_argument('--rounds', type=int, default=5)
+    ap.add_argument('--probes', action='store_true', help='load libmec_hip_probes.so (probe option values)')
     a = ap.parse_args()
     dev = torch.device('cuda', 0)
     lib = _lib.load()
@@ -53,14 +58,14 @@ def main():
         return r if isinstance(r, (tuple, list)) else (r,)
 
     for v in a.values:
-        _lib.check(lib.mec_set_option(a.opt.encode(), v), 'set_option')
+        m.set_option(a.opt, v)  # this handle's knob (the pipeline: every handle's)
         outs[v] = [t.clone() for t in fwd()]
         torch.cuda.synchronize()
         fwd()
     torch.cuda.synchronize()
     for _ in range(a.rounds):
         for v in a.values:
-            lib.mec_set_option(a.opt.encode(), v)
+            m.set_option(a.opt, v)
             torch.cuda.synchronize()
             t0 = time.perf_counter()
             for _ in range(a.iters):

@@ -12,6 +12,9 @@ import sys
 
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 sys.path.insert(0, os.path.join(ROOT, 'multimodal-emotion-classification_amd'))
+# probe option values (*_debug) exist only in the -DMEC_PROBES build (csrc: make probes)
+os.environ.setdefault('MEC_LIB', os.path.join(ROOT, 'multimodal-emotion-classification_amd', 'mec',
+                                              'libmec_hip_probes.so'))
 
 import torch  # noqa: E402
 

@@ -18,7 +18,6 @@ def t(fn, it=20):
     for _ in range(it): fn()
     e1.record(); torch.cuda.synchronize(); return e0.elapsed_time(e1) / it * 1e3
 for r in (1, 2, 4):
-    lib.mec_set_option(b'fusion_r', r)
+    fu.set_option('fusion_r', r)
     print('fusion R=%d  %.1f us' % (r, t(lambda: fu.forward(*args))))
-lib.mec_set_option(b'fusion_r', 2)
 print('speech %.1f us' % t(lambda: sp.forward(x)))
