@@ -28,6 +28,16 @@ namespace mec {
 
 __device__ __attribute__((aligned(64))) uint4 g_zero_page_f32[16];
 
+// LDS DMA issued from inline asm (16 B per lane to M0 + 16 x lane). Issued as the builtin,
+// hipcc's waitcnt pass drains vmcnt(0) before the first fragment read of every K tile, i.e.
+// waits for the DMA of the NEXT tile too, which serialises the ring (the f16 engine's float-
+// free reads escape it; see conv3x3.hip). Hidden from it, the ring is ordered only by this
+// kernel's counted vmcnt waits and barriers.
+#pragma clang diagnostic ignored "-Winline-asm"
+__device__ __forceinline__ void f32_dma(const void* src, uint32_t lds) {
+  asm volatile("s_mov_b32 m0, %1\n\ts_nop 0\n\tglobal_load_lds_dwordx4 %0, off" ::"v"(src), "s"(lds) : "memory", "m0");
+}
+
 template <int BM, int BN, int WM, int WN, int NS, int AM>
 __global__ __launch_bounds__(64 * WM * WN, (WM * WN == 4) ? 2 : 1) void gemm_f32_kernel(const GemmParams p) {
   constexpr int BK = 32;                    // floats per K tile (128-B LDS rows)
@@ -91,15 +101,16 @@ __global__ __launch_bounds__(64 * WM * WN, (WM * WN == 4) ? 2 : 1) void gemm_f32
   }
   const float* zero = reinterpret_cast<const float*>(g_zero_page_f32);
 
+  const uint32_t lds0 = (uint32_t)(uintptr_t)((__attribute__((address_space(3))) float*)smem);
   auto issue = [&](int stage, int kt) {
     const int k0 = kt * BK;
-    float* sA = smem + stage * STAGE;
-    float* sB = sA + BM * BK;
+    const uint32_t sA = lds0 + (uint32_t)(stage * STAGE) * 4u;
+    const uint32_t sB = sA + (uint32_t)(BM * BK) * 4u;
     if constexpr (AM == A_PLAIN) {
 #pragma unroll
       for (int i = 0; i < AI; ++i) {
         const float* src = a_ok[i] ? a_src[i] + k0 : zero;
-        __builtin_amdgcn_global_load_lds((const void*)src, (lds_vptr)(sA + (wave * AI + i) * RPI * BK), 16, 0, 0);
+        f32_dma(src, sA + (uint32_t)((wave * AI + i) * RPI * BK) * 4u);
       }
     } else {
       const int tap = k0 / p.C;
@@ -111,13 +122,12 @@ __global__ __launch_bounds__(64 * WM * WN, (WM * WN == 4) ? 2 : 1) void gemm_f32
         const int ih = a_ih0[i] + kh, iw = a_iw0[i] + kw;
         const bool ok = a_ok[i] && ih >= 0 && ih < p.H && iw >= 0 && iw < p.W;
         const float* src = ok ? a_src[i] + ((size_t)ih * p.W + iw) * p.C + c0 : zero;
-        __builtin_amdgcn_global_load_lds((const void*)src, (lds_vptr)(sA + (wave * AI + i) * RPI * BK), 16, 0, 0);
+        f32_dma(src, sA + (uint32_t)((wave * AI + i) * RPI * BK) * 4u);
       }
     }
 #pragma unroll
     for (int j = 0; j < BI; ++j)
-      __builtin_amdgcn_global_load_lds((const void*)(b_src[j] + k0), (lds_vptr)(sB + (wave * BI + j) * RPI * BK), 16,
-                                       0, 0);
+      f32_dma(b_src[j] + k0, sB + (uint32_t)((wave * BI + j) * RPI * BK) * 4u);
   };
 
   floatx16 acc[TI][TJ];

@@ -26,6 +26,7 @@ def main():
     ap.add_argument('--iters', type=int, default=5)
     ap.add_argument('--batch', type=int, default=256)
     ap.add_argument('--opt', action='append', default=[], help='library option NAME=VALUE (mec_set_option)')
+    ap.add_argument('--precision', default='f16', choices=['f16', 'fp32'])
     a = ap.parse_args()
     dev = torch.device('cuda', 0)
     B = a.batch
@@ -35,12 +36,12 @@ def main():
             k, v = kv.split('=')
             _lib.check(_lib.load().mec_set_option(k.encode(), int(v)), f'mec_set_option({kv})')
     if a.enc == 'text':
-        m = engine.TextEncoder(device=dev)
+        m = engine.TextEncoder(device=dev, precision=a.precision)
         ids, mask = syn.text_inputs(B, 128, seed=0)
         args = (engine.to_device(ids, dev), engine.to_device(mask, dev))
         fn = lambda: m.forward(*args)  # noqa: E731
     elif a.enc == 'image':
-        m = engine.ImageEncoder(device=dev)
+        m = engine.ImageEncoder(device=dev, precision=a.precision)
         g = engine.to_device(syn.image_inputs(B, seed=0), dev)
         fn = lambda: m.forward(g)  # noqa: E731
     elif a.enc == 'image_mbv2':
@@ -57,7 +58,7 @@ def main():
         args += [torch.softmax(torch.rand(B, 7, device=dev), 1) for _ in range(3)]
         fn = lambda: m.forward(*args)  # noqa: E731
     else:
-        m = engine.FusedPipeline(seed=1234, device=dev)
+        m = engine.FusedPipeline(seed=1234, device=dev, precision=a.precision)
         x = engine.to_device(syn.speech_inputs(B, seed=0), dev)
         ids, mask = syn.text_inputs(B, 128, seed=0)
         ids, mask = engine.to_device(ids, dev), engine.to_device(mask, dev)
@@ -74,7 +75,7 @@ def main():
     e1.record()
     torch.cuda._sleep(1)
     torch.cuda.synchronize()
-    print(json.dumps({'enc': a.enc, 'batch': B, 'ms_per_iter': e0.elapsed_time(e1) / a.iters}))
+    print(json.dumps({'enc': a.enc, 'batch': B, 'precision': a.precision, 'ms_per_iter': e0.elapsed_time(e1) / a.iters}))
 
 
 if __name__ == '__main__':
