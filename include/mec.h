@@ -25,7 +25,7 @@ extern "C" {
 
 typedef struct mec_model mec_model;
 
-enum { MEC_SPEECH = 0, MEC_TEXT = 1, MEC_IMAGE = 2, MEC_FUSION = 3, MEC_IMAGE_MBV2 = 4 };
+enum { MEC_SPEECH = 0, MEC_TEXT = 1, MEC_IMAGE = 2, MEC_FUSION = 3, MEC_IMAGE_MBV2 = 4, MEC_AUDIO = 5 };
 /* MEC_IMAGE is the reference's ResNet50 image model (inference/image_inference.py:55-65);
  * MEC_IMAGE_MBV2 the same head on a torchvision mobilenet_v2 backbone (README.md:13 names
  * MobileNetV2; blob = state_dict order of mec/synthetic.py:image_mbv2_spec). Both kinds are
@@ -93,6 +93,15 @@ int mec_image_fwd_u8(mec_model* m, const uint8_t* img, int B, int H, int W, int 
 int mec_fusion_fwd(mec_model* m, const float* s_feat, const float* t_feat, const float* i_feat,
                    const float* s_pred, const float* t_pred, const float* i_pred, int B, float* logits,
                    float* probs, float* attn_w, float* dec_w, void* stream);
+
+/* Speech features on the GPU (MEC_AUDIO handle; blob = {sample_rate, 2048, 512, 128, n_mfcc},
+ * i.e. config.py's SAMPLE_RATE / N_MFCC and librosa's n_fft / hop / n_mels). wave: f32[B, n]
+ * fixed-length waveforms (load_audio's pad/trim applied). feat: f32[B, n_mfcc + 16] =
+ * [mean MFCC | mean chroma (12) | mean zcr, centroid, rolloff, rms]; tuning: f32[B] (the
+ * estimate_tuning value chroma used) or NULL. Replaces preprocess_audio's feature arithmetic
+ *   preprocessing/audio_preprocessing.py:22-46 (librosa 0.10.0 mfcc / chroma_stft /
+ *   zero_crossing_rate / spectral_centroid / spectral_rolloff / rms). */
+int mec_audio_fwd(mec_model* m, const float* wave, int B, int n_samples, float* feat, float* tuning, void* stream);
 
 /* Weighted-average fallback (float64, like numpy); any of s/t/i may be NULL (= zeros).
  * Replaces MultimodalFusion.fuse_predictions  inference/multimodal_fusion.py:184-199. */

@@ -62,6 +62,7 @@ size_t blob_floats(int kind) {
       s += (size_t)256 * 263 + 256 + 512 + 128 * 256 + 128 + 7 * 128 + 7;
       return s;
     }
+    case KIND_AUDIO: return 5;  // [sample_rate, n_fft, hop, n_mels, n_mfcc]
     default: return 0;
   }
 }
@@ -147,11 +148,12 @@ int mec_create_ex(int kind, const float* host_blob, size_t n, int device, int pr
       case KIND_IMAGE: { auto* p = new ImageModel(); p->prec = precision; impl = p; rc = p->create(host_blob, n); break; }
       case KIND_FUSION: { auto* p = new FusionModel(); impl = p; rc = p->create(host_blob, n); break; }
       case KIND_IMAGE_MBV2: { auto* p = new MobileNetModel(); impl = p; rc = p->create(host_blob, n); break; }
+      case KIND_AUDIO: { auto* p = new AudioModel(); impl = p; rc = p->create(host_blob, n); break; }
     }
     if (rc != 0) { delete impl; return -1; }
     impl->kind = kind;
     impl->device = device;
-    impl->prec = (kind == KIND_SPEECH || kind == KIND_FUSION) ? MEC_PREC_FP32 : precision;
+    impl->prec = (kind == KIND_SPEECH || kind == KIND_FUSION || kind == KIND_AUDIO) ? MEC_PREC_FP32 : precision;
     *out = new mec_model{impl};
     return 0;
   })
@@ -212,6 +214,15 @@ int mec_fusion_fwd(mec_model* m, const float* s_feat, const float* t_feat, const
     if (!p) return -1;
     OptScope sc(&p->opts, &p->tune);
     return p->forward(s_feat, t_feat, i_feat, s_pred, t_pred, i_pred, B, logits, probs, attn_w, dec_w, S(stream));
+  })
+}
+
+int mec_audio_fwd(mec_model* m, const float* wave, int B, int n_samples, float* feat, float* tuning, void* stream) {
+  API_GUARD({
+    auto* p = as<AudioModel>(m, KIND_AUDIO);
+    if (!p) return -1;
+    OptScope sc(&p->opts, &p->tune);
+    return p->forward(wave, B, n_samples, feat, tuning, S(stream));
   })
 }
 

@@ -60,7 +60,8 @@ enum KernelTag : int {
   TAG_FUSION = 11,
   TAG_MBV2_BLOCK = 12,
   TAG_MBV2_LAST = 13,
-  TAG_COUNT = 14,
+  TAG_AUDIO = 14,
+  TAG_COUNT = 15,
 };
 
 // Tuning knobs (mec_set_option / mec_model_set_option, include/mec.h). Every model handle

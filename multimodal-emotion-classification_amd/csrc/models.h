@@ -6,7 +6,7 @@
 
 namespace mec {
 
-enum ModelKind : int { KIND_SPEECH = 0, KIND_TEXT = 1, KIND_IMAGE = 2, KIND_FUSION = 3, KIND_IMAGE_MBV2 = 4 };
+enum ModelKind : int { KIND_SPEECH = 0, KIND_TEXT = 1, KIND_IMAGE = 2, KIND_FUSION = 3, KIND_IMAGE_MBV2 = 4, KIND_AUDIO = 5 };
 
 size_t blob_floats(int kind);
 
@@ -31,6 +31,19 @@ struct SpeechModel : Model {
   size_t off_mean = 0, off_scale = 0, off_W[6] = {}, off_b[6] = {}, off_inv[5] = {}, off_shift[5] = {};
   int create(const float* blob, size_t n);
   int forward(const float* x, int B, float* feat, float* logits, float* probs, hipStream_t s);
+};
+
+// ---------------------------------------------------------------- speech features (audio.hip)
+// blob = [sample_rate, n_fft, hop, n_mels, n_mfcc] (config.py:57-59 + librosa defaults); the
+// handle owns the filterbank / window / twiddle tables and a grow-only workspace.
+struct AudioModel : Model {
+  int sr = 22050, n_mfcc = 40, lo_bin = 0, hi_bin = 0;
+  DevBuf tables, ws;
+  size_t off_hann = 0, off_tw = 0, off_post = 0, off_freq = 0, off_dct = 0, off_chroma = 0, off_meloff = 0,
+         off_melbin = 0, off_melw = 0;
+  int create(const float* blob, size_t n);
+  // wave f32 [B, L] -> feat f32 [B, n_mfcc + 16]; tuning f32 [B] (estimate_tuning) or null
+  int forward(const float* wave, int B, int L, float* feat, float* tuning, hipStream_t s);
 };
 
 // ---------------------------------------------------------------- fusion model

@@ -32,6 +32,7 @@ SIGNATURES = {
     'mec_image_fwd': (c_int, [c_vp, c_vp, c_int, c_vp, c_vp, c_vp, c_vp]),
     'mec_image_fwd_u8': (c_int, [c_vp, c_vp, c_int, c_int, c_int, c_int, c_vp, c_vp, c_vp, c_vp]),
     'mec_fusion_fwd': (c_int, [c_vp, c_vp, c_vp, c_vp, c_vp, c_vp, c_vp, c_int, c_vp, c_vp, c_vp, c_vp, c_vp]),
+    'mec_audio_fwd': (c_int, [c_vp, c_vp, c_int, c_int, c_vp, c_vp, c_vp]),
     'mec_fuse_weighted': (c_int, [c_vp, c_vp, c_vp, c_int, c_vp, c_vp]),
     'mec_fuse_weighted_f64': (c_int, [c_vp, c_vp, c_vp, c_int, c_vp, c_vp]),
     'mec_resize_u8': (c_int, [c_vp, c_int, c_int, c_int, c_vp, c_int, c_int, c_vp]),
@@ -54,7 +55,7 @@ SIGNATURES = {
 # Kernel tags for mec_prof_enable (csrc/mec_common.h KernelTag).
 TAGS = {'bert_qkv': 1, 'bert_attn': 2, 'bert_oproj': 3, 'bert_ffn1': 4, 'bert_ffn2': 5, 'bert_ln': 6,
         'resnet_conv3x3': 7, 'resnet_conv1x1': 8, 'resnet_stem': 9, 'speech': 10, 'fusion': 11,
-        'mbv2_blocks': 12, 'mbv2_last': 13}
+        'mbv2_blocks': 12, 'mbv2_last': 13, 'audio': 14}
 
 
 # Handle precision (include/mec.h MEC_PREC_*): 'f16' = f16 MFMA operands with fp32

@@ -177,6 +177,43 @@ class MobileNetImageEncoder(ImageEncoder):
 
 IMAGE_BACKBONES = {'resnet50': ImageEncoder, 'mobilenet_v2': MobileNetImageEncoder}
 
+AUDIO_KIND = 5  # include/mec.h MEC_AUDIO
+N_FFT, HOP, N_MELS = 2048, 512, 128  # librosa defaults the reference never overrides
+
+
+class AudioFeaturizer(HipModel):
+    """preprocess_audio's 56-d speech features (preprocessing/audio_preprocessing.py:22-46:
+    mean MFCC-40 | mean chroma-12 | mean zcr, centroid, rolloff, rms) computed on the GPU
+    (csrc/audio.hip) for a batch of fixed-length waveforms (load_audio's pad/trim applied)."""
+    kind = 'audio'
+
+    def __init__(self, sample_rate: int = 22050, n_mfcc: int = 40, device=None):
+        self.lib = _lib.load()
+        self.device = require_gpu(device)
+        self.precision = 'fp32'
+        self.sample_rate, self.n_mfcc = int(sample_rate), int(n_mfcc)
+        self.n_features = self.n_mfcc + 16
+        blob = np.array([sample_rate, N_FFT, HOP, N_MELS, n_mfcc], np.float32)
+        h = ctypes.c_void_p()
+        torch.cuda.set_device(self.device)
+        _lib.check(self.lib.mec_create_ex(AUDIO_KIND, blob.ctypes.data_as(_lib.c_fp), blob.size, self.device.index,
+                                          _lib.PRECISIONS['fp32'], ctypes.byref(h)), 'mec_create(audio)')
+        self.handle = h
+        self._lock = threading.Lock()
+
+    def forward(self, wave: torch.Tensor, return_tuning: bool = False):
+        """wave f32 [B, n] -> features f32 [B, n_mfcc + 16] (and the chroma tuning [B])."""
+        if wave.dim() != 2:
+            raise ValueError('wave: expected [B, n_samples]')
+        B, n = wave.shape
+        _check_tensor('wave', wave, torch.float32, (B, n), self.device)
+        feat = self._empty(B, self.n_features)
+        tun = self._empty(B) if return_tuning else None
+        with self._lock:
+            _lib.check(self.lib.mec_audio_fwd(self.handle, _ptr(wave), B, n, _ptr(feat), _ptr(tun),
+                                              _stream(self.device)), 'mec_audio_fwd')
+        return (feat, tun) if return_tuning else feat
+
 
 class FusionHead(HipModel):
     kind = 'fusion'
