@@ -182,6 +182,12 @@ def per_config(pipe, dev, precision, iters=10):
     runs = {'speech_b32': (32, lambda: pipe.speech.forward(xs)),
             'image_resnet50_b256': (256, lambda: pipe.image.forward(g)),
             'text_bert_b128': (128, lambda: pipe.text.forward(ids, mask))}
+    # speech from waveforms (§8(f) row 4): GPU features (csrc/audio.hip) then the DNN, B = 32
+    # clips of 3 s at 22050 Hz (config.py:57-58)
+    sys.path.insert(0, ROOT)
+    af = engine.AudioFeaturizer(device=dev)
+    wv = torch.from_numpy(np.random.default_rng(7).standard_normal((32, 66150)).astype(np.float32)).to(dev)
+    runs['speech_waveform_b32'] = (32, lambda: pipe.speech.forward(af.forward(wv)))
     mb = None
     if precision == 'f16':
         mb = engine.MobileNetImageEncoder(device=dev)
@@ -201,6 +207,7 @@ def per_config(pipe, dev, precision, iters=10):
         out[name] = {'samples_per_s': b / ms * 1e3, 'ms_per_batch': ms}
     if mb is not None:
         mb.close()
+    af.close()
     return out
 
 

@@ -3,13 +3,15 @@ Speech inference on the MI355X HIP path — drop-in for the reference's
 inference/speech_inference.py (same class, methods, result dicts).
 
 The model arithmetic (StandardScaler -> 5 x [Dense, BN, ReLU] -> Dense7 -> softmax) runs in
-one fused HIP kernel (csrc/speech_fusion.hip) through libmec_hip.so. Audio decoding and
-MFCC/chroma/spectral features stay in the reference's untouched preprocessing/ package
-(imported lazily from the tree this module is dropped into, as the reference does at
-inference/speech_inference.py:9).
+one fused HIP kernel (csrc/speech_fusion.hip) through libmec_hip.so, and the 56-d
+MFCC / chroma / spectral features of preprocess_audio (preprocessing/audio_preprocessing.py:
+22-46) run on the GPU too (csrc/audio.hip). Only audio decoding and resampling stay in the
+reference's untouched preprocessing/ package (load_audio, imported lazily from the tree this
+module is dropped into, as the reference does at inference/speech_inference.py:9).
 
 Added beyond the reference: predict_features(features) for an already-extracted 56-d
-vector, and predict_batch(x) for a device-resident [B,56] batch.
+vector, predict_batch(x) for a device-resident [B,56] batch, and features_from_waveforms /
+predict_waveforms for device-resident [B, n] waveforms.
 """
 
 from typing import Dict
@@ -36,6 +38,29 @@ class SpeechInference:
             # No silent CPU fallback: a missing libmec_hip.so or GPU raises MecError here.
             self.model = engine.SpeechEncoder(w, device=device)
         self.device = self.model.device if self.model is not None else None
+        self._audio = None
+
+    def _featurizer(self):
+        if self._audio is None:
+            self._audio = engine.AudioFeaturizer(Config.SAMPLE_RATE, Config.N_MFCC, device=self.device)
+        return self._audio
+
+    def _file_features(self, audio_file_path: str) -> np.ndarray:
+        # preprocess_audio (audio_preprocessing.py:40-46): load_audio on the host (decode,
+        # resample, pad/trim), the feature arithmetic on the GPU
+        audio, sr = _preprocessing().load_audio(audio_file_path)
+        if int(sr) != Config.SAMPLE_RATE:
+            return _preprocessing().preprocess_audio(audio_file_path)
+        wave = engine.to_device(np.asarray(audio, np.float32).reshape(1, -1), self.device)
+        return self._featurizer().forward(wave).cpu().numpy()[0]
+
+    def features_from_waveforms(self, wave):
+        """wave: device f32 [B, n] (load_audio's fixed length) -> raw 56-d features [B, 56]."""
+        return self._featurizer().forward(wave)
+
+    def predict_waveforms(self, wave):
+        """wave: device f32 [B, n] -> (feat [B,64], logits [B,7], probs [B,7])."""
+        return self.predict_batch(self.features_from_waveforms(wave))
 
     def _heuristic_predict(self, audio_path: str) -> Dict:
         # reference :36-58 — RMS energy / spectral centroid rule
@@ -70,15 +95,13 @@ class SpeechInference:
     def predict(self, audio_file_path: str) -> Dict:
         if self.model is None:
             return self._heuristic_predict(audio_file_path)
-        features = _preprocessing().preprocess_audio(audio_file_path)
-        return self.predict_features(features)
+        return self.predict_features(self._file_features(audio_file_path))
 
     def extract_features(self, audio_file_path: str):
         """(64-d block-5 ReLU feature, 7 probs) — one forward instead of the reference's three."""
         if self.model is None:
             return None, None
-        features = _preprocessing().preprocess_audio(audio_file_path)
-        return self._forward(features)
+        return self._forward(self._file_features(audio_file_path))
 
     def predict_batch(self, x):
         """x: device f32 [B,56] raw features -> (feat [B,64], logits [B,7], probs [B,7])."""

@@ -119,3 +119,21 @@ def test_predict_batch_matches_pipeline(fusion, dev):
     s, t_, i = [[a.cpu().numpy() for a in out[m]] for m in ('speech', 'text', 'image')]
     ref = o_f.forward(syn.weights('fusion'), s[0], t_[0], i[0], s[2], t_[2], i[2])
     assert np.abs(fp - ref[1]).max() < 1e-5
+
+
+def test_speech_predict_from_file_runs_gpu_features(fusion, monkeypatch):
+    """SpeechInference.predict(path): load_audio (the reference's preprocessing/, stubbed here:
+    librosa is absent) -> GPU features (csrc/audio.hip) -> GPU DNN, against the oracle chain
+    (preprocess_audio restated -> DNN restated); inference/speech_inference.py:60-77."""
+    import types
+    from inference import speech_inference as si
+    from oracle import audio as oa
+    wave = oa.synthetic_clips(2, seed=44)
+    stub = types.SimpleNamespace(load_audio=lambda path, sr=oa.SR, duration=oa.DURATION: (wave[int(path)], oa.SR))
+    monkeypatch.setattr(si, '_preprocessing', lambda: stub)
+    ref_feat, _ = oa.features_batch(wave)
+    _, _, rp = o_s.forward(syn.weights('speech'), ref_feat)
+    for i in range(2):
+        _check_dict(fusion.speech_inference.predict(str(i)), rp[i], 1e-4)
+        f64, p7 = fusion.speech_inference.extract_features(str(i))
+        assert f64.shape == (64,) and np.abs(p7 - rp[i]).max() < 1e-4
