@@ -297,6 +297,10 @@ int set_option(Options& o, const std::string& k, int value) {
     o.conv3x3_debug = value;
     return 0;
   }
+  if (k == "audio_debug" && (value == 0 || (probe && (value == 1 || value == 2 || value == 4 || value == 8 || value == 15)))) {
+    o.audio_debug = value;
+    return 0;
+  }
   auto tile_ok = [](int id) {
     const int v = id % 10000;
     const bool deep = id == 20256 || id == 30256 || id == 20128 || id == 40256 || id == 41256 || id == 50128 ||

@@ -40,6 +40,9 @@ constexpr double kPi = 3.14159265358979323846;
 constexpr int A_NFFT = 2048, A_HOP = 512, A_NBIN = 1025, A_NMEL = 128, A_NCHROMA = 12, A_NTUNE = 100;
 constexpr int A_CMAX = 184;  // peaks per frame: local maxima of 358 band bins are <= 179
 constexpr int A_BAND_LO = 1, A_BAND_HI = 1024;  // bins that may hold a peak (mask applied too)
+constexpr int A_TMAX = 4096;   // frames per clip (95 s at 22050 Hz)
+constexpr int A_NLDS = 24576;  // peak magnitudes kept in LDS for the median (more: read from HBM)
+constexpr int A_MSEG = 1024;   // mel segments (band x thread-chunk runs)
 }  // namespace
 
 struct AudioTables {
@@ -47,9 +50,11 @@ struct AudioTables {
   const double2* tw;      // [512] exp(-2 pi i j / 1024)
   const double2* post;    // [1025] exp(-2 pi i k / 2048)
   const double* freq;     // [1025] fft_frequencies
-  const int* mel_off;     // [129] CSR row offsets into mel_bin / mel_w
-  const int* mel_bin;     // nonzero bins
-  const float* mel_w;     // float32 weights (librosa's float32 filterbank)
+  const int* mel_bin;     // nonzero bins of the mel triangles, band-major
+  const float* mel_w;     // their float32 weights (librosa's float32 filterbank)
+  const int* mel_seg;     // per nonzero: segment = run of one band inside one thread's chunk
+  const int* mel_segoff;  // [129] first segment of each band
+  int mel_nnz, mel_ch;    // nonzeros, nonzeros per thread (mel_ch * 256 >= mel_nnz)
   const double* dct;      // [n_mfcc][128] DCT-II ortho
   const float* chroma;    // [100][12][1025] float32 filterbanks, one per tuning bin
   int lo_bin, hi_bin;     // piptrack freq mask [lo, hi): 150 <= f < 4000
@@ -74,22 +79,30 @@ __device__ __forceinline__ T block_reduce_sum(T v, T* red) {
 // Exact-rounding helpers: librosa's float32 expressions evaluated without FMA contraction.
 #pragma clang fp contract(off)
 
+// DBG (probe builds only, option "audio_debug"; wrong results): bit 1 skips the FFT stages,
+// 2 the rolloff cumsum, 4 the mel sums and the peak search, 8 the spectrum split
+template <int DBG = 0>
 __global__ __launch_bounds__(256) void audio_frame_kernel(const float* __restrict__ wave, int L, int T,
                                                           AudioTables tb, float* __restrict__ pow_out,
                                                           float* __restrict__ meldb_out, double* __restrict__ scal,
                                                           float2* __restrict__ cand, int* __restrict__ ccount) {
   __shared__ double2 z[1024];
-  __shared__ float smag[A_NBIN + 3], spow[A_NBIN + 3];
+  __shared__ double2 stw[512];  // FFT twiddles, loaded once per workgroup
+  __shared__ __attribute__((aligned(16))) float smag[A_NBIN + 3];
+  __shared__ __attribute__((aligned(16))) float spow[A_NBIN + 3];
   __shared__ double redd[4];
   __shared__ float redf[4];
   __shared__ int redi[4];
   __shared__ int sb_last[256];
   __shared__ int ncand;
+  __shared__ float mpart[A_MSEG];
   const int tid = threadIdx.x;
   const int t = blockIdx.x, b = blockIdx.y;
   const float* y = wave + (size_t)b * L;
   const size_t fr = (size_t)b * T + t;
 
+  stw[tid] = tb.tw[tid];
+  stw[tid + 256] = tb.tw[tid + 256];
   // ---- samples n = 8 tid .. 8 tid + 7 of frame t (padded offset t * hop)
   float vz[8], ve[8];
 #pragma unroll
@@ -130,14 +143,14 @@ __global__ __launch_bounds__(256) void audio_frame_kernel(const float* __restric
   }
   __syncthreads();
   // radix-2 DIT, 10 stages, 512 butterflies per stage (2 per thread)
-  for (int s = 0; s < 10; ++s) {
+  for (int s = 0; s < ((DBG & 1) ? 0 : 10); ++s) {
     const int half = 1 << s;
 #pragma unroll
     for (int r = 0; r < 2; ++r) {
       const int i = tid + 256 * r;
       const int j = i & (half - 1);
       const int i0 = ((i >> s) << (s + 1)) + j, i1 = i0 + half;
-      const double2 w = tb.tw[j << (9 - s)];
+      const double2 w = stw[j << (9 - s)];
       const double2 a = z[i0], c = z[i1];
       const double2 tt = make_double2(w.x * c.x - w.y * c.y, w.x * c.y + w.y * c.x);
       z[i0] = make_double2(a.x + tt.x, a.y + tt.y);
@@ -146,7 +159,7 @@ __global__ __launch_bounds__(256) void audio_frame_kernel(const float* __restric
     __syncthreads();
   }
   // ---- split into the 2048-point real spectrum, complex64 -> |X| (hypotf) and |X|^2 (float32)
-  for (int k = tid; k < A_NBIN; k += 256) {
+  for (int k = tid; k < ((DBG & 8) ? 0 : A_NBIN); k += 256) {
     const double2 zk = z[k & 1023], zn = z[(1024 - k) & 1023];
     const double er = 0.5 * (zk.x + zn.x), ei = 0.5 * (zk.y - zn.y);   // E = (Z[k] + conj Z[N-k]) / 2
     const double orr = 0.5 * (zk.y + zn.y), oi = -0.5 * (zk.x - zn.x);  // O = (Z[k] - conj Z[N-k]) / 2i
@@ -179,15 +192,35 @@ __global__ __launch_bounds__(256) void audio_frame_kernel(const float* __restric
   for (int k = tid; k < A_NBIN; k += 256) cen += tb.freq[k] * (double)(float)((double)smag[k] / length);
   const double centroid = block_reduce_sum<double>(cen, redd);
 
-  // ---- mel bands (sparse Slaney triangles), power_to_db before the clip-level top_db clamp
+  // ---- mel bands (sparse Slaney triangles): each thread sums its chunk of the band-major
+  // nonzeros into per-segment partials, then each band adds its segments in order (fixed
+  // summation order: deterministic); power_to_db before the clip-level top_db clamp
+  {
+    const int e0 = tid * tb.mel_ch, e1 = (DBG & 4) ? e0 : min(e0 + tb.mel_ch, tb.mel_nnz);
+    if (e0 < e1) {
+      float acc = 0.f;
+      int seg = tb.mel_seg[e0];
+      for (int e = e0; e < e1; ++e) {
+        const int sg = tb.mel_seg[e];
+        if (sg != seg) {
+          mpart[seg] = acc;
+          acc = 0.f;
+          seg = sg;
+        }
+        acc += tb.mel_w[e] * spow[tb.mel_bin[e]];
+      }
+      mpart[seg] = acc;
+    }
+  }
+  __syncthreads();
   if (tid < A_NMEL) {
     float acc = 0.f;
-    for (int e = tb.mel_off[tid]; e < tb.mel_off[tid + 1]; ++e) acc += tb.mel_w[e] * spow[tb.mel_bin[e]];
+    for (int g = tb.mel_segoff[tid]; g < tb.mel_segoff[tid + 1]; ++g) acc += mpart[g];
     meldb_out[fr * A_NMEL + tid] = 10.0f * log10f(fmaxf(1e-10f, acc));
   }
   // ---- piptrack peaks in the band: S * (S > ref) local maxima, parabolic shift (float32)
   const float ref = 0.1f * fmax_pow;
-  for (int k = tb.lo_bin + tid; k < tb.hi_bin; k += 256) {
+  for (int k = tb.lo_bin + tid; k < ((DBG & 4) ? 0 : tb.hi_bin); k += 256) {
     const float s0 = spow[k - 1], s1 = spow[k], s2 = spow[k + 1];
     const float x0 = s0 > ref ? s0 : 0.f, x1 = s1 > ref ? s1 : 0.f, x2 = s2 > ref ? s2 : 0.f;
     if (x1 > x0 && x1 >= x2) {
@@ -202,12 +235,19 @@ __global__ __launch_bounds__(256) void audio_frame_kernel(const float* __restric
   }
   // ---- spectral rolloff: numpy's sequential float32 cumsum, one lane; first bin >= 0.85 total
   __syncthreads();
-  if (tid == 0) {
+  if (tid == 0 && !(DBG & 2)) {  // the power column is no longer needed: spow receives the cumsum
     float c = 0.f;
-    for (int k = 0; k < A_NBIN; ++k) {
-      c += smag[k];
-      spow[k] = c;  // the power column is no longer needed: reuse for the cumsum
+    for (int k4 = 0; k4 < A_NBIN / 4; ++k4) {
+      const float4 m = *reinterpret_cast<const float4*>(smag + 4 * k4);
+      float4 o;
+      c += m.x; o.x = c;
+      c += m.y; o.y = c;
+      c += m.z; o.z = c;
+      c += m.w; o.w = c;
+      *reinterpret_cast<float4*>(spow + 4 * k4) = o;
     }
+    c += smag[A_NBIN - 1];
+    spow[A_NBIN - 1] = c;
   }
   __syncthreads();
   const float thr = 0.85f * spow[A_NBIN - 1];
@@ -238,25 +278,36 @@ __device__ __forceinline__ float fkey_inv(unsigned k) {
   return __uint_as_float((k & 0x80000000u) ? (k & 0x7fffffffu) : ~k);
 }
 
-// rank-r smallest key among the clip's peaks (radix select, 4 passes of 8 bits)
-__device__ unsigned radix_select(const float2* cand, const int* cnt, int T, unsigned r, int* hist, unsigned* sh) {
+// rank-r smallest of the clip's n peak magnitudes (radix select on order-preserving keys, 4
+// passes of 8 bits). The magnitudes come from LDS (smag) when the clip's peaks fit there,
+// else straight from the per-frame peak lists (soff = per-frame prefix offsets).
+__device__ unsigned radix_select(const float* smag, int n, const float2* cd, const int* soff, int T, unsigned r,
+                                 int* hist, unsigned* sh) {
   unsigned prefix = 0, pmask = 0;
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6, nw = blockDim.x >> 6;
   for (int pass = 0; pass < 4; ++pass) {
     const int shift = 24 - 8 * pass;
     for (int i = threadIdx.x; i < 256; i += blockDim.x) hist[i] = 0;
     __syncthreads();
-    for (int t = 0; t < T; ++t) {
-      const int n = cnt[t];
+    if (smag) {
       for (int i = threadIdx.x; i < n; i += blockDim.x) {
-        const unsigned k = fkey(cand[(size_t)t * A_CMAX + i].y);
+        const unsigned k = fkey(smag[i]);
         if ((k & pmask) == prefix) atomicAdd(&hist[(k >> shift) & 255], 1);
+      }
+    } else {
+      for (int t = wave; t < T; t += nw) {
+        const int cnt = soff[t + 1] - soff[t];
+        for (int i = lane; i < cnt; i += 64) {
+          const unsigned k = fkey(cd[(size_t)t * A_CMAX + i].y);
+          if ((k & pmask) == prefix) atomicAdd(&hist[(k >> shift) & 255], 1);
+        }
       }
     }
     __syncthreads();
     if (threadIdx.x == 0) {
       unsigned acc = 0;
       int d = 0;
-      for (; d < 256; ++d) {
+      for (; d < 255; ++d) {
         if (acc + (unsigned)hist[d] > r) break;
         acc += hist[d];
       }
@@ -277,8 +328,10 @@ __global__ __launch_bounds__(512) void audio_clip_kernel(const float* __restrict
                                                          const float2* __restrict__ cand, const int* __restrict__ ccount,
                                                          int T, AudioTables tb, float* __restrict__ feat, int F,
                                                          float* __restrict__ tuning_out) {
-  __shared__ double band[A_NMEL];
-  __shared__ double redd[8];
+  __shared__ float smag[A_NLDS];
+  __shared__ int soff[A_TMAX + 1];
+  __shared__ double band4[4][A_NMEL];
+  __shared__ double redd[8][4];
   __shared__ float redf[8];
   __shared__ int hist[256];
   __shared__ unsigned sh[2];
@@ -297,56 +350,57 @@ __global__ __launch_bounds__(512) void audio_clip_kernel(const float* __restrict
 #pragma unroll
   for (int o = 32; o > 0; o >>= 1) mx = fmaxf(mx, __shfl_xor(mx, o, 64));
   if (lane == 0) redf[wave] = mx;
-  __syncthreads();
-  if (tid == 0) {
-    float m = redf[0];
-    for (int i = 1; i < 8; ++i) m = fmaxf(m, redf[i]);
-    redf[0] = m - 80.0f;
+  if (tid == 0) {  // per-frame peak offsets (serial prefix, T <= A_TMAX)
+    int acc = 0;
+    for (int t = 0; t < T; ++t) {
+      soff[t] = acc;
+      acc += cnt[t];
+    }
+    soff[T] = acc;
   }
   __syncthreads();
-  const float floor_db = redf[0];
-  if (tid < A_NMEL) {
-    double s = 0.0;
-    for (int t = 0; t < T; ++t) s += (double)fmaxf(md[(size_t)t * A_NMEL + tid], floor_db);
-    band[tid] = s / (double)T;
+  float floor_db = redf[0];
+  for (int i = 1; i < 8; ++i) floor_db = fmaxf(floor_db, redf[i]);
+  floor_db -= 80.0f;
+  {
+    const int m = tid & (A_NMEL - 1), q = tid >> 7;
+    double sacc = 0.0;
+    for (int t = q; t < T; t += 4) sacc += (double)fmaxf(md[(size_t)t * A_NMEL + m], floor_db);
+    band4[q][m] = sacc;
   }
+  const int n = soff[T];
+  const bool in_lds = n <= A_NLDS;
+  if (in_lds)  // the peak magnitudes, compacted into LDS for the median
+    for (int t = wave; t < T; t += 8) {
+      const int o = soff[t], c = soff[t + 1] - o;
+      for (int i = lane; i < c; i += 64) smag[o + i] = cd[(size_t)t * A_CMAX + i].y;
+    }
   __syncthreads();
   if (tid < tb.n_mfcc) {
     double c = 0.0;
-    for (int m = 0; m < A_NMEL; ++m) c += tb.dct[tid * A_NMEL + m] * band[m];
+    for (int m = 0; m < A_NMEL; ++m)
+      c += tb.dct[tid * A_NMEL + m] * ((band4[0][m] + band4[1][m] + band4[2][m] + band4[3][m]) / (double)T);
     feat[(size_t)b * F + tid] = (float)c;
   }
 
   // ---- estimate_tuning: median peak magnitude, residual histogram, argmax
-  int n_local = 0;
-  for (int t = tid; t < T; t += 512) n_local += cnt[t];
-  int n = 0;
-  {
-    int v = n_local;
-#pragma unroll
-    for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o, 64);
-    __syncthreads();
-    if (lane == 0) hist[wave] = v;
-    __syncthreads();
-    for (int i = 0; i < 8; ++i) n += hist[i];
-    __syncthreads();
-  }
   float med = 0.f;
   if (n > 0) {
-    const unsigned k1 = radix_select(cd, cnt, T, (unsigned)((n - 1) / 2), hist, sh);
+    const float* sm = in_lds ? smag : nullptr;
+    const unsigned k1 = radix_select(sm, n, cd, soff, T, (unsigned)((n - 1) / 2), hist, sh);
     const float v1 = fkey_inv(k1);
     if (n & 1) {
       med = v1;
     } else {
-      const unsigned k2 = radix_select(cd, cnt, T, (unsigned)(n / 2), hist, sh);
+      const unsigned k2 = radix_select(sm, n, cd, soff, T, (unsigned)(n / 2), hist, sh);
       med = (v1 + fkey_inv(k2)) / 2.0f;
     }
   }
   for (int i = tid; i < A_NTUNE; i += 512) counts[i] = 0;
   __syncthreads();
-  for (int t = 0; t < T; ++t) {
-    const int nt = cnt[t];
-    for (int i = tid; i < nt; i += 512) {
+  for (int t = wave; t < T; t += 8) {
+    const int c = soff[t + 1] - soff[t];
+    for (int i = lane; i < c; i += 64) {
       const float2 pm = cd[(size_t)t * A_CMAX + i];
       if (!(pm.y >= med) || !(pm.x > 0.f)) continue;
       const float o = (float)log2((double)(pm.x / 27.5f));
@@ -405,17 +459,27 @@ __global__ __launch_bounds__(512) void audio_clip_kernel(const float* __restrict
   if (lane == 0)
 #pragma unroll
     for (int c = 0; c < A_NCHROMA; ++c) chroma_acc[wave][c] = cacc[c];
+  // ---- spectral means: zcr, centroid, rolloff, rms (frames over the block)
+  double sp[4] = {0.0, 0.0, 0.0, 0.0};
+  for (int t = tid; t < T; t += 512)
+#pragma unroll
+    for (int j = 0; j < 4; ++j) sp[j] += scal[((size_t)b * T + t) * 4 + j];
+#pragma unroll
+  for (int j = 0; j < 4; ++j)
+#pragma unroll
+    for (int o = 32; o > 0; o >>= 1) sp[j] += __shfl_xor(sp[j], o, 64);
+  if (lane == 0)
+#pragma unroll
+    for (int j = 0; j < 4; ++j) redd[wave][j] = sp[j];
   __syncthreads();
   if (tid < A_NCHROMA) {
     double s = 0.0;
     for (int w = 0; w < 8; ++w) s += chroma_acc[w][tid];
     feat[(size_t)b * F + tb.n_mfcc + tid] = (float)(s / (double)T);
-  }
-  // ---- spectral means: zcr, centroid, rolloff, rms
-  if (tid >= 64 && tid < 68) {
+  } else if (tid >= 64 && tid < 68) {
     const int j = tid - 64;
     double s = 0.0;
-    for (int t = 0; t < T; ++t) s += scal[((size_t)b * T + t) * 4 + j];
+    for (int w = 0; w < 8; ++w) s += redd[w][j];
     feat[(size_t)b * F + tb.n_mfcc + A_NCHROMA + j] = (float)(s / (double)T);
   }
 }
@@ -476,6 +540,28 @@ int AudioModel::create(const float* blob, size_t n) {
     }
     off[i + 1] = (int)bins.size();
   }
+  // mel segments: nonzeros split into 256 contiguous chunks (one per thread); a segment is a
+  // run of one band inside one chunk
+  const int nnz = (int)bins.size();
+  mel_nnz = nnz;
+  mel_ch = (nnz + 255) / 256;
+  std::vector<int> seg(nnz), segoff(A_NMEL + 1, 0);
+  {
+    int sgi = -1, prev_band = -1, prev_chunk = -1, band = 0;
+    for (int e = 0; e < nnz; ++e) {
+      while (e >= off[band + 1]) ++band;
+      const int chunk = e / mel_ch;
+      if (band != prev_band || chunk != prev_chunk) {
+        ++sgi;
+        for (int m = prev_band + 1; m <= band; ++m) segoff[m] = sgi;
+        prev_band = band;
+        prev_chunk = chunk;
+      }
+      seg[e] = sgi;
+    }
+    for (int m = prev_band + 1; m <= A_NMEL; ++m) segoff[m] = sgi + 1;
+    MEC_REQUIRE(sgi + 1 <= A_MSEG, "audio: too many mel segments");
+  }
   // DCT-II ortho [n_mfcc][128]
   std::vector<double> dct((size_t)n_mfcc * A_NMEL);
   for (int k = 0; k < n_mfcc; ++k)
@@ -529,10 +615,11 @@ int AudioModel::create(const float* blob, size_t n) {
   off_freq = off_post + A_NBIN * 16;
   off_dct = off_freq + A_NBIN * 8;
   off_chroma = off_dct + dct.size() * 8;
-  off_meloff = off_chroma + chroma.size() * 4;
-  off_melbin = off_meloff + off.size() * 4;
+  off_meloff = off_chroma + chroma.size() * 4;  // mel segment offsets [129]
+  off_melbin = off_meloff + segoff.size() * 4;
   off_melw = off_melbin + bins.size() * 4;
-  const size_t total = off_melw + wts.size() * 4;
+  off_melseg = off_melw + wts.size() * 4;
+  const size_t total = off_melseg + seg.size() * 4;
   std::vector<char> h(total);
   std::memcpy(h.data() + off_hann, hann.data(), hann.size() * 8);
   std::memcpy(h.data() + off_tw, tw.data(), tw.size() * 16);
@@ -540,7 +627,8 @@ int AudioModel::create(const float* blob, size_t n) {
   std::memcpy(h.data() + off_freq, freq.data(), freq.size() * 8);
   std::memcpy(h.data() + off_dct, dct.data(), dct.size() * 8);
   std::memcpy(h.data() + off_chroma, chroma.data(), chroma.size() * 4);
-  std::memcpy(h.data() + off_meloff, off.data(), off.size() * 4);
+  std::memcpy(h.data() + off_meloff, segoff.data(), segoff.size() * 4);
+  std::memcpy(h.data() + off_melseg, seg.data(), seg.size() * 4);
   std::memcpy(h.data() + off_melbin, bins.data(), bins.size() * 4);
   std::memcpy(h.data() + off_melw, wts.data(), wts.size() * 4);
   return upload(tables, h.data(), total);
@@ -550,7 +638,7 @@ int AudioModel::forward(const float* wave, int B, int L, float* feat, float* tun
   MEC_REQUIRE(B >= 0, "audio: B < 0");
   if (B == 0) return 0;
   MEC_REQUIRE(wave && feat, "audio: null pointer");
-  MEC_REQUIRE(L >= A_NFFT / 2 + 1 && L <= (1 << 26), "audio: n_samples out of range");
+  MEC_REQUIRE(L >= A_NFFT / 2 + 1 && L / A_HOP + 1 <= A_TMAX, "audio: n_samples out of range (1025 .. 2^21)");
   const int T = 1 + L / A_HOP;  // center=True frames
   const size_t fr = (size_t)B * T;
   const size_t need = fr * (A_NBIN * 4 + A_NMEL * 4 + 4 * 8 + A_CMAX * 8 + 4) + 1024;
@@ -569,14 +657,28 @@ int AudioModel::forward(const float* wave, int B, int L, float* feat, float* tun
   tb.freq = reinterpret_cast<const double*>(tb0 + off_freq);
   tb.dct = reinterpret_cast<const double*>(tb0 + off_dct);
   tb.chroma = reinterpret_cast<const float*>(tb0 + off_chroma);
-  tb.mel_off = reinterpret_cast<const int*>(tb0 + off_meloff);
+  tb.mel_segoff = reinterpret_cast<const int*>(tb0 + off_meloff);
+  tb.mel_seg = reinterpret_cast<const int*>(tb0 + off_melseg);
+  tb.mel_nnz = mel_nnz;
+  tb.mel_ch = mel_ch;
   tb.mel_bin = reinterpret_cast<const int*>(tb0 + off_melbin);
   tb.mel_w = reinterpret_cast<const float*>(tb0 + off_melw);
   tb.lo_bin = lo_bin;
   tb.hi_bin = hi_bin;
   tb.n_mfcc = n_mfcc;
   MEC_TRY(prof.begin(TAG_AUDIO, s));
-  hipLaunchKernelGGL(audio_frame_kernel, dim3(T, B), dim3(256), 0, s, wave, L, T, tb, pw, mdb, scal, cand, cc);
+#ifdef MEC_PROBES
+  switch (opt().audio_debug) {
+    case 1: hipLaunchKernelGGL(audio_frame_kernel<1>, dim3(T, B), dim3(256), 0, s, wave, L, T, tb, pw, mdb, scal, cand, cc); break;
+    case 2: hipLaunchKernelGGL(audio_frame_kernel<2>, dim3(T, B), dim3(256), 0, s, wave, L, T, tb, pw, mdb, scal, cand, cc); break;
+    case 4: hipLaunchKernelGGL(audio_frame_kernel<4>, dim3(T, B), dim3(256), 0, s, wave, L, T, tb, pw, mdb, scal, cand, cc); break;
+    case 8: hipLaunchKernelGGL(audio_frame_kernel<8>, dim3(T, B), dim3(256), 0, s, wave, L, T, tb, pw, mdb, scal, cand, cc); break;
+    case 15: hipLaunchKernelGGL(audio_frame_kernel<15>, dim3(T, B), dim3(256), 0, s, wave, L, T, tb, pw, mdb, scal, cand, cc); break;
+    default: hipLaunchKernelGGL(audio_frame_kernel<0>, dim3(T, B), dim3(256), 0, s, wave, L, T, tb, pw, mdb, scal, cand, cc);
+  }
+#else
+  hipLaunchKernelGGL(audio_frame_kernel<0>, dim3(T, B), dim3(256), 0, s, wave, L, T, tb, pw, mdb, scal, cand, cc);
+#endif
   MEC_LAUNCH_CHECK();
   hipLaunchKernelGGL(audio_clip_kernel, dim3(B), dim3(512), 0, s, pw, mdb, scal, cand, cc, T, tb, feat,
                      n_mfcc + A_NCHROMA + 4, tuning);

@@ -37,10 +37,10 @@ struct SpeechModel : Model {
 // blob = [sample_rate, n_fft, hop, n_mels, n_mfcc] (config.py:57-59 + librosa defaults); the
 // handle owns the filterbank / window / twiddle tables and a grow-only workspace.
 struct AudioModel : Model {
-  int sr = 22050, n_mfcc = 40, lo_bin = 0, hi_bin = 0;
+  int sr = 22050, n_mfcc = 40, lo_bin = 0, hi_bin = 0, mel_nnz = 0, mel_ch = 0;
   DevBuf tables, ws;
   size_t off_hann = 0, off_tw = 0, off_post = 0, off_freq = 0, off_dct = 0, off_chroma = 0, off_meloff = 0,
-         off_melbin = 0, off_melw = 0;
+         off_melbin = 0, off_melw = 0, off_melseg = 0;
   int create(const float* blob, size_t n);
   // wave f32 [B, L] -> feat f32 [B, n_mfcc + 16]; tuning f32 [B] (estimate_tuning) or null
   int forward(const float* wave, int B, int L, float* feat, float* tuning, hipStream_t s);

@@ -103,3 +103,12 @@ def test_waveform_to_speech_prediction(fx, dev):
     print(f'speech from waveform: probs max|d| {np.abs(probs - ref_probs).max():.3g}')
     assert (probs.argmax(1) == ref_probs.argmax(1)).all()
     assert np.abs(probs - ref_probs).max() <= 1e-4
+
+
+def test_audio_long_clip_median_from_hbm(fx, dev):
+    """A 30 s clip: more peaks than the clip kernel keeps in LDS (24576), so the median's
+    radix select reads the per-frame peak lists from HBM."""
+    wave = oa.synthetic_clips(1, seed=9, n=30 * oa.SR, kind='noise')
+    got, gt = _run(fx, dev, wave)
+    ref, rt = oa.features_batch(wave)
+    _compare('30 s noise', got, gt, ref, rt)

@@ -22,7 +22,7 @@ from mec import engine, synthetic as syn  # noqa: E402
 
 def main():
     ap = argparse.ArgumentParser()
-    ap.add_argument('--enc', choices=['text', 'image', 'image_mbv2', 'speech', 'fusion', 'pipeline'], required=True)
+    ap.add_argument('--enc', choices=['text', 'image', 'image_mbv2', 'speech', 'fusion', 'pipeline', 'audio'], required=True)
     ap.add_argument('--iters', type=int, default=5)
     ap.add_argument('--batch', type=int, default=256)
     ap.add_argument('--opt', action='append', default=[], help='library option NAME=VALUE (mec_set_option)')
@@ -52,6 +52,11 @@ def main():
         m = engine.SpeechEncoder(device=dev)
         x = engine.to_device(syn.speech_inputs(B, seed=0), dev)
         fn = lambda: m.forward(x)  # noqa: E731
+    elif a.enc == 'audio':  # waveform -> 56-d features (csrc/audio.hip), 3 s clips at 22050 Hz
+        import numpy as np
+        m = engine.AudioFeaturizer(device=dev)
+        wv = torch.from_numpy(np.random.default_rng(0).standard_normal((B, 66150)).astype(np.float32)).to(dev)
+        fn = lambda: m.forward(wv)  # noqa: E731
     elif a.enc == 'fusion':
         m = engine.FusionHead(device=dev)
         args = [torch.rand(B, d, device=dev) for d in (64, 768, 512)]
