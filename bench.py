@@ -63,10 +63,11 @@ def tile_name(tile: int, M: int) -> str:
 
 def tile_name_f32(tile: int, M: int) -> str:
     """Kernel + grid for an fp32 GEMM tile id (gemm_f32.hip, launch_tile)."""
-    bm, bn = {1: (256, 128), 2: (128, 128), 3: (128, 64), 4: (256, 256)}.get(tile, (0, 0))
-    if not bm:
+    bm, bn = {1: (256, 128), 2: (128, 128), 3: (128, 64), 4: (256, 256)}.get((tile - 1) % 4 + 1, (0, 0))
+    if not bm or not 1 <= tile <= 8:
         return f'gemm_f32 tile {tile}'
-    return f'gemm_f32_kernel<{bm}x{bn}x32, mfma_f32_32x32x2f32> grid={((M + bm - 1) // bm) * (3072 // bn)}'
+    mf = 'mfma_f32_32x32x2f32' if tile <= 4 else 'mfma_f32_16x16x4f32'
+    return f'gemm_f32_kernel<{bm}x{bn}x32, {mf}> grid={((M + bm - 1) // bm) * (3072 // bn)}'
 
 
 def parse():

@@ -138,7 +138,7 @@ int mec_conv_f32(const float* x, const float* w, const float* bias, const float*
  *   "gemm_impl" 1|[2]      register-staged / glds GEMM engine
  *   "gemm_bn" [0]|id       force one f16 GEMM tile (0 = autotune), "gemm_autotune" 0|[1]
  *   "gemm_bn_tag" tag*100000+id   force a tile for one launch class (e.g. 3 = BERT O-proj)
- *   "gemm_f32_tile" [0]|1..4  force one fp32 GEMM tile (0 = autotune)
+ *   "gemm_f32_tile" [0]|1..8  force one fp32 GEMM tile (0 = autotune; 5..8 = 1..4 on 16x16x4)
  *   "gemm_prefetch_r" 0|[1]  f16 residual prefetch in short-K GEMMs
  *   "conv3x3_direct" 0|[1] layer1 3x3 conv on the halo-tile kernel (mec_conv_f16 too)
  *   "pw_chain" 0|1|[2]     layer1 seam kernels (1: the 256->64 seams, 2: also 256->128)
@@ -163,7 +163,8 @@ int mec_build_flags(void);
 
 /* Tile width the autotuner chose for a plain (amode 0) or conv (amode 1) GEMM shape; 0 = not yet seen. */
 int mec_gemm_query(int amode, int M, int N, int K);
-/* The same for the fp32 engine: tile id 1 = 256x128 (8 waves), 2 = 128x128, 3 = 128x64, 4 = 256x256.
+/* The same for the fp32 engine: tile id 1 = 256x128 (8 waves), 2 = 128x128, 3 = 128x64, 4 = 256x256
+ * on v_mfma_f32_32x32x2_f32; 5..8 the same tiles on v_mfma_f32_16x16x4_f32.
  * Both query the process-default cache of the handle-less entry points (mec_gemm_f16/f32). */
 int mec_gemm_f32_query(int amode, int M, int N, int K);
 /* The tile a handle's own autotuner chose for a shape it ran (its precision's engine); 0 = not seen. */

@@ -38,13 +38,19 @@ __device__ __forceinline__ void f32_dma(const void* src, uint32_t lds) {
   asm volatile("s_mov_b32 m0, %1\n\ts_nop 0\n\tglobal_load_lds_dwordx4 %0, off" ::"v"(src), "s"(lds) : "memory", "m0");
 }
 
-template <int BM, int BN, int WM, int WN, int NS, int AM>
+// MF 32: v_mfma_f32_32x32x2_f32 (64 cycles, 16 accumulators); MF 16: v_mfma_f32_16x16x4_f32
+// (32 cycles, 4 accumulators; lane (r = l&15, q = l>>4) reads chunk 4s + q and supplies
+// k = 16s + 4q + j to step (s, j): the f16 engine's 16x16x32 read pattern). Same products,
+// same k set per output; the two shapes differ only in summation order.
+template <int BM, int BN, int WM, int WN, int NS, int AM, int MF = 32>
 __global__ __launch_bounds__(64 * WM * WN, (WM * WN == 4) ? 2 : 1) void gemm_f32_kernel(const GemmParams p) {
   constexpr int BK = 32;                    // floats per K tile (128-B LDS rows)
   constexpr int RPI = 8;                    // rows per glds wave-instruction (1 KB)
   constexpr int NW = WM * WN;
   constexpr int TM = BM / WM, TN = BN / WN;
-  constexpr int TI = TM / 32, TJ = TN / 32;
+  constexpr int TI = TM / MF, TJ = TN / MF;
+  typedef float accv __attribute__((ext_vector_type(MF == 32 ? 16 : 4)));
+  constexpr int NACC = MF == 32 ? 16 : 4;
   constexpr int AI = BM / RPI / NW, BI = BN / RPI / NW;
   static_assert(AI >= 1 && BI >= 1 && TI >= 1 && TJ >= 1, "tile");
   constexpr int LPT = AI + BI;
@@ -130,13 +136,13 @@ __global__ __launch_bounds__(64 * WM * WN, (WM * WN == 4) ? 2 : 1) void gemm_f32
       f32_dma(b_src[j] + k0, sB + (uint32_t)((wave * BI + j) * RPI * BK) * 4u);
   };
 
-  floatx16 acc[TI][TJ];
+  accv acc[TI][TJ];
 #pragma unroll
   for (int i = 0; i < TI; ++i)
 #pragma unroll
     for (int j = 0; j < TJ; ++j)
 #pragma unroll
-      for (int e = 0; e < 16; ++e) acc[i][j][e] = 0.f;
+      for (int e = 0; e < NACC; ++e) acc[i][j][e] = 0.f;
 
   const int nk = K / BK;
 #pragma unroll
@@ -162,49 +168,76 @@ __global__ __launch_bounds__(64 * WM * WN, (WM * WN == 4) ? 2 : 1) void gemm_f32
     if (t + NS - 1 < nk) issue((t + NS - 1) % NS, t + NS - 1);
     const float* sA = smem + (t % NS) * STAGE;
     const float* sB = sA + BM * BK;
+    if constexpr (MF == 32) {
 #pragma unroll
-    for (int s = 0; s < BK / 8; ++s) {
-      const int kcs = 2 * s + lh;
-      float4 af[TI], bf[TJ];
+      for (int s = 0; s < BK / 8; ++s) {
+        const int kcs = 2 * s + lh;
+        float4 af[TI], bf[TJ];
 #pragma unroll
-      for (int i = 0; i < TI; ++i) {
-        const int r = wm * TM + i * 32 + lr;
-        af[i] = *reinterpret_cast<const float4*>(sA + r * BK + sw<64>(r, kcs) * 4);
+        for (int i = 0; i < TI; ++i) {
+          const int r = wm * TM + i * 32 + lr;
+          af[i] = *reinterpret_cast<const float4*>(sA + r * BK + sw<64>(r, kcs) * 4);
+        }
+#pragma unroll
+        for (int j = 0; j < TJ; ++j) {
+          const int r = wn * TN + j * 32 + lr;
+          bf[j] = *reinterpret_cast<const float4*>(sB + r * BK + sw<64>(r, kcs) * 4);
+        }
+#pragma unroll
+        for (int q = 0; q < 4; ++q)
+#pragma unroll
+          for (int i = 0; i < TI; ++i)
+#pragma unroll
+            for (int j = 0; j < TJ; ++j)
+              acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x2f32(af[i][q], bf[j][q], acc[i][j], 0, 0, 0);
       }
+    } else {
+      const int l16 = lane & 15, lq = lane >> 4;
 #pragma unroll
-      for (int j = 0; j < TJ; ++j) {
-        const int r = wn * TN + j * 32 + lr;
-        bf[j] = *reinterpret_cast<const float4*>(sB + r * BK + sw<64>(r, kcs) * 4);
+      for (int s = 0; s < BK / 16; ++s) {
+        const int kcs = 4 * s + lq;
+        float4 af[TI], bf[TJ];
+#pragma unroll
+        for (int i = 0; i < TI; ++i) {
+          const int r = wm * TM + i * 16 + l16;
+          af[i] = *reinterpret_cast<const float4*>(sA + r * BK + sw<64>(r, kcs) * 4);
+        }
+#pragma unroll
+        for (int j = 0; j < TJ; ++j) {
+          const int r = wn * TN + j * 16 + l16;
+          bf[j] = *reinterpret_cast<const float4*>(sB + r * BK + sw<64>(r, kcs) * 4);
+        }
+#pragma unroll
+        for (int q = 0; q < 4; ++q)
+#pragma unroll
+          for (int i = 0; i < TI; ++i)
+#pragma unroll
+            for (int j = 0; j < TJ; ++j)
+              acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x4f32(af[i][q], bf[j][q], acc[i][j], 0, 0, 0);
       }
-#pragma unroll
-      for (int q = 0; q < 4; ++q)
-#pragma unroll
-        for (int i = 0; i < TI; ++i)
-#pragma unroll
-          for (int j = 0; j < TJ; ++j)
-            acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x2f32(af[i][q], bf[j][q], acc[i][j], 0, 0, 0);
     }
   }
   asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)" ::: "memory");
   __builtin_amdgcn_s_barrier();
   asm volatile("" ::: "memory");
-  gemm_epilogue<BM, BN, WM, WN, 32>(p, acc, reinterpret_cast<f16*>(smem), m0, n0, wm, wn, wave, lane);
+  gemm_epilogue<BM, BN, WM, WN, MF>(p, acc, reinterpret_cast<f16*>(smem), m0, n0, wm, wn, wave, lane);
 }
 
 // Tiles (id): 1 = 256 x 128 on 8 waves (2 stages, 96 KB), 2 = 128 x 128 on 4 waves (2 stages,
 // 64 KB: two blocks per CU), 3 = 128 x 64 on 4 waves (3 stages), 4 = 256 x 256 on 8 waves
-// (wave tile 128 x 64, 2 stages, 128 KB). Every tile accumulates each output along the same
-// k order, so the choice changes speed only.
-static int tile_n(int id) { return id == 3 ? 64 : (id == 4 ? 256 : 128); }
+// (wave tile 128 x 64, 2 stages, 128 KB), all on the 32x32x2 MFMA; 5..8 = the same tiles on
+// the 16x16x4 MFMA. Tiles of one MFMA shape accumulate each output along the same k order
+// (bit-identical); the two shapes sum in different orders (rounding-level difference).
+static int tile_n(int id) { const int b = (id - 1) % 4 + 1; return b == 3 ? 64 : (b == 4 ? 256 : 128); }
 
-template <int BM, int BN, int WM, int WN, int NS>
+template <int BM, int BN, int WM, int WN, int NS, int MF = 32>
 static int launch_f32(const GemmParams& p, hipStream_t s) {
   const int nwg = ((p.M + BM - 1) / BM) * (p.N / BN);
   const dim3 blk(64 * WM * WN);
   if (p.amode == A_PLAIN)
-    hipLaunchKernelGGL((gemm_f32_kernel<BM, BN, WM, WN, NS, A_PLAIN>), dim3(nwg), blk, 0, s, p);
+    hipLaunchKernelGGL((gemm_f32_kernel<BM, BN, WM, WN, NS, A_PLAIN, MF>), dim3(nwg), blk, 0, s, p);
   else
-    hipLaunchKernelGGL((gemm_f32_kernel<BM, BN, WM, WN, NS, A_CONV>), dim3(nwg), blk, 0, s, p);
+    hipLaunchKernelGGL((gemm_f32_kernel<BM, BN, WM, WN, NS, A_CONV, MF>), dim3(nwg), blk, 0, s, p);
   MEC_LAUNCH_CHECK();
   return 0;
 }
@@ -215,6 +248,10 @@ static int launch_tile(const GemmParams& p, hipStream_t s, int id) {
     case 2: return launch_f32<128, 128, 2, 2, 2>(p, s);
     case 3: return launch_f32<128, 64, 2, 2, 3>(p, s);
     case 4: return launch_f32<256, 256, 2, 4, 2>(p, s);
+    case 5: return launch_f32<256, 128, 4, 2, 2, 16>(p, s);
+    case 6: return launch_f32<128, 128, 2, 2, 2, 16>(p, s);
+    case 7: return launch_f32<128, 64, 2, 2, 3, 16>(p, s);
+    case 8: return launch_f32<256, 256, 2, 4, 2, 16>(p, s);
     default: set_error("gemm_f32: unsupported tile id"); return -1;
   }
 }
@@ -238,7 +275,7 @@ static int tune_tile(const GemmParams& p, hipStream_t s, int* out) {
   for (auto& e : ev) MEC_HIP(hipEventCreate(&e));
   float best = 1e30f;
   int best_id = heuristic_tile(p);
-  for (int id = 1; id <= 4; ++id) {
+  for (int id = 1; id <= 8; ++id) {
     if (p.N % tile_n(id)) continue;
     MEC_TRY(launch_tile(p, s, id));
     MEC_HIP(hipEventRecord(ev[0], s));
@@ -275,7 +312,7 @@ int launch_gemm_f32(const GemmParams& p, hipStream_t s, Prof* prof, int tag) {
   const auto key = f32_key(p);
   int id = opt().gemm_f32_tile;
   if (id) {
-    MEC_REQUIRE(id >= 1 && id <= 4 && p.N % tile_n(id) == 0, "gemm_f32: forced tile does not fit N");
+    MEC_REQUIRE(id >= 1 && id <= 8 && p.N % tile_n(id) == 0, "gemm_f32: forced tile does not fit N");
   } else {
     id = tune_cache().find(key);
   }

@@ -100,7 +100,7 @@ def test_option_validation_without_gpu():
           (b'gemm_bn', 40256), (b'gemm_bn', 0),
           (b'gemm_bn_tag', 3 * 100000 + 40256), (b'gemm_bn_tag', 3 * 100000 + 11128),
           (b'gemm_debug', 0), (b'gemm_f32_tile', 3), (b'gemm_f32_tile', 0), (b'bert_oproj_ln', 3)]
-    bad = [(b'gemm_f32_tile', 5), (b'fusion_r', 3), (b'fusion_split', 2), (b'bert_qkv_attn', 4), (b'bert_oproj_ln', 5), (b'gemm_bn', 12345),
+    bad = [(b'gemm_f32_tile', 9), (b'fusion_r', 3), (b'fusion_split', 2), (b'bert_qkv_attn', 4), (b'bert_oproj_ln', 5), (b'gemm_bn', 12345),
            (b'gemm_bn', 42256), (b'gemm_bn_tag', 11128), (b'gemm_bn_tag', 15 * 100000 + 256),
            (b'gemm_bn_tag', 3 * 100000 + 999), (b'gemm_bn_tag', -1), (b'gemm_debug', 5)]
     try:
