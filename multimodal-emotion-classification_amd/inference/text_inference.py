@@ -101,6 +101,9 @@ class TextInference:
     def _forward(self, ids: np.ndarray, mask: np.ndarray):
         ids = np.asarray(ids, np.int32).reshape(1, -1)
         mask = np.asarray(mask, np.int32).reshape(1, -1)
+        if ids.size and (ids.min() < 0 or ids.max() >= engine.TextEncoder.VOCAB):
+            # the reference's nn.Embedding raises IndexError for such ids
+            raise ValueError(f'token id out of range [0, {engine.TextEncoder.VOCAB})')
         cls, logits, probs = self.model.forward(engine.to_device(ids, self.device), engine.to_device(mask, self.device))
         return cls.cpu().numpy()[0], probs.cpu().numpy()[0]
 
@@ -152,4 +155,4 @@ class TextInference:
         """ids/mask: device int32 [B,128] -> (cls [B,768], logits [B,7], probs [B,7])."""
         if self.model is None:
             raise RuntimeError('text model not loaded')
-        return self.model.forward(ids, mask)
+        return self.model.forward(ids, mask, check_ids=True)

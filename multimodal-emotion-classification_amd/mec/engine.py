@@ -126,8 +126,14 @@ class SpeechEncoder(HipModel):
 class TextEncoder(HipModel):
     kind = 'text'
 
-    def forward(self, ids: torch.Tensor, mask: torch.Tensor):
-        """ids/mask int32 [B,128] -> (cls [B,768], logits [B,7], probs [B,7])."""
+    VOCAB = 30522  # bert-base-uncased word embeddings
+
+    def forward(self, ids: torch.Tensor, mask: torch.Tensor, check_ids: bool = False):
+        """ids/mask int32 [B,128] -> (cls [B,768], logits [B,7], probs [B,7]).
+
+        check_ids: raise ValueError for ids outside [0, 30522) like nn.Embedding does (one
+        device min/max reduction and a host sync; the batched hot path skips it, and the kernel
+        then clamps out-of-range ids)."""
         if ids.dim() != 2:
             raise ValueError('ids: expected [B, L]')
         B, L = ids.shape
@@ -135,6 +141,10 @@ class TextEncoder(HipModel):
             raise ValueError('ids: L must be 128 (padding=max_length, Config.MAX_TEXT_LENGTH)')
         _check_tensor('ids', ids, torch.int32, (B, L), self.device)
         _check_tensor('mask', mask, torch.int32, (B, L), self.device)
+        if check_ids and B:
+            lo, hi = (int(v) for v in torch.aminmax(ids))
+            if lo < 0 or hi >= self.VOCAB:
+                raise ValueError(f'ids: token id out of range [0, {self.VOCAB}): min {lo}, max {hi}')
         cls, logits, probs = self._empty(B, 768), self._empty(B, 7), self._empty(B, 7)
         with self._lock:
             _lib.check(self.lib.mec_text_fwd(self.handle, _ptr(ids), _ptr(mask), B, L, _ptr(cls), _ptr(logits),

@@ -137,3 +137,18 @@ def test_speech_predict_from_file_runs_gpu_features(fusion, monkeypatch):
         _check_dict(fusion.speech_inference.predict(str(i)), rp[i], 1e-4)
         f64, p7 = fusion.speech_inference.extract_features(str(i))
         assert f64.shape == (64,) and np.abs(p7 - rp[i]).max() < 1e-4
+
+
+def test_text_out_of_range_ids_raise(fusion, dev):
+    """nn.Embedding raises for ids outside the vocabulary; so do the drop-in's id entry points
+    (the batched hot path skips the check and the kernel clamps)."""
+    import torch
+    ids, mask = syn.text_inputs(1, 128, seed=3)
+    bad = ids.copy()
+    bad[0, 5] = 30522
+    with pytest.raises(ValueError):
+        fusion.text_inference.predict_ids(bad[0], mask[0])
+    neg = ids.copy()
+    neg[0, 7] = -1
+    with pytest.raises(ValueError):
+        fusion.text_inference.predict_batch(torch.from_numpy(neg).to(dev), torch.from_numpy(mask).to(dev))
