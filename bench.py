@@ -173,7 +173,7 @@ def parity(out, x, ids, mask, gray, rows):
 
 def per_config(pipe, dev, precision, iters=10):
     """Single-encoder throughput on the other BASELINE configs (rank 0, N=1; informational,
-    not `value`): speech B=32, image B=256 (ResNet50 and, f16 only, the MobileNetV2 backbone),
+    not `value`): speech B=32, image B=256 (ResNet50 and the MobileNetV2 backbone),
     text B=128 (L=128). hipEvents around `iters` back-to-back calls, inputs in HBM."""
     from mec import engine, synthetic as syn
     xs = engine.to_device(syn.speech_inputs(32, seed=7), dev)
@@ -189,10 +189,8 @@ def per_config(pipe, dev, precision, iters=10):
     af = engine.AudioFeaturizer(device=dev)
     wv = torch.from_numpy(np.random.default_rng(7).standard_normal((32, 66150)).astype(np.float32)).to(dev)
     runs['speech_waveform_b32'] = (32, lambda: pipe.speech.forward(af.forward(wv)))
-    mb = None
-    if precision == 'f16':
-        mb = engine.MobileNetImageEncoder(device=dev)
-        runs['image_mobilenet_v2_b256'] = (256, lambda: mb.forward(g))
+    mb = engine.MobileNetImageEncoder(device=dev, precision=precision)
+    runs['image_mobilenet_v2_b256'] = (256, lambda: mb.forward(g))
     out = {}
     for name, (b, fn) in runs.items():
         for _ in range(3):
@@ -206,8 +204,7 @@ def per_config(pipe, dev, precision, iters=10):
         torch.cuda.synchronize()
         ms = e0.elapsed_time(e1) / iters
         out[name] = {'samples_per_s': b / ms * 1e3, 'ms_per_batch': ms}
-    if mb is not None:
-        mb.close()
+    mb.close()
     af.close()
     return out
 

@@ -51,8 +51,8 @@ int mec_create(int kind, const float* host_blob, size_t n, int device, mec_model
  * image backbones on f16 MFMA operands with fp32 accumulation, LayerNorm, softmax, GELU,
  * residual stream and heads. MEC_PREC_FP32: every operand and product in fp32
  * (v_mfma_f32_32x32x2_f32, an exact fmaf chain), the precision the reference computes in
- * (inference/text_inference.py:91-93, inference/image_inference.py:116-118); not available
- * for MEC_IMAGE_MBV2. Speech and fusion handles are fp32 at either setting. */
+ * (inference/text_inference.py:91-93, inference/image_inference.py:116-118). Speech, fusion
+ * and audio handles are fp32 at either setting. */
 enum { MEC_PREC_F16 = 0, MEC_PREC_FP32 = 1 };
 int mec_create_ex(int kind, const float* host_blob, size_t n, int device, int precision, mec_model** out);
 /* The handle's precision (MEC_PREC_*), -1 on a null handle. */

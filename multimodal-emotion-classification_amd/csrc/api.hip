@@ -127,10 +127,6 @@ int mec_create_ex(int kind, const float* host_blob, size_t n, int device, int pr
       set_error("mec_create: precision must be MEC_PREC_F16 or MEC_PREC_FP32");
       return -1;
     }
-    if (precision == MEC_PREC_FP32 && kind == KIND_IMAGE_MBV2) {
-      set_error("mec_create: MEC_PREC_FP32 is not implemented for the MobileNetV2 backbone");
-      return -1;
-    }
     *out = nullptr;
     const size_t want = blob_floats(kind);
     if (!want) { set_error("mec_create: unknown kind"); return -1; }
@@ -147,7 +143,7 @@ int mec_create_ex(int kind, const float* host_blob, size_t n, int device, int pr
       case KIND_TEXT: { auto* p = new TextModel(); p->prec = precision; impl = p; rc = p->create(host_blob, n); break; }
       case KIND_IMAGE: { auto* p = new ImageModel(); p->prec = precision; impl = p; rc = p->create(host_blob, n); break; }
       case KIND_FUSION: { auto* p = new FusionModel(); impl = p; rc = p->create(host_blob, n); break; }
-      case KIND_IMAGE_MBV2: { auto* p = new MobileNetModel(); impl = p; rc = p->create(host_blob, n); break; }
+      case KIND_IMAGE_MBV2: { auto* p = new MobileNetModel(); p->prec = precision; impl = p; rc = p->create(host_blob, n); break; }
       case KIND_AUDIO: { auto* p = new AudioModel(); impl = p; rc = p->create(host_blob, n); break; }
     }
     if (rc != 0) { delete impl; return -1; }

@@ -274,4 +274,16 @@ __global__ __launch_bounds__(256) static __attribute__((unused)) void avgpool_ke
   y[(size_t)b * C + c] = s / (float)HW;
 }
 
+// Global average pool, NHWC f32 [B, HW, C] -> f32 [B, C]; grid (B, ceil(C/256)).
+__global__ __launch_bounds__(256) static __attribute__((unused)) void avgpool_f32_kernel(const float* __restrict__ x,
+                                                                                         int HW, int C,
+                                                                                         float* __restrict__ y) {
+  const int b = blockIdx.x, c = blockIdx.y * 256 + threadIdx.x;
+  if (c >= C) return;
+  const float* p = x + (size_t)b * HW * C + c;
+  float s = 0.f;
+  for (int q = 0; q < HW; ++q) s += p[(size_t)q * C];
+  y[(size_t)b * C + c] = s / (float)HW;
+}
+
 }  // namespace mec

@@ -140,9 +140,13 @@ struct MobileNetModel : ImageNet {
   std::vector<MbBlock> blocks;
   size_t last_w_off = 0, last_b_off = 0;  // features[18]: f16 [1280][320], f32 [1280]
   size_t fc1_off = 0, fc1b_off = 0, fc2_off = 0, fc2b_off = 0;
+  DevBuf wts32;  // fp32 path (mobilenet_f32.hip): f32 weights, channels padded to 64
   int create(const float* blob, size_t n);
+  int create_f32(const float* blob, size_t n);
   int forward_u8(const uint8_t* img, int B, int H, int W, int C, float* feat, float* logits, float* probs,
                  hipStream_t s) override;
+  int forward_f32(const uint8_t* img, int B, int H, int W, int C, float* feat, float* logits, float* probs,
+                  hipStream_t s);
 };
 
 int resize_u8(const uint8_t* in, int B, int H, int W, uint8_t* out, int OH, int OW, hipStream_t s);

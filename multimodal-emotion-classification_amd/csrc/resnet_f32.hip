@@ -78,17 +78,6 @@ __global__ __launch_bounds__(256) void maxpool_f32_kernel(const float* __restric
   *reinterpret_cast<float4*>(y + idx * 4) = m;
 }
 
-// AdaptiveAvgPool2d(1) on NHWC f32 [B, HW, C] -> [B, C]; grid (B, C / 256).
-__global__ __launch_bounds__(256) void avgpool_f32_kernel(const float* __restrict__ x, int HW, int C,
-                                                          float* __restrict__ y) {
-  const int b = blockIdx.x, c = blockIdx.y * 256 + threadIdx.x;
-  if (c >= C) return;
-  const float* p = x + (size_t)b * HW * C + c;
-  float s = 0.f;
-  for (int q = 0; q < HW; ++q) s += p[(size_t)q * C];
-  y[(size_t)b * C + c] = s / (float)HW;
-}
-
 int ImageModel::create_f32(const float* blob, size_t n) {
   BlobReader rd(blob, n);
   std::vector<float> w;

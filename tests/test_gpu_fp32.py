@@ -120,8 +120,8 @@ def test_precision_query(dev):
     assert s.lib.mec_precision(s.handle) == 1  # speech is fp32 at either setting
     with pytest.raises(ValueError):
         engine.TextEncoder(device=dev, precision='bf16')
-    with pytest.raises(_lib.MecError):
-        engine.MobileNetImageEncoder(device=dev, precision='fp32')
+    m = engine.MobileNetImageEncoder(device=dev, precision='fp32')
+    assert m.lib.mec_precision(m.handle) == 1
 
 
 def test_text_fp32_golden(dev, golden):
@@ -194,3 +194,18 @@ def test_fused_fp32_end_to_end(dev):
                        ('image', got['image'][2], ri[2]), ('fused', got['fusion'][1], rf[1])):
         err, agree = _report(f'fp32 pipeline {name}', g, r)
         assert agree == B and err <= FP32_PROB_TOL, name
+
+
+@pytest.mark.parametrize('B', [3, 32])
+def test_mobilenet_v2_fp32_vs_oracle(dev, B):
+    """MobileNetV2 backbone (BASELINE config "Image-only: MobileNetV2 on 48x48x1") in fp32."""
+    from oracle import image_mbv2 as o_mb
+    gray = syn.image_inputs(B, seed=70 + B)
+    enc = engine.MobileNetImageEncoder(device=dev, precision='fp32')
+    feat, logits, probs = _np(enc.forward(engine.to_device(gray, dev)))
+    sub = np.unique(np.r_[0, np.arange(0, B, max(1, B // 6)), B - 1])
+    rf, rl, rp = o_mb.forward(syn.weights('image_mbv2'), gray[sub])
+    err, agree = _report(f'mobilenet_v2 fp32 B={B}', probs[sub], rp)
+    ferr = float(np.abs(feat[sub] - rf).max() / np.abs(rf).max())
+    print(f'  feat rel err {ferr:.3g}, logits max|d| {np.abs(logits[sub] - rl).max():.3g}')
+    assert agree == len(sub) and err <= FP32_PROB_TOL and ferr <= FP32_FEAT_RTOL
