@@ -270,6 +270,10 @@ int set_option(Options& o, const std::string& k, int value) {
   if (k == "gemm_debug" && (value == 0 || (probe && value >= 1 && value <= 4))) { o.gemm_debug = value; return 0; }
   if (k == "gemm_autotune" && (value == 0 || value == 1)) { o.gemm_autotune = value; return 0; }
   if (k == "gemm_f32_tile" && value >= 0 && value <= 8) { o.gemm_f32_tile = value; return 0; }
+  if (k == "gemm_f32_tag" && value >= 0 && value / 100000 > 0 && value / 100000 < TAG_COUNT && value % 100000 <= 8) {
+    o.gemm_f32_tag[value / 100000] = value % 100000;
+    return 0;
+  }
   if (k == "gemm_prefetch_r" && (value == 0 || value == 1)) { o.gemm_prefetch_r = value; return 0; }
   if (k == "resnet_fused_tail" && (value == 0 || value == 1)) { o.resnet_fused_tail = value; return 0; }
   if (k == "mbv2_impl" && value >= 0 && value <= 2) { o.mbv2_impl = value; return 0; }

@@ -75,6 +75,9 @@ struct Options {
   int gemm_autotune = 1;
   int gemm_prefetch_r = 1;  // f16 residual prefetch in short-K GEMMs
   int gemm_f32_tile = 0;    // forced fp32 GEMM tile id (0 = autotune)
+  // fp32 engine, per launch class: BERT FFN1 pinned to 256x256 on 16x16x4 (it and the 32x32x2
+  // form time within 0.3%, so the autotune flipped between them run to run)
+  int gemm_f32_tag[TAG_COUNT] = {0, 0, 0, 0, /*TAG_BERT_FFN1*/ 8};
   // per launch class (profiling tag): forced tile, 0 = autotune. The BERT O-projection is
   // pinned to 128 x 128 (its candidates time within 2% alone; in the encoder 128 x 128 wins)
   int gemm_bn_tag[TAG_COUNT] = {0, 0, 0, /*TAG_BERT_OPROJ*/ 11128};
