@@ -151,10 +151,12 @@ int mec_conv_f32(const float* x, const float* w, const float* bias, const float*
  *   "resnet_fused_tail" [0]|1, "mbv2_impl" [0]|1|2
  *   "fusion_r" 1|2|[4]     samples per fusion workgroup
  *   "fusion_split" 0|[1]   fusion as 3 launches (per-modality projection, cross-attention, head)
+ *   "speech_impl" [0]|1    speech DNN: 0 = layer-split launch (speech_flow_kernel, in-launch
+ *                          hand-offs between 16-sample stages), 1 = one workgroup per 4 samples
  * Probe values, which skip work to time a kernel's parts and return WRONG results, exist only
  * in the -DMEC_PROBES build (libmec_hip_probes.so, `make probes`; tools/ only): "gemm_debug"
- * 1..4, "conv3x3_debug" / "stem_debug" 1|2|4|7, "bert_qkv_attn" 2|3, "bert_oproj_ln" 2|4. The
- * product library rejects them (-1). */
+ * 1..4, "conv3x3_debug" / "stem_debug" 1|2|4|7, "bert_qkv_attn" 2|3, "bert_oproj_ln" 2|4,
+ * "audio_debug" 1|2|4|8|15, "speech_debug" 1. The product library rejects them (-1). */
 int mec_set_option(const char* key, int value);
 int mec_model_set_option(mec_model* m, const char* key, int value);
 

@@ -8,9 +8,6 @@
 
 namespace mec {
 const char* last_error();
-extern int g_fusion_r;
-extern int g_fusion_split;
-extern int g_gemm_bn_tag[TAG_COUNT];
 
 size_t blob_floats(int kind) {
   switch (kind) {
@@ -267,6 +264,7 @@ int set_option(Options& o, const std::string& k, int value) {
   if (k == "gemm_impl" && (value == 1 || value == 2)) { o.gemm_impl = value; return 0; }
   if (k == "fusion_r" && (value == 1 || value == 2 || value == 4)) { o.fusion_r = value; return 0; }
   if (k == "fusion_split" && (value == 0 || value == 1)) { o.fusion_split = value; return 0; }
+  if (k == "speech_impl" && (value == 0 || value == 1)) { o.speech_impl = value; return 0; }
   if (k == "gemm_debug" && (value == 0 || (probe && value >= 1 && value <= 4))) { o.gemm_debug = value; return 0; }
   if (k == "gemm_autotune" && (value == 0 || value == 1)) { o.gemm_autotune = value; return 0; }
   if (k == "gemm_f32_tile" && value >= 0 && value <= 8) { o.gemm_f32_tile = value; return 0; }
@@ -295,6 +293,10 @@ int set_option(Options& o, const std::string& k, int value) {
   if (k == "pw_chain_form" && (value >= 0 && value <= 2)) { o.pw_chain_form = value; return 0; }
   if (k == "conv3x3_debug" && (value == 0 || (probe && (value == 1 || value == 2 || value == 4 || value == 7)))) {
     o.conv3x3_debug = value;
+    return 0;
+  }
+  if (k == "speech_debug" && (value == 0 || (probe && value == 1))) {
+    o.speech_debug = value;
     return 0;
   }
   if (k == "audio_debug" && (value == 0 || (probe && (value == 1 || value == 2 || value == 4 || value == 8 || value == 15)))) {

@@ -311,8 +311,10 @@ int launch_gemm_f32(const GemmParams& p, hipStream_t s, Prof* prof, int tag) {
   }
   const auto key = f32_key(p);
   int id = opt().gemm_f32_tile;
-  if (!id && tag > 0 && tag < TAG_COUNT && p.N % tile_n(std::max(1, opt().gemm_f32_tag[tag])) == 0)
+  if (!id && tag > 0 && tag < TAG_COUNT && opt().gemm_f32_tag[tag] && p.N % tile_n(opt().gemm_f32_tag[tag]) == 0) {
     id = opt().gemm_f32_tag[tag];
+    tune_cache().put(key, id);  // so mec_model_gemm_query reports the tile that runs
+  }
   if (id) {
     MEC_REQUIRE(id >= 1 && id <= 8 && p.N % tile_n(id) == 0, "gemm_f32: forced tile does not fit N");
   } else {

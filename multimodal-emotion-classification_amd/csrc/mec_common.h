@@ -91,7 +91,8 @@ struct Options {
   int mbv2_impl = 0;
   int fusion_r = 4;         // samples per fusion workgroup
   int fusion_split = 1;     // fusion as 3 launches
-  int gemm_debug = 0, conv3x3_debug = 0, stem_debug = 0, audio_debug = 0;  // probe builds only
+  int speech_impl = 0;      // 0 = layer-split dataflow kernel (speech_flow_kernel), 1 = one WG per 4 samples
+  int gemm_debug = 0, conv3x3_debug = 0, stem_debug = 0, audio_debug = 0, speech_debug = 0;  // probe builds only
 };
 
 // GEMM autotuner results: tile id per (engine, shape), per handle.

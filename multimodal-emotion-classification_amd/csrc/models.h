@@ -29,6 +29,10 @@ struct Model {
 struct SpeechModel : Model {
   DevBuf w;  // fp32: mean, scale, {W,b,inv,shift} x5, W6, b6
   size_t off_mean = 0, off_scale = 0, off_W[6] = {}, off_b[6] = {}, off_inv[5] = {}, off_shift[5] = {};
+  // speech_flow_kernel: hand-off buffers of layers 0-3 (f32 [16 * chunks, N_l]) and the
+  // per-chunk arrival counters (zero between launches: the last stage resets them) + error word
+  DevBuf flow_act, flow_sync;
+  int flow_chunks = 0;
   int create(const float* blob, size_t n);
   int forward(const float* x, int B, float* feat, float* logits, float* probs, hipStream_t s);
 };

@@ -70,6 +70,250 @@ __global__ __launch_bounds__(512) void speech_kernel(SpeechW w, const float* __r
   }
 }
 
+// ---- speech_flow_kernel: the same network with every layer split by output columns over
+// workgroups, so each weight byte is read by one workgroup per 16-sample chunk instead of
+// by every workgroup (speech_kernel streams all 1.85 MB of weights through each CU, which
+// bounds it at ~40 us for any batch). Per chunk of 16 samples, five stages:
+//   stage 0  L0  56->512   8 WGs x 64 columns (4 waves = 4 column tiles, K 56 padded to 64)
+//   stage 1  L1 512->512  32 WGs x 16 columns (4 waves = 4 K quarters, summed in LDS)
+//   stage 2  L2 512->256  16 WGs x 16 columns
+//   stage 3  L3 256->128   8 WGs x 16 columns
+//   stage 4  L4 128->64 + Dense7 + softmax, 1 WG (writes feat / logits / probs)
+// on v_mfma_f32_16x16x4f32 (exact f32 products, fp32 accumulate). A stage's workgroup loads
+// its weight fragments into registers, then reads its inputs from the previous stage.
+// Hand-off (MI355X_MICROARCH.md, inter-workgroup visibility, first row of the sc1 hand-off
+// table): the producer stores its activations write-through (sc1), every storing wave drains
+// them (vmcnt(0)), a workgroup barrier, then one agent-scope atomic add on the chunk's
+// per-stage counter; the consumer polls that counter with one lane (sc1 dword loads + s_sleep)
+// and every wave reads its inputs with sc1 loads. Blocks are numbered stage-major, so every
+// producer precedes its consumers in dispatch order; every spin is bounded (an expired wait
+// sets the sticky error word and the stage proceeds; the chunk's probs then come out NaN).
+// The last stage of a chunk resets the chunk's counters: by then every wait on them is over
+// (each stage arrives only after its own wait and reads). Measured hop on MI355X, B = 32:
+// ~1.9 us from the last arrival to the wait's exit, ~1.2 us for the sc1 input loads.
+// (Tagged 8-B granules polled directly, with or without the counter, measured no faster at
+// B = 32 and up to 2x slower at B = 256, where 1,040 polling blocks flood the memory system.)
+constexpr int SPF_SB = 16;    // samples per chunk
+constexpr int SPF_LINE = 32;  // u32 words between counters (one 128-B line each)
+constexpr int SPF_WG_PER_CHUNK = 8 + 32 + 16 + 8 + 1;
+constexpr int SPF_SPIN_LIMIT = 1 << 22;
+__host__ __device__ constexpr int spf_groups(int st) {
+  return st == 0 ? 8 : st == 1 ? 32 : st == 2 ? 16 : st == 3 ? 8 : 1;
+}
+
+struct SpeechFlow {
+  float* act[4];               // stage outputs, f32 [16 * chunks, N_l]
+  unsigned* cnt;               // [chunks][4] arrival counters, SPF_LINE apart
+  unsigned* err;               // sticky: a wait expired
+  int chunks;
+};
+
+typedef float f32x4 __attribute__((ext_vector_type(4)));
+
+__device__ __forceinline__ f32x4 ld_sc1x4(const float* p) {
+  f32x4 v;
+  asm volatile("global_load_dwordx4 %0, %1, off sc1" : "=v"(v) : "v"(p) : "memory");
+  return v;
+}
+__device__ __forceinline__ void st_sc1x4(float* p, f32x4 v) {
+  asm volatile("global_store_dwordx4 %0, %1, off sc1" ::"v"(p), "v"(v) : "memory");
+}
+__device__ __forceinline__ void st_sc1(float* p, float v) {
+  asm volatile("global_store_dword %0, %1, off sc1" ::"v"(p), "v"(v) : "memory");
+}
+
+struct SpfShared {
+  float red[4][256];          // per-wave 16x16 partial sums (K-split stages)
+  float hs[SPF_SB][64 + 1];   // stage 4: block-5 ReLU output
+  float lg[SPF_SB][8];        // stage 4: logits
+  float w5[64 * 7 + 8];       // stage 4: Dense(7) kernel + bias, loaded at entry
+};
+
+// DBG (probe build, option speech_debug; wrong results): lane 0 of every block writes six
+// s_memrealtime stamps (100 MHz) into feat as u64 [block][6] (entry, weights issued, wait
+// over, inputs landed, outputs drained, arrival) and stage 4 skips its outputs.
+template <int ST, int DBG>
+__device__ __forceinline__ void spf_stage(const SpeechW& w, const SpeechFlow& f, const float* __restrict__ x, int B,
+                                          int chunk, int g, float* feat, float* logits, float* probs,
+                                          SpfShared& sh) {
+  auto stamp = [&](int i) {
+    if constexpr (DBG) {
+      if (threadIdx.x == 0)
+        reinterpret_cast<unsigned long long*>(feat)[blockIdx.x * 6 + i] = __builtin_amdgcn_s_memrealtime();
+    }
+  };
+  stamp(0);
+  constexpr int K = ST == 0 ? 56 : ST == 1 ? 512 : ST == 2 ? 512 : ST == 3 ? 256 : 128;
+  constexpr int N = ST == 0 ? 512 : ST == 1 ? 512 : ST == 2 ? 256 : ST == 3 ? 128 : 64;
+  constexpr int CT = (ST == 0 || ST == 4) ? 4 : 1;  // column tiles per WG (one per wave)
+  constexpr int KS = 4 / CT;                          // K split over waves
+  constexpr int KP = ST == 0 ? 64 : K;
+  constexpr int T = KP / (16 * KS);                   // 16-deep k groups per wave
+  static_assert(N % (16 * CT) == 0 && N / (16 * CT) == spf_groups(ST), "stage geometry");
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int c16 = lane & 15, q = lane >> 4;
+  const int ct = wave % CT, ks = wave / CT;
+  const int n0 = g * 16 * CT;
+  const int n = n0 + ct * 16 + c16;
+  const int kb = ks * (KP / KS);
+  const int row0 = chunk * SPF_SB;
+  const int r = row0 + c16;
+
+  // B fragments (lane: k = kb + 16t + 4q + j, column n) and the epilogue constants: independent
+  // of the previous stage, so they load while it runs
+  const float* W = w.W[ST];
+  float bw[T][4];
+#pragma unroll
+  for (int t = 0; t < T; ++t)
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+      const int k = kb + 16 * t + 4 * q + j;
+      bw[t][j] = (KP == K || k < K) ? W[(size_t)k * N + n] : 0.f;
+    }
+  const int fin_c = n0 + (tid & 3) * 4;  // K-split finisher: 4 columns
+  float ep_b[4], ep_i[4], ep_s[4];
+#pragma unroll
+  for (int i = 0; i < 4; ++i) {
+    const int nn = KS == 1 ? n : fin_c + i;
+    ep_b[i] = w.b[ST][nn];
+    ep_i[i] = w.inv[ST][nn];
+    ep_s[i] = w.shift[ST][nn];
+  }
+  if constexpr (ST == 4)
+    for (int i = tid; i < 64 * 7 + 7; i += blockDim.x) sh.w5[i] = i < 64 * 7 ? w.W[5][i] : w.b[5][i - 64 * 7];
+  stamp(1);
+  if constexpr (ST > 0) {
+    if (tid == 0) {
+      const unsigned* c = f.cnt + (size_t)(chunk * 4 + ST - 1) * SPF_LINE;
+      for (int spins = 0; __hip_atomic_load(c, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) < spf_groups(ST - 1);) {
+        __builtin_amdgcn_s_sleep(1);
+        if (++spins > SPF_SPIN_LIMIT) {
+          __hip_atomic_fetch_or(f.err, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+          break;
+        }
+      }
+    }
+    __syncthreads();
+  }
+  stamp(2);
+
+  // A fragments (lane: row c16 of the chunk, k = kb + 16t + 4q + j)
+  f32x4 a[T];
+  if constexpr (ST == 0) {
+#pragma unroll
+    for (int t = 0; t < T; ++t)
+#pragma unroll
+      for (int j = 0; j < 4; ++j) {
+        const int k = kb + 16 * t + 4 * q + j;
+        // sklearn StandardScaler.transform: (X - mean_) / scale_
+        a[t][j] = (r < B && k < K) ? (x[(size_t)r * K + k] - w.mean[k]) / w.scale[k] : 0.f;
+      }
+  } else {
+    const float* in = f.act[ST - 1] + (size_t)r * K + kb + 4 * q;
+#pragma unroll
+    for (int t = 0; t < T; ++t) a[t] = ld_sc1x4(in + 16 * t);
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+#pragma unroll
+    for (int t = 0; t < T; ++t) asm volatile("" : "+v"(a[t]));  // uses stay behind the wait
+  }
+  stamp(3);
+
+  f32x4 acc = {0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+  for (int t = 0; t < T; ++t)
+#pragma unroll
+    for (int j = 0; j < 4; ++j) acc = __builtin_amdgcn_mfma_f32_16x16x4f32(a[t][j], bw[t][j], acc, 0, 0, 0);
+
+  // Dense bias, then tf.nn.batch_normalization x * inv + (beta - mean * inv), then ReLU.
+  // D layout: lane holds rows 4q + e of column c16.
+  if constexpr (KS == 1) {
+#pragma unroll
+    for (int e = 0; e < 4; ++e) {
+      const int row = 4 * q + e;
+      const float v = fmaxf((acc[e] + ep_b[0]) * ep_i[0] + ep_s[0], 0.f);
+      if constexpr (ST < 4)
+        st_sc1(f.act[ST] + (size_t)(row0 + row) * N + n, v);
+      else
+        sh.hs[row][n] = v;
+    }
+  } else {
+#pragma unroll
+    for (int e = 0; e < 4; ++e) sh.red[wave][(4 * q + e) * 16 + c16] = acc[e];
+    __syncthreads();
+    if (tid < 64) {
+      const int row = tid >> 2, c4 = (tid & 3) * 4;
+      f32x4 v;
+#pragma unroll
+      for (int i = 0; i < 4; ++i) {
+        const int o = row * 16 + c4 + i;
+        const float s = ((sh.red[0][o] + sh.red[1][o]) + sh.red[2][o]) + sh.red[3][o];
+        v[i] = fmaxf((s + ep_b[i]) * ep_i[i] + ep_s[i], 0.f);
+      }
+      st_sc1x4(f.act[ST] + (size_t)(row0 + row) * N + n0 + c4, v);
+    }
+  }
+
+  if constexpr (ST < 4) {  // publish: every storing wave drained, a barrier, one arrival
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    __syncthreads();
+    stamp(4);
+    if (tid == 0)
+      __hip_atomic_fetch_add(f.cnt + (size_t)(chunk * 4 + ST) * SPF_LINE, 1u, __ATOMIC_RELAXED,
+                             __HIP_MEMORY_SCOPE_AGENT);
+  } else {
+    __syncthreads();
+    stamp(4);
+    if (tid == 0)  // every wait of this chunk is over: reset its counters for the next launch
+      for (int s = 0; s < 4; ++s)
+        __hip_atomic_store(f.cnt + (size_t)(chunk * 4 + s) * SPF_LINE, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    if constexpr (DBG) {
+      stamp(5);
+      return;
+    }
+    const int nr = min(SPF_SB, B - row0);
+    for (int i = tid; i < nr * 64; i += blockDim.x) feat[(size_t)row0 * 64 + i] = sh.hs[i >> 6][i & 63];
+    if (tid < SPF_SB * 7) {  // Dense(7): feat @ W + b
+      const int row = tid / 7, o = tid - row * 7;
+      float s = 0.f;
+#pragma unroll 16
+      for (int k = 0; k < 64; ++k) s = fmaf(sh.hs[row][k], sh.w5[k * 7 + o], s);
+      sh.lg[row][o] = s + sh.w5[64 * 7 + o];
+    }
+    __syncthreads();
+    if (tid < nr) {
+      const bool bad = __hip_atomic_load(f.err, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) != 0;
+      const float* z = sh.lg[tid];
+      float m = z[0];
+      for (int o = 1; o < 7; ++o) m = fmaxf(m, z[o]);
+      float e[7], s = 0.f;
+      for (int o = 0; o < 7; ++o) { e[o] = expf(z[o] - m); s += e[o]; }
+      const size_t ro = (size_t)(row0 + tid) * 7;
+      for (int o = 0; o < 7; ++o) {
+        logits[ro + o] = z[o];
+        probs[ro + o] = bad ? __builtin_nanf("") : e[o] / s;
+      }
+    }
+  }
+  stamp(5);
+}
+
+template <int DBG>
+__global__ __launch_bounds__(256) void speech_flow_kernel(SpeechW w, SpeechFlow f, const float* __restrict__ x, int B,
+                                                          float* feat, float* logits, float* probs) {
+  __shared__ SpfShared sh;
+  const int nc = f.chunks;
+  int b = blockIdx.x;
+  if (b < 8 * nc) return spf_stage<0, DBG>(w, f, x, B, b / 8, b % 8, feat, logits, probs, sh);
+  b -= 8 * nc;
+  if (b < 32 * nc) return spf_stage<1, DBG>(w, f, x, B, b / 32, b % 32, feat, logits, probs, sh);
+  b -= 32 * nc;
+  if (b < 16 * nc) return spf_stage<2, DBG>(w, f, x, B, b / 16, b % 16, feat, logits, probs, sh);
+  b -= 16 * nc;
+  if (b < 8 * nc) return spf_stage<3, DBG>(w, f, x, B, b / 8, b % 8, feat, logits, probs, sh);
+  b -= 8 * nc;
+  spf_stage<4, DBG>(w, f, x, B, b, 0, feat, logits, probs, sh);
+}
+
 int SpeechModel::create(const float* blob, size_t n) {
   BlobReader rd(blob, n);
   const int dims[6] = {56, 512, 512, 256, 128, 64};
@@ -113,9 +357,42 @@ int SpeechModel::forward(const float* x, int B, float* feat, float* logits, floa
   p.scale = base + off_scale;
   for (int l = 0; l < 6; ++l) { p.W[l] = base + off_W[l]; p.b[l] = base + off_b[l]; }
   for (int l = 0; l < 5; ++l) { p.inv[l] = base + off_inv[l]; p.shift[l] = base + off_shift[l]; }
+  if (opt().speech_impl == 1) {
+    MEC_TRY(prof.begin(TAG_SPEECH, s));
+    hipLaunchKernelGGL(speech_kernel, dim3((B + SPEECH_R - 1) / SPEECH_R), dim3(SF_THREADS), 0, s, p, x, B, feat,
+                       logits, probs);
+    MEC_LAUNCH_CHECK();
+    MEC_TRY(prof.end(TAG_SPEECH, s));
+    return 0;
+  }
+  const int nch = (B + SPF_SB - 1) / SPF_SB;
+  MEC_REQUIRE(nch <= (1 << 24) / SPF_WG_PER_CHUNK, "speech: batch too large");
+  if (nch > flow_chunks) {  // grown: counters start at zero
+    MEC_TRY(flow_act.ensure((size_t)nch * SPF_SB * (512 + 512 + 256 + 128) * sizeof(float)));
+    MEC_TRY(flow_sync.ensure(((size_t)nch * 4 + 1) * SPF_LINE * sizeof(unsigned)));
+    MEC_HIP(hipMemsetAsync(flow_sync.p, 0, flow_sync.bytes, s));
+    flow_chunks = nch;
+  }
+  SpeechFlow fl;
+  float* a = flow_act.as<float>();
+  const size_t rows = (size_t)flow_chunks * SPF_SB;
+  fl.act[0] = a;
+  fl.act[1] = a + rows * 512;
+  fl.act[2] = a + rows * 1024;
+  fl.act[3] = a + rows * 1280;
+  fl.cnt = flow_sync.as<unsigned>();
+  fl.err = fl.cnt + (size_t)flow_chunks * 4 * SPF_LINE;
+  fl.chunks = nch;
   MEC_TRY(prof.begin(TAG_SPEECH, s));
-  hipLaunchKernelGGL(speech_kernel, dim3((B + SPEECH_R - 1) / SPEECH_R), dim3(SF_THREADS), 0, s, p, x, B, feat,
-                     logits, probs);
+#ifdef MEC_PROBES
+  if (opt().speech_debug) {
+    MEC_REQUIRE((size_t)B * 64 >= (size_t)nch * SPF_WG_PER_CHUNK * 12, "speech_debug: feat too small for the trace");
+    hipLaunchKernelGGL(speech_flow_kernel<1>, dim3(nch * SPF_WG_PER_CHUNK), dim3(256), 0, s, p, fl, x, B, feat, logits,
+                       probs);
+  } else
+#endif
+  hipLaunchKernelGGL(speech_flow_kernel<0>, dim3(nch * SPF_WG_PER_CHUNK), dim3(256), 0, s, p, fl, x, B, feat, logits,
+                     probs);
   MEC_LAUNCH_CHECK();
   MEC_TRY(prof.end(TAG_SPEECH, s));
   return 0;

@@ -91,7 +91,8 @@ def test_option_validation_without_gpu():
     lib = _lib.load()
     assert lib.mec_build_flags() == 0, 'the product library must not be a probe build'
     probes = [(b'gemm_debug', 1), (b'gemm_debug', 2), (b'gemm_debug', 4), (b'stem_debug', 1), (b'conv3x3_debug', 2),
-              (b'bert_qkv_attn', 2), (b'bert_qkv_attn', 3), (b'bert_oproj_ln', 2), (b'bert_oproj_ln', 4)]
+              (b'bert_qkv_attn', 2), (b'bert_qkv_attn', 3), (b'bert_oproj_ln', 2), (b'bert_oproj_ln', 4),
+              (b'speech_debug', 1), (b'audio_debug', 15)]
     for k, v in probes:
         assert lib.mec_set_option(k, v) == -1, (k, v)
         assert b'MEC_PROBES' in lib.mec_last_error()
@@ -99,10 +100,11 @@ def test_option_validation_without_gpu():
           (b'bert_qkv_attn', 0), (b'bert_qkv_attn', 1), (b'bert_oproj_ln', 0), (b'bert_oproj_ln', 1),
           (b'gemm_bn', 40256), (b'gemm_bn', 0),
           (b'gemm_bn_tag', 3 * 100000 + 40256), (b'gemm_bn_tag', 3 * 100000 + 11128),
-          (b'gemm_debug', 0), (b'gemm_f32_tile', 3), (b'gemm_f32_tile', 0), (b'bert_oproj_ln', 3)]
+          (b'gemm_debug', 0), (b'gemm_f32_tile', 3), (b'gemm_f32_tile', 0), (b'bert_oproj_ln', 3),
+          (b'speech_impl', 1), (b'speech_impl', 0), (b'speech_debug', 0)]
     bad = [(b'gemm_f32_tile', 9), (b'fusion_r', 3), (b'fusion_split', 2), (b'bert_qkv_attn', 4), (b'bert_oproj_ln', 5), (b'gemm_bn', 12345),
            (b'gemm_bn', 42256), (b'gemm_bn_tag', 11128), (b'gemm_bn_tag', 15 * 100000 + 256),
-           (b'gemm_bn_tag', 3 * 100000 + 999), (b'gemm_bn_tag', -1), (b'gemm_debug', 5)]
+           (b'gemm_bn_tag', 3 * 100000 + 999), (b'gemm_bn_tag', -1), (b'gemm_debug', 5), (b'speech_impl', 2)]
     try:
         for k, v in ok:
             assert lib.mec_set_option(k, v) == 0, (k, v)
@@ -110,7 +112,7 @@ def test_option_validation_without_gpu():
             assert lib.mec_set_option(k, v) == -1, (k, v)
             assert b'bad value' in lib.mec_last_error()
     finally:  # the defaults
-        for k, v in [(b'fusion_r', 4), (b'fusion_split', 1), (b'bert_qkv_attn', 1), (b'bert_oproj_ln', 0),
+        for k, v in [(b'fusion_r', 4), (b'fusion_split', 1), (b'bert_qkv_attn', 1), (b'bert_oproj_ln', 0), (b'speech_impl', 0),
                      (b'gemm_f32_tile', 0),
                      (b'gemm_bn', 0),
                      (b'gemm_bn_tag', 3 * 100000 + 11128), (b'gemm_debug', 0)]:
