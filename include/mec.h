@@ -134,7 +134,7 @@ int mec_conv_f32(const float* x, const float* w, const float* bias, const float*
  * each other: mec_model_set_option sets one handle's knob; mec_set_option sets the process
  * default that handles created AFTERWARDS copy (and that the handle-less kernel entry points
  * use). Every pair of settings of one knob gives bit-identical outputs, except "fusion_r" 4 vs
- * 1|2 (ulp-level fp32 reassociation, both within the oracle tolerance).
+ * 1|2 and "conv3x3_halo" 0 vs 1 (fp32 reassociation, both within the oracle tolerance).
  *   "gemm_impl" 1|[2]      register-staged / glds GEMM engine
  *   "gemm_bn" [0]|id       force one f16 GEMM tile (0 = autotune), "gemm_autotune" 0|[1]
  *   "gemm_bn_tag" tag*100000+id   force a tile for one launch class (e.g. 3 = BERT O-proj)
@@ -142,6 +142,8 @@ int mec_conv_f32(const float* x, const float* w, const float* bias, const float*
  *   "gemm_f32_tag" tag*100000+id  pin an fp32 tile for one launch class (default: BERT FFN1 -> 8)
  *   "gemm_prefetch_r" 0|[1]  f16 residual prefetch in short-K GEMMs
  *   "conv3x3_direct" 0|[1] layer1 3x3 conv on the halo-tile kernel (mec_conv_f16 too)
+ *   "conv3x3_halo" 0|[1]   layers 2-3 stride-1 3x3 convs on the halo kernel (mec_conv_f16 too;
+ *                          fp32 accumulation in another order: not bit-identical to 0)
  *   "pw_chain" 0|1|[2]     layer1 seam kernels (1: the 256->64 seams, 2: also 256->128)
  *   "pw_chain_form" [0]|1|2  seam weight placement (LDS / registers)
  *   "bert_qkv_attn" 0|[1]  fused BERT QKV projection + attention

@@ -235,6 +235,10 @@ int launch_gemm(const GemmParams& p, hipStream_t s, Prof* prof, int tag) {
   if (opt().conv3x3_direct && !opt().gemm_bn && p.amode == A_CONV && p.ks == 3 && p.stride == 1 && p.pad == 1 && p.H == 56 &&
       p.W == 56 && p.C == 64 && p.N == 64 && p.act == ACT_RELU && !p.R && p.C16 && !p.C32 && p.M % (56 * 56) == 0)
     rc = launch_conv3x3_c64(reinterpret_cast<const f16*>(p.A), p.B, p.bias, p.C16, p.M / (56 * 56), 56, 64, 64, s);
+  else if (opt().conv3x3_halo && !opt().gemm_bn && p.amode == A_CONV && p.ks == 3 && p.stride == 1 && p.pad == 1 &&
+           p.H == p.W && p.OH == p.H && p.OW == p.W && conv3x3_halo_supported(p.H, p.C, p.N) && p.act == ACT_RELU &&
+           !p.R && p.bias && p.C16 && !p.C32 && p.M % (p.H * p.W) == 0)
+    rc = launch_conv3x3_halo(reinterpret_cast<const f16*>(p.A), p.B, p.bias, p.C16, p.M / (p.H * p.W), p.H, p.C, s);
   else if (opt().gemm_impl == 2)
     rc = launch_gemm_glds(p, s, opt().gemm_bn ? opt().gemm_bn : (tag > 0 && tag < TAG_COUNT ? opt().gemm_bn_tag[tag] : 0));
   else

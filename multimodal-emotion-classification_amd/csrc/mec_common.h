@@ -82,6 +82,7 @@ struct Options {
   // pinned to 128 x 128 (its candidates time within 2% alone; in the encoder 128 x 128 wins)
   int gemm_bn_tag[TAG_COUNT] = {0, 0, 0, /*TAG_BERT_OPROJ*/ 11128};
   int conv3x3_direct = 1;   // ResNet layer1 conv2 on the halo-tile kernel (conv3x3.hip)
+  int conv3x3_halo = 1;     // layers 2-3 stride-1 conv2 on the halo kernel (conv3x3_halo.hip)
   int resnet_fused_tail = 0;
   int resnet_chunk = 0;
   int pw_chain = 2;         // layer1 seam kernels (pw_chain.hip)
@@ -210,6 +211,11 @@ int launch_gemm_glds(const GemmParams& p, hipStream_t s, int force_bn);
 // launch_gemm routes matching A_CONV shapes to it while opt().conv3x3_direct is set
 int launch_conv3x3_c64(const f16* x, const f16* w, const float* bias, f16* y, int B, int H, int C, int Cout,
                        hipStream_t s);
+// 3x3/1 convs C -> C on 28x28x128 and 14x14x256 (+ BN shift + ReLU): halo kernel
+// (conv3x3_halo.hip), routed from launch_gemm while opt().conv3x3_halo is set. Same fp32
+// accumulation as the GEMM path in another summation order (not bit-identical to it).
+bool conv3x3_halo_supported(int H, int C, int N);
+int launch_conv3x3_halo(const f16* x, const f16* w, const float* bias, f16* y, int B, int H, int C, hipStream_t s);
 int gemm_tuned_bn(int amode, int M, int N, int K);
 // fp32 engine (gemm_f32.hip): f32 A (plain or NHWC conv) and B32, v_mfma_f32_32x32x2_f32
 int launch_gemm_f32(const GemmParams& p, hipStream_t s, Prof* prof, int tag);

@@ -239,6 +239,44 @@ def test_conv3x3_c64_bit_identical(dev, n):
     assert torch.equal(outs[0], outs[1])
 
 
+@pytest.mark.parametrize('H,C', [(28, 128), (14, 256)])
+@pytest.mark.parametrize('n', [1, 6, 13])
+def test_conv3x3_halo(dev, H, C, n):
+    """ResNet layers 2-3's stride-1 3x3 convs (28x28x128, 14x14x256) on the halo kernel
+    (conv3x3_halo.hip) vs the implicit-GEMM path and torch fp32: the same fp32 accumulation in
+    another order, so within f16 output rounding of the GEMM path, not bit-identical. A batch
+    split gives the same bits (image 0 alone = image 0 of the batch); n = 13 gives 52 / 26 tiles
+    on partially filled XCD groups."""
+    lib = _lib.load()
+    g = torch.Generator().manual_seed(1000 * n + H)
+    x = torch.rand(n, H, H, C, generator=g).half().to(dev)
+    w = ((torch.rand(C, 3, 3, C, generator=g) * 2 - 1) * (9 * C) ** -0.5).half().to(dev)
+    bias = (torch.rand(C, generator=g) - 0.5).to(dev)
+
+    def run(halo, xx):
+        y = torch.full(xx.shape, float('nan'), dtype=torch.float16, device=dev)
+        _lib.check(lib.mec_set_option(b'conv3x3_halo', halo), 'option')
+        try:
+            _lib.check(lib.mec_conv_f16(_p(xx), _p(w), _p(bias), None, _p(y), xx.shape[0], H, H, C, C, 3, 1, 1, 1, _s()),
+                       'conv')
+        finally:
+            lib.mec_set_option(b'conv3x3_halo', 1)
+        torch.cuda.synchronize()
+        return y.cpu()
+
+    yh, yg = run(1, x), run(0, x)
+    ref = torch.relu(torch.nn.functional.conv2d(x.permute(0, 3, 1, 2).float(), w.permute(0, 3, 1, 2).float(), bias,
+                                                padding=1)).permute(0, 2, 3, 1).cpu()
+    assert not torch.isnan(yh).any()
+    assert _rel_err(yh.float(), ref) < 2e-3
+    # both paths round an fp32 sum of the same products (reassociation error ~1e-5 absolute
+    # at these magnitudes) to f16: one f16 ulp apart at most, plus that error near zero
+    d = (yh.float() - yg.float()).abs()
+    ulp = torch.maximum(yh.float().abs(), yg.float().abs()).clamp_min(2 ** -14) * 2 ** -10
+    assert bool((d <= ulp + 1e-4).all()), float((d - ulp).max())
+    assert torch.equal(run(1, x[:1].contiguous())[0], yh[0])
+
+
 @pytest.mark.parametrize('B', [3, 37])
 def test_pw_chain_bit_identical(dev, B):
     """ResNet50 with layer1's seam kernels (pw_chain.hip: block 1 -> 2 dual seam, block 2 -> 3
