@@ -157,7 +157,7 @@ int mec_conv_f32(const float* x, const float* w, const float* bias, const float*
  *                          hand-offs between 16-sample stages), 1 = one workgroup per 4 samples
  * Probe values, which skip work to time a kernel's parts and return WRONG results, exist only
  * in the -DMEC_PROBES build (libmec_hip_probes.so, `make probes`; tools/ only): "gemm_debug"
- * 1..4, "conv3x3_debug" / "stem_debug" 1|2|4|7, "bert_qkv_attn" 2|3, "bert_oproj_ln" 2|4,
+ * 1..5, "conv3x3_debug" / "stem_debug" 1|2|4|7, "bert_qkv_attn" 2|3, "bert_oproj_ln" 2|4,
  * "audio_debug" 1|2|4|8|15, "speech_debug" 1. The product library rejects them (-1). */
 int mec_set_option(const char* key, int value);
 int mec_model_set_option(mec_model* m, const char* key, int value);

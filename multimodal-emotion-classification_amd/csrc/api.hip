@@ -265,7 +265,7 @@ int set_option(Options& o, const std::string& k, int value) {
   if (k == "fusion_r" && (value == 1 || value == 2 || value == 4)) { o.fusion_r = value; return 0; }
   if (k == "fusion_split" && (value == 0 || value == 1)) { o.fusion_split = value; return 0; }
   if (k == "speech_impl" && (value == 0 || value == 1)) { o.speech_impl = value; return 0; }
-  if (k == "gemm_debug" && (value == 0 || (probe && value >= 1 && value <= 4))) { o.gemm_debug = value; return 0; }
+  if (k == "gemm_debug" && (value == 0 || (probe && value >= 1 && value <= 5))) { o.gemm_debug = value; return 0; }
   if (k == "gemm_autotune" && (value == 0 || value == 1)) { o.gemm_autotune = value; return 0; }
   if (k == "gemm_f32_tile" && value >= 0 && value <= 8) { o.gemm_f32_tile = value; return 0; }
   if (k == "gemm_f32_tag" && value >= 0 && value / 100000 > 0 && value / 100000 < TAG_COUNT && value % 100000 <= 8) {

@@ -19,25 +19,28 @@ __device__ __forceinline__ int sw(int row, int kc) {
   else return kc ^ ((4 - ((row >> 2) & 3)) & 3);
 }
 
-// GELU(x) = x/2 (1 + erf(x/sqrt2)) (HF "gelu"), erf by Abramowitz-Stegun 7.1.26
-// (|err| <= 1.5e-7 absolute over [-12, 12], far below the f16 rounding of FFN1's output).
-// With z = |x|/sqrt2: erf(z) = 1 - t P(t) exp(-z^2), t = 1/(1 + p z), so
-//   GELU(x) = 0.5 (x + |x| (1 - t P(t) exp2(-x^2 log2(e)/2)))      (no sign select)
-// evaluated on pairs with packed f32 math; v_rcp / v_exp are the raw instructions.
+// GELU(x) = x Phi(x) = x/2 (1 + erf(x/sqrt2)) (HF "gelu") with Phi(x) - 1/2 = c P(c^2) / Q(c^2),
+// c = clamp(x, -5.5, 5.5), a (4, 3) rational minimax fit (|GELU error| <= 3.0e-6 max(|x|, 1) in
+// f32, about 0.6 % of the f16 ulp of FFN1's output; Phi(-5.5) = 1.9e-8): 12 VALU + one v_rcp per
+// element, where the Abramowitz-Stegun 7.1.26 erf it replaces took two transcendentals (v_rcp,
+// v_exp) and ~13 VALU (|err| <= 4.6e-7): the BERT FFN1 epilogue's GELU 37 -> ~28 us at B = 256.
+// Fit: least squares in s = c^2 weighted by c, refined by Levenberg-Marquardt, then rounded to
+// f32 (tools/gelu_fit.py).
 typedef float f32x2 __attribute__((ext_vector_type(2)));
-__device__ __forceinline__ f32x2 gelu_erf_x2(f32x2 x) {
-  const f32x2 ax = {fabsf(x.x), fabsf(x.y)};
-  const f32x2 d = ax * 0.23164189f + 1.0f;                 // 1 + (0.3275911/sqrt2) |x|
-  const f32x2 t = {__builtin_amdgcn_rcpf(d.x), __builtin_amdgcn_rcpf(d.y)};
-  const f32x2 a = (x * x) * -0.72134752f;                  // -x^2 log2(e) / 2
-  const f32x2 e = {__builtin_amdgcn_exp2f(a.x), __builtin_amdgcn_exp2f(a.y)};
-  f32x2 p = t * 1.061405429f - 1.453152027f;
-  p = p * t + 1.421413741f;
-  p = p * t - 0.284496736f;
-  p = p * t + 0.254829592f;
-  const f32x2 q = 1.0f - (p * t) * e;
-  return (ax * q + x) * 0.5f;
+__device__ __forceinline__ float gelu_rat(float x) {
+  const float c = __builtin_amdgcn_fmed3f(x, -5.5f, 5.5f);
+  const float s = c * c;
+  float pn = __builtin_fmaf(s, -1.0374993308914782e-07f, 4.8630190576659516e-05f);
+  pn = __builtin_fmaf(pn, s, 0.004202467855066061f);
+  pn = __builtin_fmaf(pn, s, 0.028525715693831444f);
+  pn = __builtin_fmaf(pn, s, 0.39895108342170715f);
+  float qd = __builtin_fmaf(s, 0.001403174945153296f, 0.02511732093989849f);
+  qd = __builtin_fmaf(qd, s, 0.2382698804140091f);
+  qd = __builtin_fmaf(qd, s, 1.0f);
+  const float phi = __builtin_fmaf(c * pn, __builtin_amdgcn_rcpf(qd), 0.5f);
+  return x * phi;
 }
+__device__ __forceinline__ f32x2 gelu_erf_x2(f32x2 x) { return f32x2{gelu_rat(x.x), gelu_rat(x.y)}; }
 
 template <int N>
 __device__ __forceinline__ void wait_vm() {
@@ -58,7 +61,8 @@ struct EpiGeom {
   static constexpr int NPS = 32 / RPP;    // passes per slab
 };
 
-template <int BM, int BN, int WM, int WN, int MF, typename accv, int TI, int TJ, int PRE = 0>
+// NOSTORE (probe builds only): every value is computed but (almost) never stored
+template <int BM, int BN, int WM, int WN, int MF, typename accv, int TI, int TJ, int PRE = 0, bool NOSTORE = false>
 __device__ __forceinline__ void gemm_epilogue(const GemmParams& p, accv (&acc)[TI][TJ], f16* smem, int m0, int n0,
                                               int wm, int wn, int wave, int lane,
                                               const half8 (*rpre)[EpiGeom<BM, BN, WM, WN>::NPS] = nullptr,
@@ -186,7 +190,7 @@ __device__ __forceinline__ void gemm_epilogue(const GemmParams& p, accv (&acc)[T
 #pragma unroll
         for (int q = 0; q < 8; ++q) v[q] = (v[q] * 0.5f) * (1.0f + erff(v[q] * 0.70710678118654752f));
       }
-      if (row < M) {
+      if (row < M && (!NOSTORE || v[0] == 1234.5f)) {
         const size_t base = (size_t)row * N + col0;
         if (p.C16) {
           half8 h;

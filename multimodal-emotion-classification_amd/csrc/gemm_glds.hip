@@ -281,6 +281,146 @@ __global__ __launch_bounds__(64 * WM * WN, (WM * WN == 4) ? 2 : 1) void gemm_gld
 
 
 
+// Epilogue of the ping-pong tile. Its MFMAs compute out^T = W . X^T, so a lane holds 4
+// consecutive output features of one token per 16x16 block (acc[ia][jb]: token block ia of the
+// wave's BM/2 rows, feature block jb of its 64 columns): the LDS staging writes are whole 8-B
+// (f16) / 16-B (f32) vectors instead of single floats, and every wave stages and stores its own
+// region (no workgroup barrier). Same expressions and order as gemm_epilogue, so the same bits:
+// ((acc + bias) + residual') -> act -> f16 / f32, residual' = R, or the deferred LayerNorm
+// fma((R - mean) rstd, g, b), or +0.
+//   * no residual, f16 out only (BERT FFN1, ResNet 1x1): bias, act and the f16 rounding happen
+//     in registers; the wave's f16 region (BM/2 rows x 128 B, 16-B chunk x of row r at
+//     x ^ ((r >> 1) & 7)) is then stored as whole 128-B row segments;
+//   * otherwise (BERT FFN2): (acc + bias) in f32 slabs of 32 rows x 256 B per wave (chunk x of row
+//     r at x ^ (r & 15)); each slab's residual loads are all issued before any is consumed.
+// NOSTORE (probe builds only): everything computed, (almost) nothing stored.
+template <int BM, bool NOSTORE = false, int ACT = -1>
+__device__ __forceinline__ void pp_epilogue(const GemmParams& p, floatx4 (&acc)[BM / 32][4], char* smem, int m0,
+                                            int n0, int wm, int wn, int tid, int lane) {
+  constexpr int HB = BM / 2;    // rows per wave
+  constexpr int NIA = BM / 32;  // 16-row token blocks per wave
+  const int M = p.M, N = p.N;
+  const int l16 = lane & 15, q = lane >> 4;
+  const int wave = tid >> 6;
+  const int rw0 = m0 + wm * HB, cw0 = n0 + wn * 64;  // the wave's first row / column
+  char* reg = smem + wave * (HB * 128 > 8192 ? HB * 128 : 8192);
+  float4 bb[4];
+#pragma unroll
+  for (int jb = 0; jb < 4; ++jb)
+    bb[jb] = p.bias ? *reinterpret_cast<const float4*>(p.bias + cw0 + jb * 16 + 4 * q)
+                    : make_float4(0.f, 0.f, 0.f, 0.f);
+  const int act = ACT >= 0 ? ACT : p.act;  // compile-time where the launch knows it
+  auto act4 = [&](float (&v)[4]) {
+    if (act == ACT_RELU) {
+#pragma unroll
+      for (int e = 0; e < 4; ++e) v[e] = fmaxf(v[e], 0.f);
+    } else if (act == ACT_RELU6) {
+#pragma unroll
+      for (int e = 0; e < 4; ++e) v[e] = fminf(fmaxf(v[e], 0.f), 6.f);
+    } else if (act == ACT_GELU) {
+#pragma unroll
+      for (int e = 0; e < 4; e += 2) {
+        const f32x2 r = gelu_erf_x2(f32x2{v[e], v[e + 1]});
+        v[e] = r.x;
+        v[e + 1] = r.y;
+      }
+    } else if (act == ACT_GELU_EXACT) {
+#pragma unroll
+      for (int e = 0; e < 4; ++e) v[e] = (v[e] * 0.5f) * (1.0f + erff(v[e] * 0.70710678118654752f));
+    }
+  };
+  if (!p.R && p.C16 && !p.C32) {
+#pragma unroll
+    for (int ia = 0; ia < NIA; ++ia)
+#pragma unroll
+      for (int jb = 0; jb < 4; ++jb) {
+        float v[4] = {acc[ia][jb][0] + bb[jb].x, acc[ia][jb][1] + bb[jb].y, acc[ia][jb][2] + bb[jb].z,
+                      acc[ia][jb][3] + bb[jb].w};
+#pragma unroll
+        for (int e = 0; e < 4; ++e) v[e] += 0.f;  // gemm_epilogue's "+ residual" with none: -0 -> +0
+        act4(v);
+        half4 h;
+#pragma unroll
+        for (int e = 0; e < 4; ++e) h[e] = (f16)v[e];
+        const int r = ia * 16 + l16, x = jb * 2 + (q >> 1);
+        *reinterpret_cast<half4*>(reg + r * 128 + ((x ^ ((r >> 1) & 7)) << 4) + (q & 1) * 8) = h;
+      }
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+#pragma unroll
+    for (int it = 0; it < HB / 8; ++it) {
+      const int r = it * 8 + (lane >> 3), x = lane & 7;
+      const uint4 v = *reinterpret_cast<const uint4*>(reg + r * 128 + ((x ^ ((r >> 1) & 7)) << 4));
+      if (rw0 + r < M && (!NOSTORE || v.x == 0x12345678u))
+        *reinterpret_cast<uint4*>(p.C16 + (size_t)(rw0 + r) * N + cw0 + x * 8) = v;
+    }
+    return;
+  }
+  // f32 slabs: lane -> row (lane >> 4) of each 4-row group, 16-B chunk (lane & 15) = 4 features
+  const int sc = lane & 15, col = cw0 + sc * 4;
+  float4 g4 = make_float4(0.f, 0.f, 0.f, 0.f), b4 = g4;
+  if (p.r_stats) {
+    g4 = *reinterpret_cast<const float4*>(p.r_g + col);
+    b4 = *reinterpret_cast<const float4*>(p.r_b + col);
+  }
+#pragma unroll
+  for (int sl = 0; sl < HB / 32; ++sl) {
+#pragma unroll
+    for (int a = 0; a < 2; ++a)
+#pragma unroll
+      for (int jb = 0; jb < 4; ++jb) {
+        const int ia = sl * 2 + a;
+        const float4 v = make_float4(acc[ia][jb][0] + bb[jb].x, acc[ia][jb][1] + bb[jb].y,
+                                     acc[ia][jb][2] + bb[jb].z, acc[ia][jb][3] + bb[jb].w);
+        const int r = a * 16 + l16, x = jb * 4 + q;
+        *reinterpret_cast<float4*>(reg + r * 256 + ((x ^ (r & 15)) << 4)) = v;
+      }
+    float rv[8][4];
+#pragma unroll
+    for (int it = 0; it < 8; ++it) {
+      const int rowc = min(rw0 + sl * 32 + it * 4 + (lane >> 4), M - 1);
+      const size_t base = (size_t)rowc * N + col;
+#pragma unroll
+      for (int e = 0; e < 4; ++e) rv[it][e] = 0.f;
+      if (p.R) {
+        if (p.r_f32) {
+          const float4 r4 = *reinterpret_cast<const float4*>(reinterpret_cast<const float*>(p.R) + base);
+          rv[it][0] = r4.x; rv[it][1] = r4.y; rv[it][2] = r4.z; rv[it][3] = r4.w;
+          if (p.r_stats) {
+            const float2 st = p.r_stats[rowc];
+            rv[it][0] = __builtin_fmaf((rv[it][0] - st.x) * st.y, g4.x, b4.x);
+            rv[it][1] = __builtin_fmaf((rv[it][1] - st.x) * st.y, g4.y, b4.y);
+            rv[it][2] = __builtin_fmaf((rv[it][2] - st.x) * st.y, g4.z, b4.z);
+            rv[it][3] = __builtin_fmaf((rv[it][3] - st.x) * st.y, g4.w, b4.w);
+          }
+        } else {
+          const half4 r4 = *reinterpret_cast<const half4*>(reinterpret_cast<const f16*>(p.R) + base);
+#pragma unroll
+          for (int e = 0; e < 4; ++e) rv[it][e] = (float)r4[e];
+        }
+      }
+    }
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+#pragma unroll
+    for (int it = 0; it < 8; ++it) {
+      const int r = it * 4 + (lane >> 4), row = rw0 + sl * 32 + r;
+      const float4 sv = *reinterpret_cast<const float4*>(reg + r * 256 + ((sc ^ (r & 15)) << 4));
+      float v[4] = {sv.x + rv[it][0], sv.y + rv[it][1], sv.z + rv[it][2], sv.w + rv[it][3]};
+      act4(v);
+      if (row < M && (!NOSTORE || v[0] == 1234.5f)) {
+        const size_t base = (size_t)row * N + col;
+        if (p.C16) {
+          half4 h;
+#pragma unroll
+          for (int e = 0; e < 4; ++e) h[e] = (f16)v[e];
+          *reinterpret_cast<half4*>(p.C16 + base) = h;
+        }
+        if (p.C32) *reinterpret_cast<float4*>(p.C32 + base) = make_float4(v[0], v[1], v[2], v[3]);
+      }
+    }
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+  }
+}
+
 // ---- 256x256x64 ping-pong GEMM (A_PLAIN), v_mfma_f32_16x16x32_f16, 8 waves (2 x 4).
 // Each K tile lives in one of two LDS buffers as four 16-KB pieces: A0/A1 = the 64-row
 // halves of both wave rows' 128-row strips, B0/B1 = the 32-column halves of the four wave
@@ -295,8 +435,9 @@ __global__ __launch_bounds__(64 * WM * WN, (WM * WN == 4) ? 2 : 1) void gemm_gld
 // pieces issued for tile t+2 has landed, i.e. all of tile t+1, read one phase later.
 // Same k order per output as every other tile, so results are bit-identical to them.
 // DBG = 4 (probe build, tools/pp_trace.py): s_memtime at four points of every phase of the
-// first 12 K tiles, per wave, kept in spare LDS and dumped by one block into C32.
-template <int AM, int DBG = 0, int BM = 256>
+// first 12 K tiles, per wave, kept in spare LDS and dumped by one block into C32. DBG = 5
+// (probe): the epilogue computes everything but stores nothing.
+template <int AM, int DBG = 0, int BM = 256, int ACT = -1>
 __global__ __launch_bounds__(512) void gemm_pp_kernel(const GemmParams p) {
   static_assert(AM == A_PLAIN, "ping-pong tile: plain A only");
   static_assert(BM == 256 || BM == 128, "BM");
@@ -420,7 +561,7 @@ __global__ __launch_bounds__(512) void gemm_pp_kernel(const GemmParams p) {
 #pragma unroll
         for (int j = 0; j < 2; ++j)
           acc[qa * QI + i][qb * 2 + j] =
-              __builtin_amdgcn_mfma_f32_16x16x32_f16(af[k][i], bf[k][j], acc[qa * QI + i][qb * 2 + j], 0, 0, 0);
+              __builtin_amdgcn_mfma_f32_16x16x32_f16(bf[k][j], af[k][i], acc[qa * QI + i][qb * 2 + j], 0, 0, 0);
     __builtin_amdgcn_s_setprio(0);
     __builtin_amdgcn_sched_barrier(0);
     tmark();
@@ -493,7 +634,7 @@ __global__ __launch_bounds__(512) void gemm_pp_kernel(const GemmParams p) {
     if (s == 12345.678f) p.C32[0] = s;
     return;
   }
-  gemm_epilogue<BM, BN, WM, WN, 16>(p, acc, smem, m0, n0, wm, wn, wave, lane);
+  pp_epilogue<BM, DBG == 5, ACT>(p, acc, reinterpret_cast<char*>(smem), m0, n0, wm, wn, tid, lane);
 }
 
 // BM=256 tiles: (BN, WM, WN, NS)
@@ -584,16 +725,34 @@ static int launch_bn(const GemmParams& p, hipStream_t s, int id) {
       const int dbg = opt().gemm_debug;
       if (id == 40256 && dbg == 4)
         hipLaunchKernelGGL((gemm_pp_kernel<A_PLAIN, 4, 256>), grd, blk, 0, s, p);
+      else if (id == 40256 && dbg == 5 && p.act == ACT_GELU)
+        hipLaunchKernelGGL((gemm_pp_kernel<A_PLAIN, 5, 256, ACT_GELU>), grd, blk, 0, s, p);
+      else if (id == 40256 && dbg == 5)
+        hipLaunchKernelGGL((gemm_pp_kernel<A_PLAIN, 5, 256>), grd, blk, 0, s, p);
       else if (id == 40256 && dbg == 2)
         hipLaunchKernelGGL((gemm_pp_kernel<A_PLAIN, 2, 256>), grd, blk, 0, s, p);
       else if (dbg == 2)
         hipLaunchKernelGGL((gemm_pp_kernel<A_PLAIN, 2, 128>), grd, blk, 0, s, p);
       else
 #endif
-      if (id == 40256)
-        hipLaunchKernelGGL((gemm_pp_kernel<A_PLAIN, 0, 256>), grd, blk, 0, s, p);
-      else
-        hipLaunchKernelGGL((gemm_pp_kernel<A_PLAIN, 0, 128>), grd, blk, 0, s, p);
+      // the activation is a template argument for the common cases: one epilogue path per kernel
+      if (id == 40256) {
+        if (p.act == ACT_GELU)
+          hipLaunchKernelGGL((gemm_pp_kernel<A_PLAIN, 0, 256, ACT_GELU>), grd, blk, 0, s, p);
+        else if (p.act == ACT_RELU)
+          hipLaunchKernelGGL((gemm_pp_kernel<A_PLAIN, 0, 256, ACT_RELU>), grd, blk, 0, s, p);
+        else if (p.act == ACT_NONE)
+          hipLaunchKernelGGL((gemm_pp_kernel<A_PLAIN, 0, 256, ACT_NONE>), grd, blk, 0, s, p);
+        else
+          hipLaunchKernelGGL((gemm_pp_kernel<A_PLAIN, 0, 256>), grd, blk, 0, s, p);
+      } else {
+        if (p.act == ACT_RELU)
+          hipLaunchKernelGGL((gemm_pp_kernel<A_PLAIN, 0, 128, ACT_RELU>), grd, blk, 0, s, p);
+        else if (p.act == ACT_NONE)
+          hipLaunchKernelGGL((gemm_pp_kernel<A_PLAIN, 0, 128, ACT_NONE>), grd, blk, 0, s, p);
+        else
+          hipLaunchKernelGGL((gemm_pp_kernel<A_PLAIN, 0, 128>), grd, blk, 0, s, p);
+      }
       MEC_LAUNCH_CHECK();
       return 0;
     }

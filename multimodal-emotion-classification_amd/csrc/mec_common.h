@@ -178,7 +178,7 @@ struct BlobReader {
 // C[M,N] = epilogue( A'[M,K] . B[N,K]^T ), A' = A (plain) or the im2col view of an NHWC
 // tensor (conv).
 enum AMode : int { A_PLAIN = 0, A_CONV = 1, A_DUAL = 2 };
-// ACT_GELU: the packed A&S erf form (f16 path, |err| <= 2.1e-7); ACT_GELU_EXACT: libm erff,
+// ACT_GELU: a (4, 3) rational Phi (f16 path, gemm_common.h gelu_rat); ACT_GELU_EXACT: libm erff,
 // x * 0.5 * (1 + erf(x / sqrt2)) as torch's CPU gelu kernel orders it (fp32 path)
 enum Act : int { ACT_NONE = 0, ACT_RELU = 1, ACT_GELU = 2, ACT_RELU6 = 3, ACT_GELU_EXACT = 4 };
 

@@ -90,7 +90,7 @@ def test_option_validation_without_gpu():
     only sets the process defaults, so this runs without a GPU. Defaults restored."""
     lib = _lib.load()
     assert lib.mec_build_flags() == 0, 'the product library must not be a probe build'
-    probes = [(b'gemm_debug', 1), (b'gemm_debug', 2), (b'gemm_debug', 4), (b'stem_debug', 1), (b'conv3x3_debug', 2),
+    probes = [(b'gemm_debug', 1), (b'gemm_debug', 2), (b'gemm_debug', 4), (b'gemm_debug', 5), (b'stem_debug', 1), (b'conv3x3_debug', 2),
               (b'bert_qkv_attn', 2), (b'bert_qkv_attn', 3), (b'bert_oproj_ln', 2), (b'bert_oproj_ln', 4),
               (b'speech_debug', 1), (b'audio_debug', 15)]
     for k, v in probes:
@@ -104,7 +104,7 @@ def test_option_validation_without_gpu():
           (b'speech_impl', 1), (b'speech_impl', 0), (b'speech_debug', 0)]
     bad = [(b'gemm_f32_tile', 9), (b'fusion_r', 3), (b'fusion_split', 2), (b'bert_qkv_attn', 4), (b'bert_oproj_ln', 5), (b'gemm_bn', 12345),
            (b'gemm_bn', 42256), (b'gemm_bn_tag', 11128), (b'gemm_bn_tag', 15 * 100000 + 256),
-           (b'gemm_bn_tag', 3 * 100000 + 999), (b'gemm_bn_tag', -1), (b'gemm_debug', 5), (b'speech_impl', 2)]
+           (b'gemm_bn_tag', 3 * 100000 + 999), (b'gemm_bn_tag', -1), (b'gemm_debug', 6), (b'speech_impl', 2)]
     try:
         for k, v in ok:
             assert lib.mec_set_option(k, v) == 0, (k, v)
