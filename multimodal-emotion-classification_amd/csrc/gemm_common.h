@@ -62,7 +62,9 @@ struct EpiGeom {
 };
 
 // NOSTORE (probe builds only): every value is computed but (almost) never stored
-template <int BM, int BN, int WM, int WN, int MF, typename accv, int TI, int TJ, int PRE = 0, bool NOSTORE = false>
+// ACT >= 0: the activation as a compile-time constant (one epilogue path per kernel)
+template <int BM, int BN, int WM, int WN, int MF, typename accv, int TI, int TJ, int PRE = 0, bool NOSTORE = false,
+          int ACT = -1>
 __device__ __forceinline__ void gemm_epilogue(const GemmParams& p, accv (&acc)[TI][TJ], f16* smem, int m0, int n0,
                                               int wm, int wn, int wave, int lane,
                                               const half8 (*rpre)[EpiGeom<BM, BN, WM, WN>::NPS] = nullptr,
@@ -173,20 +175,21 @@ __device__ __forceinline__ void gemm_epilogue(const GemmParams& p, accv (&acc)[T
       v[4] = x1.x + bias[4]; v[5] = x1.y + bias[5]; v[6] = x1.z + bias[6]; v[7] = x1.w + bias[7];
 #pragma unroll
       for (int q = 0; q < 8; ++q) v[q] += rv[ps][q];
-      if (p.act == ACT_RELU) {
+      const int act = ACT >= 0 ? ACT : p.act;
+      if (act == ACT_RELU) {
 #pragma unroll
         for (int q = 0; q < 8; ++q) v[q] = fmaxf(v[q], 0.f);
-      } else if (p.act == ACT_RELU6) {
+      } else if (act == ACT_RELU6) {
 #pragma unroll
         for (int q = 0; q < 8; ++q) v[q] = fminf(fmaxf(v[q], 0.f), 6.f);
-      } else if (p.act == ACT_GELU) {
+      } else if (act == ACT_GELU) {
 #pragma unroll
         for (int q = 0; q < 8; q += 2) {
           const f32x2 r = gelu_erf_x2(f32x2{v[q], v[q + 1]});
           v[q] = r.x;
           v[q + 1] = r.y;
         }
-      } else if (p.act == ACT_GELU_EXACT) {
+      } else if (act == ACT_GELU_EXACT) {
 #pragma unroll
         for (int q = 0; q < 8; ++q) v[q] = (v[q] * 0.5f) * (1.0f + erff(v[q] * 0.70710678118654752f));
       }

@@ -29,7 +29,8 @@ namespace mec {
 
 __device__ __attribute__((aligned(64))) uint4 g_zero_page[16];
 
-template <int BM, int BN, int WM, int WN, int NS, int AM, int DBG = 0, int MF = 32, int BK = 64, int PRE = 0>
+template <int BM, int BN, int WM, int WN, int NS, int AM, int DBG = 0, int MF = 32, int BK = 64, int PRE = 0,
+          int ACT = -1>
 __global__ __launch_bounds__(64 * WM * WN, (WM * WN == 4) ? 2 : 1) void gemm_glds_kernel(const GemmParams p) {
   // MF: 32 = v_mfma_f32_32x32x16_f16 tiles, 16 = v_mfma_f32_16x16x32_f16 tiles
   // DBG (probe builds only): 1 = no operand loads inside the K loop, 2 = no epilogue
@@ -276,7 +277,8 @@ __global__ __launch_bounds__(64 * WM * WN, (WM * WN == 4) ? 2 : 1) void gemm_gld
     if (s == 12345.678f) p.C32[0] = s;  // keeps the accumulators live
     return;
   }
-  gemm_epilogue<BM, BN, WM, WN, MF, accv, TI, TJ, PRE>(p, acc, smem, m0, n0, wm, wn, wave, lane, rpre, rpre32);
+  gemm_epilogue<BM, BN, WM, WN, MF, accv, TI, TJ, PRE, false, ACT>(p, acc, smem, m0, n0, wm, wn, wave, lane, rpre,
+                                                                   rpre32);
 }
 
 
@@ -639,6 +641,24 @@ __global__ __launch_bounds__(512) void gemm_pp_kernel(const GemmParams p) {
 
 // BM=256 tiles: (BN, WM, WN, NS)
 
+template <int BM, int BN, int WM, int WN, int NS, int MF, int BK, int ACT>
+static int launch_cfg_act(const GemmParams& p, hipStream_t s, int nwg, dim3 blk) {
+  if (BM * BN <= 128 * 128 && opt().gemm_prefetch_r && p.amode == A_PLAIN && p.R && !p.r_f32 && p.K <= 512) {
+    // f16 residual prefetch for ResNet's short-K conv3 GEMMs (small tiles only: no spills);
+    // 225 -> 170 us on layer1's conv3. The f32 form (PRE = 2, BERT's O-projection, K = 768)
+    // measured 10-15% slower than no prefetch, so it is not dispatched.
+    if constexpr (BM * BN <= 128 * 128)
+      hipLaunchKernelGGL((gemm_glds_kernel<BM, BN, WM, WN, NS, A_PLAIN, 0, MF, BK, 1, ACT>), dim3(nwg), blk, 0, s, p);
+  } else if (p.amode == A_PLAIN)
+    hipLaunchKernelGGL((gemm_glds_kernel<BM, BN, WM, WN, NS, A_PLAIN, 0, MF, BK, 0, ACT>), dim3(nwg), blk, 0, s, p);
+  else if (p.amode == A_DUAL)
+    hipLaunchKernelGGL((gemm_glds_kernel<BM, BN, WM, WN, NS, A_DUAL, 0, MF, BK, 0, ACT>), dim3(nwg), blk, 0, s, p);
+  else
+    hipLaunchKernelGGL((gemm_glds_kernel<BM, BN, WM, WN, NS, A_CONV, 0, MF, BK, 0, ACT>), dim3(nwg), blk, 0, s, p);
+  MEC_LAUNCH_CHECK();
+  return 0;
+}
+
 template <int BM, int BN, int WM, int WN, int NS, int MF = 32, int BK = 64>
 static int launch_cfg(const GemmParams& p, hipStream_t s) {
   const int nwg = ((p.M + BM - 1) / BM) * (p.N / BN);
@@ -653,20 +673,10 @@ static int launch_cfg(const GemmParams& p, hipStream_t s) {
     return 0;
   }
 #endif
-  if (BM * BN <= 128 * 128 && opt().gemm_prefetch_r && p.amode == A_PLAIN && p.R && !p.r_f32 && p.K <= 512) {
-    // f16 residual prefetch for ResNet's short-K conv3 GEMMs (small tiles only: no spills);
-    // 225 -> 170 us on layer1's conv3. The f32 form (PRE = 2, BERT's O-projection, K = 768)
-    // measured 10-15% slower than no prefetch, so it is not dispatched.
-    if constexpr (BM * BN <= 128 * 128)
-      hipLaunchKernelGGL((gemm_glds_kernel<BM, BN, WM, WN, NS, A_PLAIN, 0, MF, BK, 1>), dim3(nwg), blk, 0, s, p);
-  } else if (p.amode == A_PLAIN)
-    hipLaunchKernelGGL((gemm_glds_kernel<BM, BN, WM, WN, NS, A_PLAIN, 0, MF, BK>), dim3(nwg), blk, 0, s, p);
-  else if (p.amode == A_DUAL)
-    hipLaunchKernelGGL((gemm_glds_kernel<BM, BN, WM, WN, NS, A_DUAL, 0, MF, BK>), dim3(nwg), blk, 0, s, p);
-  else
-    hipLaunchKernelGGL((gemm_glds_kernel<BM, BN, WM, WN, NS, A_CONV, 0, MF, BK>), dim3(nwg), blk, 0, s, p);
-  MEC_LAUNCH_CHECK();
-  return 0;
+  // the activation is a template argument for ReLU (ResNet) and none (BERT O-proj); others runtime
+  if (p.act == ACT_RELU) return launch_cfg_act<BM, BN, WM, WN, NS, MF, BK, ACT_RELU>(p, s, nwg, blk);
+  if (p.act == ACT_NONE) return launch_cfg_act<BM, BN, WM, WN, NS, MF, BK, ACT_NONE>(p, s, nwg, blk);
+  return launch_cfg_act<BM, BN, WM, WN, NS, MF, BK, -1>(p, s, nwg, blk);
 }
 
 // Tile-width choice. Every BN computes each output with the same k-ordered MFMA chain, so
