@@ -277,6 +277,7 @@ int set_option(Options& o, const std::string& k, int value) {
   if (k == "mbv2_impl" && value >= 0 && value <= 2) { o.mbv2_impl = value; return 0; }
   if (k == "conv3x3_direct" && (value == 0 || value == 1)) { o.conv3x3_direct = value; return 0; }
   if (k == "conv3x3_halo" && (value == 0 || value == 1)) { o.conv3x3_halo = value; return 0; }
+  if (k == "stem_gray_f32" && (value == 0 || value == 1)) { o.stem_gray_f32 = value; return 0; }
   if (k == "resnet_chunk" && value >= 0) { o.resnet_chunk = value; return 0; }
   if (k == "bert_qkv_attn" && (value == 0 || value == 1 || (probe && (value == 2 || value == 3)))) {
     o.bert_qkv_attn = value;

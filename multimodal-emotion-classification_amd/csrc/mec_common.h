@@ -83,6 +83,7 @@ struct Options {
   int gemm_bn_tag[TAG_COUNT] = {0, 0, 0, /*TAG_BERT_OPROJ*/ 11128};
   int conv3x3_direct = 1;   // ResNet layer1 conv2 on the halo-tile kernel (conv3x3.hip)
   int conv3x3_halo = 1;     // layers 2-3 stride-1 conv2 on the halo kernel (conv3x3_halo.hip)
+  int stem_gray_f32 = 1;    // fp32 gray stem as one conv + pool kernel (else im2col + GEMM + pool)
   int resnet_fused_tail = 0;
   int resnet_chunk = 0;
   int pw_chain = 2;         // layer1 seam kernels (pw_chain.hip)

@@ -118,6 +118,7 @@ struct ImageModel : ImageNet {
   // fp32 path (resnet_f32.hip): f32 weights, same [Cout][kh][kw][Cin] layout; the stem is a
   // [64][160] GEMM over an explicit im2col of the normalized image (k = c*49 + kh*7 + kw)
   DevBuf wts32;
+  size_t stem_gray32_off = 0;  // f32 [49][2][64]: gray-input stem folded to (pixel, inside) taps
   int create(const float* blob, size_t n);
   int create_f32(const float* blob, size_t n);
   int forward_u8(const uint8_t* img, int B, int H, int W, int C, float* feat, float* logits, float* probs,

@@ -1,10 +1,12 @@
 // ResNet50 image path in fp32 end to end (mec_create_ex(..., MEC_PREC_FP32)), the reference's
 // own precision (inference/image_inference.py:28-32 transform, :55-65 network + head):
 //   resize      PIL-exact u8 bilinear 48 -> 224 (resnet.hip, shared with the f16 path)
-//   stem        explicit im2col of ToTensor + Normalize (x / 255 - mean) / std, exactly as
+//   stem, gray  (the FER path: convert('RGB') replicates the channel) conv 7x7/2 + BN + ReLU +
+//               maxpool 3x3/2 in one kernel, stem_pool_gray_f32_kernel (below)
+//   stem, RGB   explicit im2col of ToTensor + Normalize (x / 255 - mean) / std, exactly as
 //               torchvision computes it, k = c*49 + kh*7 + kw (the torch weight order), K
-//               padded 147 -> 160; then one fp32 GEMM [B*112*112, 160] x [64, 160]^T + BN + ReLU
-//   maxpool     3x3/2 pad 1, NHWC f32
+//               padded 147 -> 160; then one fp32 GEMM [B*112*112, 160] x [64, 160]^T + BN + ReLU;
+//               maxpool 3x3/2 pad 1, NHWC f32
 //   bottlenecks conv1 / conv2 (3x3, stride on the 3x3: v1.5) / conv3 + residual (identity or
 //               the 1x1/s downsample GEMM) + ReLU, all on gemm_f32 (A_PLAIN / A_CONV), BN
 //               folded into f32 weights and bias
@@ -78,6 +80,133 @@ __global__ __launch_bounds__(256) void maxpool_f32_kernel(const float* __restric
   *reinterpret_cast<float4*>(y + idx * 4) = m;
 }
 
+// Stem of a gray image (the FER path), fp32. With the channel replicated to RGB and
+// Normalize affine, conv(Normalize(x)) over the 3 channels of one 7x7 window is
+//   sum over in-image taps t of ( px_t Wg[t] + 1 . Wm[t] ),
+//   Wg[t] = sum_c W[c][t] / (255 std_c),   Wm[t] = -sum_c W[c][t] mean_c / std_c
+// (BN scale folded in; host-folded in float64), i.e. a 2-channel conv over (pixel, in-image
+// indicator): K = 49 taps x 2 = 98, exactly 49 steps of v_mfma_f32_32x32x2_f32 with the two
+// lane halves on the two channels, against 147 -> 160 taps of the im2col GEMM. The sums are
+// reassociated against torch's 3-channel conv (fp32 rounding, well inside the 1e-5 probs bar).
+// A persistent workgroup (8 waves, one per CU) walks tiles of 8 x 8 pooled outputs of one image:
+//   * the tile's 39 x 39 u8 input patch sits in LDS as (px, inside) float pairs; the next tile's
+//     patch is loaded into registers under this tile's MFMAs and written after its last read;
+//   * the 17 x 17 stem pixels it pools from (289 rows, 10 M-tiles of 32) x 64 channels (2 N-tiles)
+//     are 20 (M, N) tile pairs: wave w takes pairs w, w + 8, w + 16, so each SIMD's two waves
+//     carry 5; the folded weights [49][2][64] stay in LDS for the launch;
+//   * bias + ReLU -> the stem tile in LDS -> MaxPool2d(3, 2, 1) (stem pixels outside the
+//     112 x 112 map skipped, as padding -inf) -> float4 stores of [B, 56, 56, 64].
+// The im2col path it replaces wrote and re-read 2 GB at B = 256 (im2col 844 + GEMM 698 + pool
+// 207 us, profiles/r02_enc_fp32_image.txt).
+constexpr int SGF_P = 39, SGF_S = 17, SGF_NPIX = SGF_S * SGF_S;  // patch side, stem tile side, stem pixels
+constexpr int SGF_PL = (SGF_P * SGF_P + 511) / 512;              // patch entries per thread (3)
+
+__global__ __launch_bounds__(512, 1) void stem_pool_gray_f32_kernel(const uint8_t* __restrict__ img, int ntiles,
+                                                                   const float* __restrict__ wg,
+                                                                   const float* __restrict__ bias,
+                                                                   float* __restrict__ y) {
+  __shared__ float sw[49 * 2 * 64];                           // folded weights [tap][channel][co]
+  __shared__ __attribute__((aligned(16))) float2 patch[SGF_P * SGF_P];
+  __shared__ __attribute__((aligned(16))) float stg[SGF_NPIX * 64];  // ReLU'd stem tile [pixel][co]
+  const int tid = threadIdx.x, lane = tid & 63;
+  const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int li = lane & 31, kk = lane >> 5;
+  for (int i = tid; i < 49 * 2 * 64; i += 512) sw[i] = wg[i];
+  int base[3], nt[3];
+  float bv[3];
+#pragma unroll
+  for (int q = 0; q < 3; ++q) {  // pair w + 8q: M-tile (p >> 1), N-tile (p & 1)
+    const int pr = wave + 8 * q;
+    const int i = min((pr >> 1) * 32 + li, SGF_NPIX - 1);
+    const int sr = i / SGF_S, sc = i - (i / SGF_S) * SGF_S;
+    base[q] = 2 * sr * SGF_P + 2 * sc;  // patch slot of tap (0, 0) of the lane's stem pixel
+    nt[q] = pr & 1;
+    bv[q] = bias[nt[q] * 32 + li];
+  }
+  const int npair = wave < 4 ? 3 : 2;
+  const float* pf = reinterpret_cast<const float*>(patch);
+  // patch entries of tile t: (row, col) slots tid + 512 j; -1 = outside the image
+  auto patch_load = [&](int t, int (&v)[SGF_PL]) {
+    const int b = t / 49, tt = t - (t / 49) * 49;
+    const int r0 = 4 * (tt / 7) * 8 - 5, c0 = 4 * (tt - (tt / 7) * 7) * 8 - 5;
+#pragma unroll
+    for (int j = 0; j < SGF_PL; ++j) {
+      const int i = tid + 512 * j;
+      const int pr = i / SGF_P, pc = i - (i / SGF_P) * SGF_P;
+      const int ih = r0 + pr, iw = c0 + pc;
+      v[j] = (i < SGF_P * SGF_P && ih >= 0 && ih < 224 && iw >= 0 && iw < 224) ? (int)img[((size_t)b * 224 + ih) * 224 + iw]
+                                                                                : -1;
+    }
+  };
+  auto patch_store = [&](const int (&v)[SGF_PL]) {
+#pragma unroll
+    for (int j = 0; j < SGF_PL; ++j) {
+      const int i = tid + 512 * j;
+      if (i < SGF_P * SGF_P) patch[i] = v[j] >= 0 ? make_float2((float)v[j], 1.f) : make_float2(0.f, 0.f);
+    }
+  };
+  int pv[SGF_PL];
+  if (blockIdx.x < ntiles) {
+    patch_load(blockIdx.x, pv);
+    patch_store(pv);
+  }
+  for (int t = blockIdx.x; t < ntiles; t += gridDim.x) {
+    const int b = t / 49, tt = t - (t / 49) * 49;
+    const int py0 = (tt / 7) * 8, px0 = (tt - (tt / 7) * 7) * 8;
+    __syncthreads();  // this tile's patch and the weights are in LDS; the last pool read stg
+    const int tn = t + gridDim.x;
+    if (tn < ntiles) patch_load(tn, pv);  // lands under the MFMAs
+    floatx16 acc[3];
+#pragma unroll
+    for (int q = 0; q < 3; ++q)
+#pragma unroll
+      for (int e = 0; e < 16; ++e) acc[q][e] = 0.f;
+#pragma unroll 7
+    for (int st = 0; st < 49; ++st) {
+      const int kh = st / 7, kw = st - (st / 7) * 7;
+#pragma unroll
+      for (int q = 0; q < 3; ++q) {
+        if (q < npair) {
+          const float av = pf[(base[q] + kh * SGF_P + kw) * 2 + kk];
+          const float w = sw[(st * 2 + kk) * 64 + nt[q] * 32 + li];
+          acc[q] = __builtin_amdgcn_mfma_f32_32x32x2f32(av, w, acc[q], 0, 0, 0);
+        }
+      }
+    }
+    // D[row (e & 3) + 8 (e >> 2) + 4 kk][col li] of each 32 x 32 block: stem pixel x channel
+#pragma unroll
+    for (int q = 0; q < 3; ++q)
+      if (q < npair)
+#pragma unroll
+        for (int e = 0; e < 16; ++e) {
+          const int pix = ((wave + 8 * q) >> 1) * 32 + (e & 3) + 8 * (e >> 2) + 4 * kk;
+          if (pix < SGF_NPIX) stg[pix * 64 + nt[q] * 32 + li] = fmaxf(acc[q][e] + bv[q], 0.f);
+        }
+    __syncthreads();  // stg complete; every patch read of this tile done
+    if (tn < ntiles) patch_store(pv);
+    const float4* stg4 = reinterpret_cast<const float4*>(stg);
+#pragma unroll
+    for (int it = 0; it < 2; ++it) {  // 64 pooled pixels x 16 channel quads
+      const int idx = it * 512 + tid, pp = idx >> 4, cq = idx & 15;
+      const int py = pp >> 3, px = pp & 7;
+      float4 m = make_float4(-INFINITY, -INFINITY, -INFINITY, -INFINITY);
+#pragma unroll
+      for (int dy = 0; dy < 3; ++dy) {
+        const int sr = 2 * py + dy, R = 2 * py0 - 1 + sr;
+        if (R < 0 || R >= 112) continue;
+#pragma unroll
+        for (int dx = 0; dx < 3; ++dx) {
+          const int sc = 2 * px + dx, Cc = 2 * px0 - 1 + sc;
+          if (Cc < 0 || Cc >= 112) continue;
+          const float4 v = stg4[(sr * SGF_S + sc) * 16 + cq];
+          m.x = fmaxf(m.x, v.x); m.y = fmaxf(m.y, v.y); m.z = fmaxf(m.z, v.z); m.w = fmaxf(m.w, v.w);
+        }
+      }
+      *reinterpret_cast<float4*>(y + (((size_t)b * 56 + py0 + py) * 56 + px0 + px) * 64 + cq * 4) = m;
+    }
+  }
+}
+
 int ImageModel::create_f32(const float* blob, size_t n) {
   BlobReader rd(blob, n);
   std::vector<float> w;
@@ -123,6 +252,22 @@ int ImageModel::create_f32(const float* blob, size_t n) {
     if (rd.ok)
       for (int o = 0; o < 64; ++o)
         for (int k = 0; k < 147; ++k) w[stem.w_off + (size_t)o * STEM_K + k] = (float)((double)src[o * 147 + k] * scale[o]);
+    // gray-input fold (stem_pool_gray_f32_kernel): [49 taps][pixel, inside][64]
+    const double mean[3] = {0.485, 0.456, 0.406}, stdv[3] = {0.229, 0.224, 0.225};
+    stem_gray32_off = w.size();
+    w.resize(w.size() + 49 * 2 * 64, 0.f);
+    if (rd.ok)
+      for (int o = 0; o < 64; ++o)
+        for (int t = 0; t < 49; ++t) {
+          double g = 0.0, m = 0.0;
+          for (int c = 0; c < 3; ++c) {
+            const double wc = (double)src[o * 147 + c * 49 + t] * scale[o];
+            g += wc / (255.0 * stdv[c]);
+            m -= wc * mean[c] / stdv[c];
+          }
+          w[stem_gray32_off + ((size_t)t * 2 + 0) * 64 + o] = (float)g;
+          w[stem_gray32_off + ((size_t)t * 2 + 1) * 64 + o] = (float)m;
+        }
   }
   blocks.clear();
   int cin = 64;
@@ -195,22 +340,35 @@ int ImageModel::forward_f32(const uint8_t* img, int B, int H, int W, int C, floa
     Cin = 1;
   }
   MEC_TRY(prof.begin(TAG_RESNET_STEM, s));
-  {
-    const size_t total = (size_t)B * 112 * 112 * (STEM_K / 4);
-    hipLaunchKernelGGL(stem_im2col_f32_kernel, dim3((unsigned)((total + 255) / 256)), dim3(256), 0, s, stem_in, B, Cin,
-                       A0);
+  if (Cin == 1 && opt().stem_gray_f32) {  // conv + BN + ReLU + maxpool in one kernel -> X
+    static int ncu = 0;
+    if (!ncu) {
+      int dev = 0;
+      MEC_HIP(hipGetDevice(&dev));
+      MEC_HIP(hipDeviceGetAttribute(&ncu, hipDeviceAttributeMultiprocessorCount, dev));
+    }
+    const int ntiles = B * 49;
+    hipLaunchKernelGGL(stem_pool_gray_f32_kernel, dim3(std::min(ntiles, ncu)), dim3(512), 0, s, stem_in, ntiles,
+                       Wt + stem_gray32_off, P + stem.b_off, X);
     MEC_LAUNCH_CHECK();
-  }
-  MEC_TRY(prof.end(TAG_RESNET_STEM, s));
-  GemmParams g;
-  g.A = A0; g.B32 = Wt + stem.w_off; g.bias = P + stem.b_off; g.act = ACT_RELU; g.C32 = Y;
-  g.M = B * 112 * 112; g.N = 64; g.K = STEM_K;
-  MEC_TRY(launch_gemm_f32(g, s, &prof, TAG_RESNET_STEM));
-  {
+    MEC_TRY(prof.end(TAG_RESNET_STEM, s));
+  } else {
+    {
+      const size_t total = (size_t)B * 112 * 112 * (STEM_K / 4);
+      hipLaunchKernelGGL(stem_im2col_f32_kernel, dim3((unsigned)((total + 255) / 256)), dim3(256), 0, s, stem_in, B,
+                         Cin, A0);
+      MEC_LAUNCH_CHECK();
+    }
+    MEC_TRY(prof.end(TAG_RESNET_STEM, s));
+    GemmParams g;
+    g.A = A0; g.B32 = Wt + stem.w_off; g.bias = P + stem.b_off; g.act = ACT_RELU; g.C32 = Y;
+    g.M = B * 112 * 112; g.N = 64; g.K = STEM_K;
+    MEC_TRY(launch_gemm_f32(g, s, &prof, TAG_RESNET_STEM));
     const size_t total = (size_t)B * 56 * 56 * 16;
     hipLaunchKernelGGL(maxpool_f32_kernel, dim3((unsigned)((total + 255) / 256)), dim3(256), 0, s, Y, B, 112, 64, 56, X);
     MEC_LAUNCH_CHECK();
   }
+  GemmParams g;
   float* cur = X;
   float* other = Y;
   int Hc = 56;

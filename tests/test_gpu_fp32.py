@@ -173,6 +173,25 @@ def test_image_fp32_rgb_and_gray224(dev):
         assert agree == 2 and err <= FP32_PROB_TOL
 
 
+@pytest.mark.parametrize('B', [1, 7, 64])
+def test_image_fp32_gray_stem_matches_im2col(dev, B):
+    """The gray-input stem as one conv + BN + ReLU + max-pool kernel (stem_pool_gray_f32_kernel:
+    channels folded into (pixel, inside) taps) against the im2col GEMM + pool path it replaces:
+    the same network output to fp32 reassociation (B = 64: 3,136 tiles, several per CU)."""
+    gray = engine.to_device(syn.image_inputs(B, seed=90 + B), dev)
+    enc = engine.ImageEncoder(device=dev, precision='fp32')
+    outs = []
+    for v in (0, 1):
+        enc.set_option('stem_gray_f32', v)
+        outs.append(_np(enc.forward(gray)))
+    (f0, l0, p0), (f1, l1, p1) = outs
+    assert not np.isnan(f1).any()
+    ferr = float(np.abs(f1 - f0).max() / np.abs(f0).max())
+    perr = float(np.abs(p1 - p0).max())
+    print(f'gray stem vs im2col B={B}: feat rel {ferr:.3g}, probs max|d| {perr:.3g}')
+    assert ferr <= 1e-5 and perr <= 1e-6 and (p1.argmax(1) == p0.argmax(1)).all()
+
+
 def test_fused_fp32_end_to_end(dev):
     """Fused probs of the fp32 pipeline against the oracle chain o_f(o_s, o_t, o_i)
     (inference/multimodal_fusion.py:271-278), B = 24 with ragged text."""
