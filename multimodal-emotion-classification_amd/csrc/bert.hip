@@ -924,12 +924,8 @@ int TextModel::forward(const int32_t* ids, const int32_t* mask, int B, int L, fl
   const float* head = P + PRM_LAYER * BLAYERS;
   const float *WpT = head, *bp = WpT + (size_t)BH * BH, *WcT = bp + BH, *bc = WcT + (size_t)BH * 7;
   // pooler: tanh(cls . Wp^T + bp) over the batch (also copies the CLS feature out)
-  hipLaunchKernelGGL((linear_rows_kernel<8, 768>), dim3((B + 7) / 8, BH / 64), dim3(256), 0, s, h32, (size_t)L * BH, B,
-                     BH, WpT, bp, BH, 64, pooled, BH, (int)BACT_TANH, cls, BH);
-  MEC_LAUNCH_CHECK();
-  hipLaunchKernelGGL((head_softmax_kernel<8, 768>), dim3((B + 7) / 8), dim3(256), 0, s, pooled, B, BH, WcT, bc,
-                     logits, probs);
-  MEC_LAUNCH_CHECK();
+  MEC_TRY(launch_linear_mfma<BACT_TANH>(h32, (size_t)L * BH, B, BH, WpT, bp, BH, pooled, BH, cls, BH, s));
+  MEC_TRY(launch_head7(pooled, B, BH, WcT, bc, logits, probs, s));
   return 0;
 }
 

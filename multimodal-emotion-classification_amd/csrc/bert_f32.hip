@@ -171,12 +171,8 @@ int TextModel::forward_f32(const int32_t* ids, const int32_t* mask, int B, int L
   }
   const float* head = P + PRM_LAYER * NL;
   const float *WpT = head, *bp = WpT + (size_t)H * H, *WcT = bp + H, *bc = WcT + (size_t)H * 7;
-  hipLaunchKernelGGL((linear_rows_kernel<8, 768>), dim3((B + 7) / 8, H / 64), dim3(256), 0, s, h32, (size_t)L * H, B,
-                     H, WpT, bp, H, 64, pooled, H, (int)BACT_TANH, cls, H);
-  MEC_LAUNCH_CHECK();
-  hipLaunchKernelGGL((head_softmax_kernel<8, 768>), dim3((B + 7) / 8), dim3(256), 0, s, pooled, B, H, WcT, bc, logits,
-                     probs);
-  MEC_LAUNCH_CHECK();
+  MEC_TRY(launch_linear_mfma<BACT_TANH>(h32, (size_t)L * H, B, H, WpT, bp, H, pooled, H, cls, H, s));
+  MEC_TRY(launch_head7(pooled, B, H, WcT, bc, logits, probs, s));
   return 0;
 }
 

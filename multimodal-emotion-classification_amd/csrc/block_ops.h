@@ -235,6 +235,152 @@ __global__ __launch_bounds__(256) void linear_rows_kernel(const float* __restric
   }
 }
 
+// Batched fp32 linear for the encoder heads (ResNet fc[1] 2048->512, MobileNetV2
+// classifier[1] 1280->512, BERT pooler 768->768) on v_mfma_f32_16x16x4f32 (exact f32 products,
+// f32 accumulate, MI355X_MICROARCH.md):
+//   Y[b, n] = act(X[b, :] . Wt[:, n] + bias[n]),   Wt [K][N] (N contiguous), X rows ldx apart.
+// Grid (ceil(B/32), N/16), 512 threads: a workgroup owns 32 rows x 16 columns and its eight
+// waves split K in eighths of NG 16-deep k groups (K = 128 NG). A lane issues every load of
+// its K range before the first MFMA (one memory round trip per wave): per k group one float4
+// of each of its two rows (k = 16t + 4q .. +3, q = lane >> 4) and the four matching weights,
+// then 2 x 4 MFMAs per group (the k order inside a group is permuted the same way for A and
+// B, so the sum covers the same terms). The eighths are added in a fixed order through LDS,
+// so a row's result never depends on B or on its position in the batch. At B = 256 the grid
+// is 256-384 workgroups, two waves per SIMD: the f32 MFMA time is ~3.4 us for ResNet fc[1]
+// (537 MFLOP at 157 TF), where linear_rows_kernel (32 x N/64 workgroups, each re-reading a
+// 64-column weight slice) took 47 us alone and 179 us beside BERT
+// (profiles/r01_kernel_stats_bench_final4.txt). A first form with four waves and 4-group trips
+// (a memory round trip every 4 groups) measured 60 us.
+template <int ACT, int NG>
+__global__ __launch_bounds__(512) void linear_mfma_kernel(const float* __restrict__ X, size_t ldx, int B,
+                                                          const float* __restrict__ Wt,
+                                                          const float* __restrict__ bias, int N,
+                                                          float* __restrict__ Y, int ldy,
+                                                          float* __restrict__ Xcopy, int ldxc) {
+  constexpr int K = 128 * NG, KW = 16 * NG;  // K per wave
+  __shared__ __attribute__((aligned(16))) float red[8][32 * 16];
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int c16 = lane & 15, q = lane >> 4;
+  const int r0 = blockIdx.x * 32, n0 = blockIdx.y * 16;
+  const int kb = wave * KW;
+  const int ra = min(r0 + c16, B - 1), rb = min(r0 + 16 + c16, B - 1);
+  const float* xa = X + (size_t)ra * ldx + kb + 4 * q;
+  const float* xb = X + (size_t)rb * ldx + kb + 4 * q;
+  const float* w = Wt + (size_t)(kb + 4 * q) * N + n0 + c16;
+  floatx4 a0[NG], a1[NG];
+  float bw[NG][4];
+#pragma unroll
+  for (int g = 0; g < NG; ++g) {
+    a0[g] = *reinterpret_cast<const floatx4*>(xa + 16 * g);
+    a1[g] = *reinterpret_cast<const floatx4*>(xb + 16 * g);
+#pragma unroll
+    for (int j = 0; j < 4; ++j) bw[g][j] = w[(size_t)(16 * g + j) * N];
+  }
+  // one drain for all of them (left to itself, hipcc interleaves the loads with the MFMAs at
+  // 43 VGPRs and waits on each: a memory round trip per k group)
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+#pragma unroll
+  for (int g = 0; g < NG; ++g) {
+    asm volatile("" : "+v"(a0[g]), "+v"(a1[g]));
+#pragma unroll
+    for (int j = 0; j < 4; ++j) asm volatile("" : "+v"(bw[g][j]));
+  }
+  floatx4 acc0 = {0.f, 0.f, 0.f, 0.f}, acc1 = {0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+  for (int g = 0; g < NG; ++g)
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+      acc0 = __builtin_amdgcn_mfma_f32_16x16x4f32(a0[g][j], bw[g][j], acc0, 0, 0, 0);
+      acc1 = __builtin_amdgcn_mfma_f32_16x16x4f32(a1[g][j], bw[g][j], acc1, 0, 0, 0);
+    }
+  // D layout (16x16 f32): lane holds rows 4q + e of column c16
+#pragma unroll
+  for (int e = 0; e < 4; ++e) {
+    red[wave][(4 * q + e) * 16 + c16] = acc0[e];
+    red[wave][(16 + 4 * q + e) * 16 + c16] = acc1[e];
+  }
+  __syncthreads();
+  {
+    const int row = tid >> 4, col = tid & 15;
+    float s = red[0][tid];
+#pragma unroll
+    for (int v = 1; v < 8; ++v) s += red[v][tid];
+    const float y = block_act(s + bias[n0 + col], ACT);
+    if (r0 + row < B) Y[(size_t)(r0 + row) * ldy + n0 + col] = y;
+  }
+  if (Xcopy && blockIdx.y == 0) {
+    const int nr = min(32, B - r0);
+    for (int idx = tid; idx < nr * K; idx += 512) {
+      const int r = idx / K, k = idx - r * K;
+      Xcopy[(size_t)(r0 + r) * ldxc + k] = X[(size_t)(r0 + r) * ldx + k];
+    }
+  }
+}
+
+template <int ACT>
+static inline int launch_linear_mfma(const float* X, size_t ldx, int B, int K, const float* Wt, const float* bias,
+                                     int N, float* Y, int ldy, float* Xcopy, int ldxc, hipStream_t s) {
+  MEC_REQUIRE((K == 768 || K == 1280 || K == 2048) && N % 16 == 0 && ldx % 4 == 0,
+              "linear_mfma: K must be 768, 1280 or 2048, N % 16 and ldx % 4 must be 0");
+  if (B <= 0) return 0;
+  const dim3 grid((B + 31) / 32, N / 16), blk(512);
+  if (K == 768)
+    hipLaunchKernelGGL((linear_mfma_kernel<ACT, 6>), grid, blk, 0, s, X, ldx, B, Wt, bias, N, Y, ldy, Xcopy, ldxc);
+  else if (K == 1280)
+    hipLaunchKernelGGL((linear_mfma_kernel<ACT, 10>), grid, blk, 0, s, X, ldx, B, Wt, bias, N, Y, ldy, Xcopy, ldxc);
+  else
+    hipLaunchKernelGGL((linear_mfma_kernel<ACT, 16>), grid, blk, 0, s, X, ldx, B, Wt, bias, N, Y, ldy, Xcopy, ldxc);
+  MEC_LAUNCH_CHECK();
+  return 0;
+}
+
+// Classification head, one wave per row: logits = X[b] . Wt + b (N = 7, Wt [K][7]),
+// probs = softmax(logits). Grid ceil(B/4), 256 threads; K % 64 == 0, K <= 1024.
+__global__ __launch_bounds__(256) static __attribute__((unused)) void head7_kernel(
+    const float* __restrict__ X, int B, int K, const float* __restrict__ Wt, const float* __restrict__ b,
+    float* __restrict__ logits, float* __restrict__ probs) {
+  const int lane = threadIdx.x & 63, row = blockIdx.x * 4 + (threadIdx.x >> 6);
+  if (row >= B) return;
+  const float* x = X + (size_t)row * K;
+  float z[7];
+#pragma unroll
+  for (int o = 0; o < 7; ++o) z[o] = 0.f;
+  for (int k = lane; k < K; k += 64) {
+    const float xv = x[k];
+#pragma unroll
+    for (int o = 0; o < 7; ++o) z[o] = fmaf(xv, Wt[(size_t)k * 7 + o], z[o]);
+  }
+  float m = -INFINITY;
+#pragma unroll
+  for (int o = 0; o < 7; ++o) {
+    z[o] = wave_sum(z[o]) + b[o];  // every lane holds every logit
+    m = fmaxf(m, z[o]);
+  }
+  float e[7], s = 0.f;
+#pragma unroll
+  for (int o = 0; o < 7; ++o) {
+    e[o] = expf(z[o] - m);
+    s += e[o];
+  }
+  if (lane < 7) {
+    float zl = z[0], el = e[0];
+#pragma unroll
+    for (int o = 1; o < 7; ++o)
+      if (lane == o) { zl = z[o]; el = e[o]; }
+    logits[(size_t)row * 7 + lane] = zl;
+    probs[(size_t)row * 7 + lane] = el / s;
+  }
+}
+
+static inline int launch_head7(const float* X, int B, int K, const float* Wt, const float* b, float* logits,
+                               float* probs, hipStream_t s) {
+  MEC_REQUIRE(K % 64 == 0, "head7: K % 64 must be 0");
+  if (B <= 0) return 0;
+  hipLaunchKernelGGL(head7_kernel, dim3((B + 3) / 4), dim3(256), 0, s, X, B, K, Wt, b, logits, probs);
+  MEC_LAUNCH_CHECK();
+  return 0;
+}
+
 // Classification head: logits = X . Wt + b (N = 7), probs = softmax(logits); R rows/block.
 template <int R, int KMAX>
 __global__ __launch_bounds__(256) void head_softmax_kernel(const float* __restrict__ X, int B, int K,
@@ -272,6 +418,35 @@ __global__ __launch_bounds__(256) static __attribute__((unused)) void avgpool_ke
   float s = 0.f;
   for (int q = 0; q < HW; ++q) s += (float)p[(size_t)q * C];
   y[(size_t)b * C + c] = s / (float)HW;
+}
+
+// The same pool with 16-B loads: a thread sums 8 channels over every 4th pixel (four
+// thread groups per image), the four partial sums are added in a fixed order through LDS;
+// grid B, (C / 8) x 4 threads (C % 8 == 0, C <= 2048).
+__global__ __launch_bounds__(1024) static __attribute__((unused)) void avgpool8_kernel(const f16* __restrict__ x,
+                                                                                       int HW, int C,
+                                                                                       float* __restrict__ y) {
+  __shared__ float part[3][2048];
+  const int b = blockIdx.x, ng = C / 8, g = threadIdx.x / ng, c = (threadIdx.x - g * ng) * 8;
+  const f16* p = x + (size_t)b * HW * C + c;
+  float s[8];
+#pragma unroll
+  for (int j = 0; j < 8; ++j) s[j] = 0.f;
+  for (int q = g; q < HW; q += 4) {
+    const half8 v = *reinterpret_cast<const half8*>(p + (size_t)q * C);
+#pragma unroll
+    for (int j = 0; j < 8; ++j) s[j] += (float)v[j];
+  }
+  if (g > 0) {
+#pragma unroll
+    for (int j = 0; j < 8; ++j) part[g - 1][c + j] = s[j];
+  }
+  __syncthreads();
+  if (g == 0) {
+    float* o = y + (size_t)b * C + c;
+#pragma unroll
+    for (int j = 0; j < 8; ++j) o[j] = (((s[j] + part[0][c + j]) + part[1][c + j]) + part[2][c + j]) / (float)HW;
+  }
 }
 
 // Global average pool, NHWC f32 [B, HW, C] -> f32 [B, C]; grid (B, ceil(C/256)).

@@ -913,16 +913,11 @@ int MobileNetModel::forward_u8(const uint8_t* img, int B, int H, int W, int C, f
     g.M = B * h * h; g.N = 1280; g.K = 320;
     MEC_TRY(launch_gemm(g, s, &prof, TAG_MBV2_LAST));
   }
-  hipLaunchKernelGGL(avgpool_kernel, dim3(B, 1280 / 256), dim3(256), 0, s, L, h * h, 1280, pooled);
+  hipLaunchKernelGGL(avgpool8_kernel, dim3(B), dim3(1280 / 8 * 4), 0, s, L, h * h, 1280, pooled);
   MEC_LAUNCH_CHECK();
-  // classifier[1] Linear(1280,512) + classifier[2] ReLU -> the 512-d feature
-  hipLaunchKernelGGL((linear_rows_kernel<8, 1280>), dim3((B + 7) / 8, 512 / 64), dim3(256), 0, s, pooled,
-                     (size_t)1280, B, 1280, P + fc1_off, P + fc1b_off, 512, 64, feat, 512, (int)BACT_RELU,
-                     (float*)nullptr, 0);
-  MEC_LAUNCH_CHECK();
-  hipLaunchKernelGGL((head_softmax_kernel<8, 768>), dim3((B + 7) / 8), dim3(256), 0, s, feat, B, 512, P + fc2_off,
-                     P + fc2b_off, logits, probs);
-  MEC_LAUNCH_CHECK();
+  // classifier[1] Linear(1280,512) + classifier[2] ReLU -> the 512-d feature, then classifier[4] + softmax
+  MEC_TRY(launch_linear_mfma<BACT_RELU>(pooled, 1280, B, 1280, P + fc1_off, P + fc1b_off, 512, feat, 512, nullptr, 0, s));
+  MEC_TRY(launch_head7(feat, B, 512, P + fc2_off, P + fc2b_off, logits, probs, s));
   return 0;
 }
 

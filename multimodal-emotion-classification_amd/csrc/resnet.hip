@@ -655,15 +655,11 @@ int ImageModel::forward_u8(const uint8_t* img, int B, int H, int W, int C, float
   }
   MEC_TRY(run_blocks(kL12, blocks.size(), 0, B, 28, cur, other));
   H = 7;
-  hipLaunchKernelGGL(avgpool_kernel, dim3(B, 2048 / 256), dim3(256), 0, s, cur, H * H, 2048, pooled);
+  hipLaunchKernelGGL(avgpool8_kernel, dim3(B), dim3(2048 / 8 * 4), 0, s, cur, H * H, 2048, pooled);
   MEC_LAUNCH_CHECK();
-  // fc[1] Linear(2048,512) + fc[2] ReLU -> the 512-d feature (extract_features)
-  hipLaunchKernelGGL((linear_rows_kernel<8, 2048>), dim3((B + 7) / 8, 512 / 64), dim3(256), 0, s, pooled, (size_t)2048,
-                     B, 2048, P + fc1_off, P + fc1b_off, 512, 64, feat, 512, (int)BACT_RELU, (float*)nullptr, 0);
-  MEC_LAUNCH_CHECK();
-  hipLaunchKernelGGL((head_softmax_kernel<8, 768>), dim3((B + 7) / 8), dim3(256), 0, s, feat, B, 512, P + fc2_off,
-                     P + fc2b_off, logits, probs);
-  MEC_LAUNCH_CHECK();
+  // fc[1] Linear(2048,512) + fc[2] ReLU -> the 512-d feature (extract_features), then fc[4] + softmax
+  MEC_TRY(launch_linear_mfma<BACT_RELU>(pooled, 2048, B, 2048, P + fc1_off, P + fc1b_off, 512, feat, 512, nullptr, 0, s));
+  MEC_TRY(launch_head7(feat, B, 512, P + fc2_off, P + fc2b_off, logits, probs, s));
   return 0;
 }
 

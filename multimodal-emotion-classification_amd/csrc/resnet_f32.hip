@@ -402,12 +402,8 @@ int ImageModel::forward_f32(const uint8_t* img, int B, int H, int W, int C, floa
   }
   hipLaunchKernelGGL(avgpool_f32_kernel, dim3(B, 2048 / 256), dim3(256), 0, s, cur, Hc * Hc, 2048, pooled);
   MEC_LAUNCH_CHECK();
-  hipLaunchKernelGGL((linear_rows_kernel<8, 2048>), dim3((B + 7) / 8, 512 / 64), dim3(256), 0, s, pooled, (size_t)2048,
-                     B, 2048, P + fc1_off, P + fc1b_off, 512, 64, feat, 512, (int)BACT_RELU, (float*)nullptr, 0);
-  MEC_LAUNCH_CHECK();
-  hipLaunchKernelGGL((head_softmax_kernel<8, 768>), dim3((B + 7) / 8), dim3(256), 0, s, feat, B, 512, P + fc2_off,
-                     P + fc2b_off, logits, probs);
-  MEC_LAUNCH_CHECK();
+  MEC_TRY(launch_linear_mfma<BACT_RELU>(pooled, 2048, B, 2048, P + fc1_off, P + fc1b_off, 512, feat, 512, nullptr, 0, s));
+  MEC_TRY(launch_head7(feat, B, 512, P + fc2_off, P + fc2b_off, logits, probs, s));
   return 0;
 }
 
