@@ -235,6 +235,7 @@ def run(a, precision, B, world, rank, dev):
     from mec import _lib, dist as mdist, engine, synthetic as syn
     # the product library: no probe build (probe option values skip work and return wrong
     # results), and every knob of the pipeline's handles at its default (handles own their knobs)
+    # apart from the pipeline's own pin (BERT FFN2 on the ping-pong tile in the concurrent step)
     if _lib.load().mec_build_flags() != 0:
         raise SystemExit(f'bench.py: {_lib.LIB_PATH} is a probe build (MEC_PROBES); use the product library')
     pipe = engine.FusedPipeline(seed=1234, device=dev, concurrent=not a.serial, pipelined=not a.no_pipeline,

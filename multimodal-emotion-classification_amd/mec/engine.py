@@ -16,6 +16,8 @@ import torch
 from . import _lib, synthetic
 from ._lib import MecError
 
+TAG_BERT_FFN2 = 5  # launch class of BERT's FFN2 GEMM (mec_common.h Tag)
+
 KINDS = synthetic.KIND_IDS
 
 
@@ -315,6 +317,13 @@ class FusedPipeline:
         self._text = (torch.cuda.Stream(device=self.device, priority=0 if image_priority else -1)
                       if (concurrent and (text_priority or image_priority)) else None)
         self._tuned = set()  # batch sizes whose GEMM shapes were autotuned (serially)
+        if concurrent and precision == 'f16':
+            # BERT FFN2 (M = 128 B, N = 768, K = 3072) on the 256 x 256 ping-pong tile beside the
+            # image stream: BERT alone runs it fastest on 128 x 128 (the autotuner's pick, text
+            # 7.90 vs 8.02 ms at B = 256), but in the concurrent step the 4x fewer, larger tiles
+            # win: 11.10 vs 11.37 ms per step (interleaved A/B, tools/gpu_ab_tiles.sh,
+            # profiles/r02_ab_tiles_fused.txt). Same k order on both tiles: same bits.
+            self.text.set_option('gemm_bn_tag', TAG_BERT_FFN2 * 100000 + 40256)
 
     def forward(self, x_speech, ids, mask, gray, epilogue=None):
         """One batch through the path -> dict of per-modality and fusion outputs (and, with
