@@ -207,34 +207,6 @@ __device__ void block_softmax_small(float* X, int ldx, int N, float* out, int ld
   __syncthreads();
 }
 
-// Multi-block fp32 linear over a batch: grid (ceil(B/R), ceil(N/cols)), 256 threads.
-// Y[b, n] = act(X[b,:] . Wt[:, n] + bias[n]); optional copy of the X rows to Xcopy
-// (done by the blockIdx.y == 0 blocks).
-template <int R, int KMAX>
-__global__ __launch_bounds__(256) void linear_rows_kernel(const float* __restrict__ X, size_t ldx, int B, int K,
-                                                          const float* __restrict__ Wt, const float* __restrict__ bias,
-                                                          int N, int cols, float* __restrict__ Y, int ldy, int act,
-                                                          float* __restrict__ Xcopy, int ldxc) {
-  __shared__ __attribute__((aligned(16))) float sX[R * KMAX];
-  __shared__ __attribute__((aligned(16))) float sY[R * 256];
-  __shared__ __attribute__((aligned(16))) float red[R * 4 * 256];
-  const int tid = threadIdx.x;
-  const int r0 = blockIdx.x * R, nr = min(R, B - r0);
-  const int col0 = blockIdx.y * cols, nc = min(cols, N - col0);
-  for (int idx = tid; idx < R * K; idx += blockDim.x) {
-    const int r = idx / K, k = idx - r * K;
-    const float v = r < nr ? X[(size_t)(r0 + r) * ldx + k] : 0.f;
-    sX[idx] = v;
-    if (Xcopy && blockIdx.y == 0 && r < nr) Xcopy[(size_t)(r0 + r) * ldxc + k] = v;
-  }
-  __syncthreads();
-  block_linear<R>(sX, K, K, Wt + col0, N, bias + col0, nc, sY, cols, red, act);
-  for (int idx = tid; idx < nr * nc; idx += blockDim.x) {
-    const int r = idx / nc, c = idx - r * nc;
-    Y[(size_t)(r0 + r) * ldy + col0 + c] = sY[r * cols + c];
-  }
-}
-
 // Batched fp32 linear for the encoder heads (ResNet fc[1] 2048->512, MobileNetV2
 // classifier[1] 1280->512, BERT pooler 768->768) on v_mfma_f32_16x16x4f32 (exact f32 products,
 // f32 accumulate, MI355X_MICROARCH.md):
@@ -381,46 +353,7 @@ static inline int launch_head7(const float* X, int B, int K, const float* Wt, co
   return 0;
 }
 
-// Classification head: logits = X . Wt + b (N = 7), probs = softmax(logits); R rows/block.
-template <int R, int KMAX>
-__global__ __launch_bounds__(256) void head_softmax_kernel(const float* __restrict__ X, int B, int K,
-                                                           const float* __restrict__ Wt, const float* __restrict__ b,
-                                                           float* __restrict__ logits, float* __restrict__ probs) {
-  __shared__ __attribute__((aligned(16))) float sX[R * KMAX];
-  __shared__ __attribute__((aligned(16))) float sY[R * 8];
-  __shared__ __attribute__((aligned(16))) float red[R * 256];
-  const int tid = threadIdx.x;
-  const int r0 = blockIdx.x * R, nr = min(R, B - r0);
-  for (int idx = tid; idx < R * K; idx += blockDim.x) {
-    const int r = idx / K, k = idx - r * K;
-    sX[idx] = r < nr ? X[(size_t)(r0 + r) * K + k] : 0.f;
-  }
-  __syncthreads();
-  block_linear<R>(sX, K, K, Wt, 7, b, 7, sY, 8, red, BACT_NONE);
-  for (int idx = tid; idx < nr * 7; idx += blockDim.x) {
-    const int r = idx / 7, c = idx - r * 7;
-    logits[(size_t)(r0 + r) * 7 + c] = sY[r * 8 + c];
-  }
-  __syncthreads();
-  block_softmax_small<R>(sY, 8, 7, nullptr, 0);
-  for (int idx = tid; idx < nr * 7; idx += blockDim.x) {
-    const int r = idx / 7, c = idx - r * 7;
-    probs[(size_t)(r0 + r) * 7 + c] = sY[r * 8 + c];
-  }
-}
-
-// Global average pool, NHWC f16 [B, HW, C] -> f32 [B, C]; grid (B, ceil(C/256)).
-__global__ __launch_bounds__(256) static __attribute__((unused)) void avgpool_kernel(const f16* __restrict__ x, int HW, int C,
-                                                             float* __restrict__ y) {
-  const int b = blockIdx.x, c = blockIdx.y * 256 + threadIdx.x;
-  if (c >= C) return;
-  const f16* p = x + (size_t)b * HW * C + c;
-  float s = 0.f;
-  for (int q = 0; q < HW; ++q) s += (float)p[(size_t)q * C];
-  y[(size_t)b * C + c] = s / (float)HW;
-}
-
-// The same pool with 16-B loads: a thread sums 8 channels over every 4th pixel (four
+// Global average pool, NHWC f16 [B, HW, C] -> f32 [B, C], 16-B loads: a thread sums 8 channels over every 4th pixel (four
 // thread groups per image), the four partial sums are added in a fixed order through LDS;
 // grid B, (C / 8) x 4 threads (C % 8 == 0, C <= 2048).
 __global__ __launch_bounds__(1024) static __attribute__((unused)) void avgpool8_kernel(const f16* __restrict__ x,

@@ -1,7 +1,7 @@
 """GPU parity of the MobileNetV2 image backbone (csrc/mobilenet.hip) vs the CPU oracle
 (oracle/image_mbv2.py) and its fixture. Parity unpinned beyond the restatement (no
 reference code for MobileNetV2; torchvision absent). Tolerance as north_star: probs within
-1e-3, argmax exact on clear-margin samples."""
+1e-3, argmax exact on every sample (near-ties included; the margins are printed)."""
 import numpy as np
 import pytest
 import torch
@@ -29,10 +29,11 @@ def _check(got, ref):
     rf, rl, rp = ref
     assert np.abs(probs - rp).max() < PROB_TOL
     assert np.abs(logits - rl).max() < 5e-3
-    assert np.abs(feat - rf).max() < 0.02 * max(1.0, np.abs(rf).max())
     srt = np.sort(rp, axis=1)
-    clear = (srt[:, -1] - srt[:, -2]) > 2 * PROB_TOL
-    assert np.array_equal(rp.argmax(1)[clear], probs.argmax(1)[clear])
+    print(f'mbv2 B={len(rp)}: feat max|d| {np.abs(feat - rf).max():.3g} (|feat| max {np.abs(rf).max():.3g}), '
+          f'probs max|d| {np.abs(probs - rp).max():.3g}, min top-2 margin {(srt[:, -1] - srt[:, -2]).min():.3g}')
+    assert np.abs(feat - rf).max() < 5e-3 * max(1.0, np.abs(rf).max())  # measured <= 3.3e-3 at |feat| ~ 2
+    assert np.array_equal(rp.argmax(1), probs.argmax(1))
 
 
 def test_mbv2_golden(mb, dev, golden):

@@ -24,13 +24,6 @@ def _np(ts):
     return [t.cpu().numpy() for t in ts]
 
 
-def _margin_ok(ref_probs, got_probs):
-    """argmax exact wherever the oracle's top-2 gap exceeds the numeric tolerance."""
-    srt = np.sort(ref_probs, axis=1)
-    clear = (srt[:, -1] - srt[:, -2]) > 2 * PROB_TOL
-    return np.array_equal(ref_probs.argmax(1)[clear], got_probs.argmax(1)[clear]), int((~clear).sum())
-
-
 def test_speech_golden(models, dev, golden):
     g = golden('speech.npz')
     feat, logits, probs = _np(models['speech'].forward(engine.to_device(g['x'], dev)))
@@ -77,7 +70,9 @@ def test_text_golden(models, dev, golden):
     cls, logits, probs = _np(models['text'].forward(engine.to_device(g['ids'], dev), engine.to_device(g['mask'], dev)))
     assert np.abs(probs - g['probs']).max() < PROB_TOL
     assert np.array_equal(probs.argmax(1), g['probs'].argmax(1))
-    assert np.abs(cls - g['cls']).max() < 0.05  # fp16 operands through 12 layers, |cls| ~ 1
+    e_cls = float(np.abs(cls - g['cls']).max())
+    print(f'text golden: cls max|d| {e_cls:.3g}, probs max|d| {np.abs(probs - g["probs"]).max():.3g}')
+    assert e_cls < 0.01  # f16 operands through 12 layers, |cls| ~ 5: measured 2.2e-3 (round 2)
 
 
 @pytest.mark.parametrize('B,ragged', [(2, True), (16, True), (64, False)])
@@ -85,9 +80,12 @@ def test_text_vs_oracle(models, dev, B, ragged):
     ids, mask = syn.text_inputs(B, 128, seed=100 + B, ragged=ragged)
     cls, logits, probs = _np(models['text'].forward(engine.to_device(ids, dev), engine.to_device(mask, dev)))
     rc, rl, rp = o_t.forward(syn.weights('text'), ids, mask)
+    srt = np.sort(rp, axis=1)
+    print(f'text B={B}: cls max|d| {np.abs(cls - rc).max():.3g} (|cls| max {np.abs(rc).max():.3g}), '
+          f'probs max|d| {np.abs(probs - rp).max():.3g}, min top-2 margin {(srt[:, -1] - srt[:, -2]).min():.3g}')
     assert np.abs(probs - rp).max() < PROB_TOL
-    ok, ties = _margin_ok(rp, probs)
-    assert ok, f'argmax mismatch on a clear-margin sample ({ties} near-ties excluded)'
+    assert np.abs(cls - rc).max() < 0.01  # measured 2.0-2.5e-3 at |cls| ~ 5 (round 2)
+    assert np.array_equal(probs.argmax(1), rp.argmax(1))  # every row, near-ties included
 
 
 def test_image_golden(models, dev, golden):
@@ -102,10 +100,12 @@ def test_image_vs_oracle(models, dev, B):
     gray = syn.image_inputs(B, seed=200 + B)
     feat, logits, probs = _np(models['image'].forward(engine.to_device(gray, dev)))
     rf, rl, rp = o_i.forward(syn.weights('image'), gray)
+    srt = np.sort(rp, axis=1)
+    print(f'image B={B}: feat max|d| {np.abs(feat - rf).max():.3g} (|feat| max {np.abs(rf).max():.3g}), '
+          f'probs max|d| {np.abs(probs - rp).max():.3g}, min top-2 margin {(srt[:, -1] - srt[:, -2]).min():.3g}')
     assert np.abs(probs - rp).max() < PROB_TOL
-    assert np.abs(feat - rf).max() < 0.02 * max(1.0, np.abs(rf).max())
-    ok, ties = _margin_ok(rp, probs)
-    assert ok
+    assert np.abs(feat - rf).max() < 2e-3 * max(1.0, np.abs(rf).max())  # measured 4e-4 of max (round 2)
+    assert np.array_equal(probs.argmax(1), rp.argmax(1))  # every row, near-ties included
 
 
 def test_fused_pipeline(dev):

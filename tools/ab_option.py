@@ -30,11 +30,12 @@ def main():
     ap.add_argument('--iters', type=int, default=5)
     ap.add_argument('--rounds', type=int, default=5)
     ap.add_argument('--probes', action='store_true', help='load libmec_hip_probes.so (probe option values)')
+    ap.add_argument('--precision', default='f16', choices=['f16', 'fp32'])
     a = ap.parse_args()
     dev = torch.device('cuda', 0)
     lib = _lib.load()
     if a.enc == 'pipeline':  # the bench step: speech + text + image + fusion on three streams
-        m = engine.FusedPipeline(seed=1234, device=dev)
+        m = engine.FusedPipeline(seed=1234, device=dev, precision=a.precision)
         ids, mask = syn.text_inputs(256, 128, seed=0)
         args = tuple(engine.to_device(v, dev) for v in (syn.speech_inputs(256, seed=0), ids, mask,
                                                         syn.image_inputs(256, seed=0)))
@@ -44,11 +45,12 @@ def main():
         args = tuple(torch.randn(256, d, generator=g).to(dev) for d in (64, 768, 512))
         args += tuple(torch.softmax(torch.randn(256, 7, generator=g), 1).to(dev) for _ in range(3))
     elif a.enc == 'text':
-        m = engine.TextEncoder(device=dev)
+        m = engine.TextEncoder(device=dev, precision=a.precision)
         ids, mask = syn.text_inputs(256, 128, seed=0)
         args = (engine.to_device(ids, dev), engine.to_device(mask, dev))
     else:
-        m = engine.ImageEncoder(device=dev) if a.enc == 'image' else engine.MobileNetImageEncoder(device=dev)
+        m = (engine.ImageEncoder(device=dev, precision=a.precision) if a.enc == 'image'
+             else engine.MobileNetImageEncoder(device=dev, precision=a.precision))
         args = (engine.to_device(syn.image_inputs(256, seed=0), dev),)
     outs, times = {}, {v: [] for v in a.values}
     def fwd():
@@ -75,7 +77,7 @@ def main():
     base = outs[a.values[0]]
     for v in a.values:
         d = [float((x - y).abs().max()) for x, y in zip(outs[v], base)]
-        print(json.dumps({'enc': a.enc, a.opt: v, 'ms': round(sorted(times[v])[len(times[v]) // 2], 4),
+        print(json.dumps({'enc': a.enc, 'precision': a.precision, a.opt: v, 'ms': round(sorted(times[v])[len(times[v]) // 2], 4),
                           'max_abs_diff_vs_first': d}))
 
 
