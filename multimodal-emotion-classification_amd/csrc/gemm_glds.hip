@@ -476,7 +476,16 @@ __global__ __launch_bounds__(512) void gemm_pp_kernel(const GemmParams p) {
     const int xcd = bid & 7, q = nwg >> 3, r = nwg & 7;
     bid = (xcd < r ? xcd * (q + 1) : r * (q + 1) + (xcd - r) * q) + (bid >> 3);
   }
-  const int bm = bid / nbn, bn = bid - (bid / nbn) * nbn;
+  int bm, bn;
+  if (p.group_m > 0) {  // groups of group_m M panels, M-fastest (the last group may be short)
+    const int gsz = p.group_m * nbn, grp = bid / gsz, in = bid - grp * gsz;
+    const int gm = min(p.group_m, nbm - grp * p.group_m);
+    bm = grp * p.group_m + in % gm;
+    bn = in / gm;
+  } else {
+    bm = bid / nbn;
+    bn = bid - (bid / nbn) * nbn;
+  }
   const int m0 = bm * BM, n0 = bn * BN;
 
   const int lrow = lane >> 3, pchunk = lane & 7;
@@ -727,7 +736,8 @@ static int launch_bn(const GemmParams& p, hipStream_t s, int id) {
     case 40256:
     case 41256: {
       if (p0.amode != A_PLAIN) { set_error("gemm_glds: ping-pong tiles take a plain A only"); return -1; }
-      const GemmParams& p = p0;
+      GemmParams p = p0;
+      p.group_m = opt().gemm_group_m;
       const dim3 blk(512);
       const int nbn = p.N / 256;
       const dim3 grd(((p.M + (id == 40256 ? 255 : 127)) / (id == 40256 ? 256 : 128)) * nbn);

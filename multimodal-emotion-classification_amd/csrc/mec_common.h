@@ -91,6 +91,11 @@ struct Options {
   int bert_qkv_attn = 1;    // fused BERT QKV projection + attention
   int bert_oproj_ln = 0;    // O-projection + residual + LayerNorm 1 in one kernel (1 | 3)
   int mbv2_impl = 0;
+  // ping-pong GEMM tile order inside each XCD's contiguous tile range: 0 = row-major (all N
+  // panels of one M panel in turn), G = groups of G M panels walked M-fastest, so the 32
+  // tiles an XCD runs at once share G A panels and 32/G weight panels
+  // (8: FFN1 reads 290 -> 227 MB per launch at B = 256, time unchanged; profiles/ffn1_traffic_gm*.json)
+  int gemm_group_m = 8;
   int fusion_r = 4;         // samples per fusion workgroup
   int fusion_split = 1;     // fusion as 3 launches
   int speech_impl = 0;      // 0 = layer-split dataflow kernel (speech_flow_kernel), 1 = one WG per 4 samples
@@ -204,6 +209,7 @@ struct GemmParams {
   int K1 = 0;
   // conv geometry (NHWC input)
   int H = 1, W = 1, C = 0, OH = 1, OW = 1, ks = 1, stride = 1, pad = 0;
+  int group_m = 0;  // ping-pong tile order inside an XCD's range: 0 row-major, G = G-row groups
 };
 
 int launch_gemm(const GemmParams& p, hipStream_t s, Prof* prof, int tag);

@@ -119,6 +119,33 @@ def test_pingpong_tile_k_tails(dev, M, K):
     assert all(torch.equal(o, outs[-1]) for o in outs[:-1])
 
 
+@pytest.mark.parametrize('M,N', [(300, 512), (2304 + 100, 768), (8192, 3072)])
+def test_pingpong_group_order_bit_identical(dev, M, N):
+    """Tile order inside an XCD's range (gemm_group_m 0 / 2 / 4 / 8 / 16), short last groups
+    and partial M tiles included: every order writes the same bits (each output keeps its k
+    chain; only which workgroup computes which tile changes)."""
+    lib = _lib.load()
+    K = 768
+    g = torch.Generator().manual_seed(M + N)
+    A = (torch.rand(M, K, generator=g) * 2 - 1).half().to(dev)
+    B = (torch.rand(N, K, generator=g) * 2 - 1).mul(K ** -0.5).half().to(dev)
+    bias = torch.rand(N, generator=g).to(dev)
+    ref = A.float() @ B.float().t() + bias
+    outs = []
+    try:
+        for gm in (0, 2, 4, 8, 16):
+            _lib.check(lib.mec_set_option(b'gemm_group_m', gm), 'gemm_group_m')
+            C32 = torch.empty(M, N, device=dev)
+            _forced(lib, 40256, lambda: _lib.check(lib.mec_gemm_f16(_p(A), _p(B), _p(bias), None, 0, None, _p(C32),
+                                                                    M, N, K, 0, _s()), f'gemm gm={gm}'))
+            torch.cuda.synchronize()
+            assert _rel_err(C32, ref) < 1e-5, gm
+            outs.append(C32.cpu())
+    finally:
+        lib.mec_set_option(b'gemm_group_m', 8)
+    assert all(torch.equal(o, outs[0]) for o in outs[1:])
+
+
 def test_gemm_f16_residual_f16_asymmetric(dev):
     """A = I with an asymmetric B catches a transposed C write."""
     lib = _lib.load()
