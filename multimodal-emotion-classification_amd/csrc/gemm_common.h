@@ -42,6 +42,23 @@ __device__ __forceinline__ float gelu_rat(float x) {
 }
 __device__ __forceinline__ f32x2 gelu_erf_x2(f32x2 x) { return f32x2{gelu_rat(x.x), gelu_rat(x.y)}; }
 
+// Tile coordinates of logical tile `bid` (after the XCD remap, which gives each XCD a
+// contiguous range): row-major over (bm, bn), or with group_m = G > 0 groups of G M panels
+// walked M-fastest (the last group may be short), so the tiles an XCD runs at once share G
+// A panels and fewer weight panels (opt().gemm_group_m). Result-neutral: every output keeps
+// its k chain.
+__device__ __forceinline__ void tile_coords(int bid, int nbm, int nbn, int group_m, int& bm, int& bn) {
+  if (group_m > 0) {
+    const int gsz = group_m * nbn, grp = bid / gsz, in = bid - grp * gsz;
+    const int gm = min(group_m, nbm - grp * group_m);
+    bm = grp * group_m + in % gm;
+    bn = in / gm;
+  } else {
+    bm = bid / nbn;
+    bn = bid - bm * nbn;
+  }
+}
+
 template <int N>
 __device__ __forceinline__ void wait_vm() {
   asm volatile("s_waitcnt vmcnt(%0)" ::"n"(N) : "memory");

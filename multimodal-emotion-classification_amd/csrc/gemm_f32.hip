@@ -71,7 +71,8 @@ __global__ __launch_bounds__(64 * WM * WN, (WM * WN == 4) ? 2 : 1) void gemm_f32
     const int xcd = bid & 7, q = nwg >> 3, r = nwg & 7;
     bid = (xcd < r ? xcd * (q + 1) : r * (q + 1) + (xcd - r) * q) + (bid >> 3);
   }
-  const int bm = bid / nbn, bn = bid - (bid / nbn) * nbn;
+  int bm, bn;
+  tile_coords(bid, nbm, nbn, p.group_m, bm, bn);
   const int m0 = bm * BM, n0 = bn * BN;
 
   const int lrow = lane >> 3, pchunk = lane & 7;
@@ -231,7 +232,9 @@ __global__ __launch_bounds__(64 * WM * WN, (WM * WN == 4) ? 2 : 1) void gemm_f32
 static int tile_n(int id) { const int b = (id - 1) % 4 + 1; return b == 3 ? 64 : (b == 4 ? 256 : 128); }
 
 template <int BM, int BN, int WM, int WN, int NS, int MF = 32>
-static int launch_f32(const GemmParams& p, hipStream_t s) {
+static int launch_f32(const GemmParams& p0, hipStream_t s) {
+  GemmParams p = p0;
+  p.group_m = opt().gemm_group_m;
   const int nwg = ((p.M + BM - 1) / BM) * (p.N / BN);
   const dim3 blk(64 * WM * WN);
   if (p.amode == A_PLAIN)

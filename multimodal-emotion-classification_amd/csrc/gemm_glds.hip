@@ -477,15 +477,7 @@ __global__ __launch_bounds__(512) void gemm_pp_kernel(const GemmParams p) {
     bid = (xcd < r ? xcd * (q + 1) : r * (q + 1) + (xcd - r) * q) + (bid >> 3);
   }
   int bm, bn;
-  if (p.group_m > 0) {  // groups of group_m M panels, M-fastest (the last group may be short)
-    const int gsz = p.group_m * nbn, grp = bid / gsz, in = bid - grp * gsz;
-    const int gm = min(p.group_m, nbm - grp * p.group_m);
-    bm = grp * p.group_m + in % gm;
-    bn = in / gm;
-  } else {
-    bm = bid / nbn;
-    bn = bid - (bid / nbn) * nbn;
-  }
+  tile_coords(bid, nbm, nbn, p.group_m, bm, bn);
   const int m0 = bm * BM, n0 = bn * BN;
 
   const int lrow = lane >> 3, pchunk = lane & 7;
