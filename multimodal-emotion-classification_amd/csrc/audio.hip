@@ -42,6 +42,7 @@ constexpr int A_CMAX = 184;  // peaks per frame: local maxima of 358 band bins a
 constexpr int A_BAND_LO = 1, A_BAND_HI = 1024;  // bins that may hold a peak (mask applied too)
 constexpr int A_TMAX = 4096;   // frames per clip (95 s at 22050 Hz)
 constexpr int A_NLDS = 24576;  // peak magnitudes kept in LDS for the median (more: read from HBM)
+static_assert(A_NCHROMA * A_NBIN <= A_NLDS, "the chroma filterbank reuses the peak buffer");
 constexpr int A_MSEG = 1024;   // mel segments (band x thread-chunk runs)
 }  // namespace
 
@@ -279,40 +280,59 @@ __device__ __forceinline__ float fkey_inv(unsigned k) {
 }
 
 // rank-r smallest of the clip's n peak magnitudes (radix select on order-preserving keys, 4
-// passes of 8 bits). The magnitudes come from LDS (smag) when the clip's peaks fit there,
+// passes of 8 bits; hist holds 256 x (1 + waves) ints: per-wave histograms, then their sum). The magnitudes come from LDS (smag) when the clip's peaks fit there,
 // else straight from the per-frame peak lists (soff = per-frame prefix offsets).
 __device__ unsigned radix_select(const float* smag, int n, const float2* cd, const int* soff, int T, unsigned r,
                                  int* hist, unsigned* sh) {
   unsigned prefix = 0, pmask = 0;
   const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6, nw = blockDim.x >> 6;
+  int* wh = hist + 256 * (1 + wave);  // this wave's own histogram: 8x less same-address contention
   for (int pass = 0; pass < 4; ++pass) {
     const int shift = 24 - 8 * pass;
-    for (int i = threadIdx.x; i < 256; i += blockDim.x) hist[i] = 0;
+    for (int i = threadIdx.x; i < 256 * (1 + nw); i += blockDim.x) hist[i] = 0;
     __syncthreads();
     if (smag) {
       for (int i = threadIdx.x; i < n; i += blockDim.x) {
         const unsigned k = fkey(smag[i]);
-        if ((k & pmask) == prefix) atomicAdd(&hist[(k >> shift) & 255], 1);
+        if ((k & pmask) == prefix) atomicAdd(&wh[(k >> shift) & 255], 1);
       }
     } else {
       for (int t = wave; t < T; t += nw) {
         const int cnt = soff[t + 1] - soff[t];
         for (int i = lane; i < cnt; i += 64) {
           const unsigned k = fkey(cd[(size_t)t * A_CMAX + i].y);
-          if ((k & pmask) == prefix) atomicAdd(&hist[(k >> shift) & 255], 1);
+          if ((k & pmask) == prefix) atomicAdd(&wh[(k >> shift) & 255], 1);
         }
       }
     }
     __syncthreads();
-    if (threadIdx.x == 0) {
-      unsigned acc = 0;
-      int d = 0;
-      for (; d < 255; ++d) {
-        if (acc + (unsigned)hist[d] > r) break;
-        acc += hist[d];
+    for (int i = threadIdx.x; i < 256; i += blockDim.x) {
+      int s = 0;
+      for (int w = 0; w < nw; ++w) s += hist[256 * (1 + w) + i];
+      hist[i] = s;
+    }
+    __syncthreads();
+    if (threadIdx.x < 64) {  // first bin d < 255 whose inclusive count exceeds r (else 255): one wave,
+      // 4 bins per lane, a lane prefix sum, the lowest qualifying lane by ballot
+      const int l = threadIdx.x;
+      const unsigned h0 = hist[4 * l], h1 = hist[4 * l + 1], h2 = hist[4 * l + 2], h3 = hist[4 * l + 3];
+      const unsigned tot = h0 + h1 + h2 + h3;
+      unsigned inc = tot;
+#pragma unroll
+      for (int o = 1; o < 64; o <<= 1) {
+        const unsigned v = __shfl_up(inc, o, 64);
+        if (l >= o) inc += v;
       }
-      sh[0] = prefix | ((unsigned)d << shift);
-      sh[1] = r - acc;
+      const unsigned c0 = inc - tot, c1 = c0 + h0, c2 = c1 + h1, c3 = c2 + h2;  // counts before bins 4l+j
+      const int dj = c1 > r ? 0 : c2 > r ? 1 : c3 > r ? 2 : (c3 + h3 > r && l < 63) ? 3 : -1;
+      const unsigned long long bal = __ballot(dj >= 0);
+      const int src = bal ? __ffsll((long long)bal) - 1 : 63;
+      if (l == src) {
+        const int d = bal ? 4 * l + dj : 255;
+        const unsigned acc = bal ? (dj == 0 ? c0 : dj == 1 ? c1 : dj == 2 ? c2 : c3) : c3;
+        sh[0] = prefix | ((unsigned)d << shift);
+        sh[1] = r - acc;
+      }
     }
     __syncthreads();
     prefix = sh[0];
@@ -333,7 +353,7 @@ __global__ __launch_bounds__(512) void audio_clip_kernel(const float* __restrict
   __shared__ double band4[4][A_NMEL];
   __shared__ double redd[8][4];
   __shared__ float redf[8];
-  __shared__ int hist[256];
+  __shared__ int hist[256 * 9];  // the radix select's histogram + one per wave
   __shared__ unsigned sh[2];
   __shared__ int counts[A_NTUNE];
   __shared__ int s_tidx;
@@ -350,13 +370,31 @@ __global__ __launch_bounds__(512) void audio_clip_kernel(const float* __restrict
 #pragma unroll
   for (int o = 32; o > 0; o >>= 1) mx = fmaxf(mx, __shfl_xor(mx, o, 64));
   if (lane == 0) redf[wave] = mx;
-  if (tid == 0) {  // per-frame peak offsets (serial prefix, T <= A_TMAX)
-    int acc = 0;
-    for (int t = 0; t < T; ++t) {
-      soff[t] = acc;
-      acc += cnt[t];
+  {  // per-frame peak offsets: exclusive prefix of the counts (T <= A_TMAX = 8 per thread)
+    const int per = (T + 511) / 512, t0 = min(tid * per, T), t1 = min(t0 + per, T);
+    int c[8], own = 0;
+#pragma unroll
+    for (int i = 0; i < 8; ++i) {
+      c[i] = t0 + i < t1 ? cnt[t0 + i] : 0;
+      own += c[i];
     }
-    soff[T] = acc;
+    int inc = own;
+#pragma unroll
+    for (int o = 1; o < 64; o <<= 1) {
+      const int v = __shfl_up(inc, o, 64);
+      if (lane >= o) inc += v;
+    }
+    if (lane == 63) hist[wave] = inc;  // per-wave totals (hist is free until the median)
+    __syncthreads();
+    int acc = inc - own;
+    for (int w = 0; w < wave; ++w) acc += hist[w];
+#pragma unroll
+    for (int i = 0; i < 8; ++i)
+      if (t0 + i < t1) {
+        soff[t0 + i] = acc;
+        acc += c[i];
+      }
+    if (tid == 511) soff[T] = acc;
   }
   __syncthreads();
   float floor_db = redf[0];
@@ -431,7 +469,13 @@ __global__ __launch_bounds__(512) void audio_clip_kernel(const float* __restrict
   __syncthreads();
 
   // ---- chroma at that tuning: per frame raw = fb . P, / max |raw|, frame mean
-  const float* fb = tb.chroma + (size_t)s_tidx * A_NCHROMA * A_NBIN;
+  // the tuning's filterbank (48 KB) staged into the peak-magnitude buffer, free after the median
+  float* fb = smag;
+  {
+    const float* fbg = tb.chroma + (size_t)s_tidx * A_NCHROMA * A_NBIN;
+    for (int i = tid; i < A_NCHROMA * A_NBIN; i += 512) fb[i] = fbg[i];
+  }
+  __syncthreads();
   double cacc[A_NCHROMA];
 #pragma unroll
   for (int c = 0; c < A_NCHROMA; ++c) cacc[c] = 0.0;
@@ -440,10 +484,17 @@ __global__ __launch_bounds__(512) void audio_clip_kernel(const float* __restrict
     float part[A_NCHROMA];
 #pragma unroll
     for (int c = 0; c < A_NCHROMA; ++c) part[c] = 0.f;
-    for (int k = lane; k < A_NBIN; k += 64) {
-      const float p = P[k];
+    constexpr int KI = (A_NBIN + 63) / 64;
+    float pv[KI];  // the frame's power column, all loads in flight at once
 #pragma unroll
-      for (int c = 0; c < A_NCHROMA; ++c) part[c] += fb[c * A_NBIN + k] * p;
+    for (int i = 0; i < KI; ++i) pv[i] = lane + 64 * i < A_NBIN ? P[lane + 64 * i] : 0.f;
+#pragma unroll
+    for (int i = 0; i < KI; ++i) {
+      const int k = lane + 64 * i;
+      if (k < A_NBIN) {
+#pragma unroll
+        for (int c = 0; c < A_NCHROMA; ++c) part[c] += fb[c * A_NBIN + k] * pv[i];
+      }
     }
 #pragma unroll
     for (int c = 0; c < A_NCHROMA; ++c)
