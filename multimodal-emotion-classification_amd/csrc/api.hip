@@ -305,7 +305,8 @@ int set_option(Options& o, const std::string& k, int value) {
     o.speech_debug = value;
     return 0;
   }
-  if (k == "audio_debug" && (value == 0 || (probe && (value == 1 || value == 2 || value == 4 || value == 8 || value == 15)))) {
+  if (k == "audio_debug" && (value == 0 || (probe && (value == 1 || value == 2 || value == 4 || value == 8 || value == 15 ||
+                                                       value == 32 || value == 64 || value == 96 || value == 128)))) {
     o.audio_debug = value;
     return 0;
   }

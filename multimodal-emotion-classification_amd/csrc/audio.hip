@@ -343,12 +343,72 @@ __device__ unsigned radix_select(const float* smag, int n, const float2* cd, con
   return prefix;
 }
 
+// estimate_tuning's histogram bin of a peak frequency (pitch_tuning: residual of 12 log2(f /
+// 27.5) folded to [-0.5, 0.5), numpy's 101 float64 edges, last bin closed); 255 = no bin (f <= 0)
+__device__ __noinline__ int tuning_bin(float fx) {  // out of line: the float64 log2 inlined 12x cost registers
+  if (!(fx > 0.f)) return 255;
+  const float o = (float)log2((double)(fx / 27.5f));
+  const float x = 12.0f * o;
+  float r = x - floorf(x);  // np.mod(x, 1.0), x > 0
+  if (r >= 0.5f) r -= 1.0f;
+  const double rd = (double)r;
+  int bi = (int)floor((rd + 0.5) * 100.0);
+  bi = min(max(bi, 0), A_NTUNE - 1);
+  // exact edges: edges[i] = i * 0.01 + (-0.5) (numpy linspace), last bin closed
+  while (bi > 0 && rd < (double)bi * 0.01 + (-0.5)) --bi;
+  while (bi < A_NTUNE - 1 && rd >= (double)(bi + 1) * 0.01 + (-0.5)) ++bi;
+  return bi;
+}
+
+// The order statistic after rank r whose key is k (rank r + 1): k itself when more than r + 1
+// keys are <= k, else the smallest key above k. One counting pass instead of a second radix
+// select (scratch: 2 words).
+__device__ unsigned next_order_key(const float* smag, int n, const float2* cd, const int* soff, int T, unsigned k,
+                                   unsigned r, unsigned* scratch) {
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6, nw = blockDim.x >> 6;
+  if (threadIdx.x == 0) {
+    scratch[0] = 0u;
+    scratch[1] = 0xffffffffu;
+  }
+  __syncthreads();
+  unsigned le = 0, gt = 0xffffffffu;
+  auto visit = [&](unsigned q) {
+    if (q <= k) ++le;
+    else gt = min(gt, q);
+  };
+  if (smag) {
+    for (int i = threadIdx.x; i < n; i += blockDim.x) visit(fkey(smag[i]));
+  } else {
+    for (int t = wave; t < T; t += nw) {
+      const int cnt = soff[t + 1] - soff[t];
+      for (int i = lane; i < cnt; i += 64) visit(fkey(cd[(size_t)t * A_CMAX + i].y));
+    }
+  }
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) {
+    le += __shfl_xor(le, o, 64);
+    gt = min(gt, (unsigned)__shfl_xor(gt, o, 64));
+  }
+  if (lane == 0) {
+    atomicAdd(&scratch[0], le);
+    atomicMin(&scratch[1], gt);
+  }
+  __syncthreads();
+  const unsigned res = scratch[0] > r + 1 ? k : scratch[1];
+  __syncthreads();
+  return res;
+}
+
+// STOP (probe builds only, audio_debug 32 * STOP; wrong results): return after phase STOP
+// (1 MFCC + peak compaction, 2 median, 3 tuning histogram, 4 chroma)
+template <int STOP = 0>
 __global__ __launch_bounds__(512) void audio_clip_kernel(const float* __restrict__ pow_in,
                                                          const float* __restrict__ meldb, const double* __restrict__ scal,
                                                          const float2* __restrict__ cand, const int* __restrict__ ccount,
                                                          int T, AudioTables tb, float* __restrict__ feat, int F,
                                                          float* __restrict__ tuning_out) {
   __shared__ float smag[A_NLDS];
+  __shared__ unsigned char sbin[A_NLDS];  // each peak's tuning bin (255: none), beside smag
   __shared__ int soff[A_TMAX + 1];
   __shared__ double band4[4][A_NMEL];
   __shared__ double redd[8][4];
@@ -365,8 +425,15 @@ __global__ __launch_bounds__(512) void audio_clip_kernel(const float* __restrict
   const float2* cd = cand + (size_t)b * T * A_CMAX;
 
   // ---- MFCC: top_db = 80 clamp against the clip max, frame mean, DCT-II ortho
+  // loads batched 8 deep (a load-use chain per element was one memory round trip each)
   float mx = -INFINITY;
-  for (int i = tid; i < T * A_NMEL; i += 512) mx = fmaxf(mx, md[i]);
+  for (int i0 = tid; i0 < T * A_NMEL; i0 += 512 * 8) {
+    float v[8];
+#pragma unroll
+    for (int j = 0; j < 8; ++j) v[j] = i0 + 512 * j < T * A_NMEL ? md[i0 + 512 * j] : -INFINITY;
+#pragma unroll
+    for (int j = 0; j < 8; ++j) mx = fmaxf(mx, v[j]);
+  }
 #pragma unroll
   for (int o = 32; o > 0; o >>= 1) mx = fmaxf(mx, __shfl_xor(mx, o, 64));
   if (lane == 0) redf[wave] = mx;
@@ -403,24 +470,60 @@ __global__ __launch_bounds__(512) void audio_clip_kernel(const float* __restrict
   {
     const int m = tid & (A_NMEL - 1), q = tid >> 7;
     double sacc = 0.0;
-    for (int t = q; t < T; t += 4) sacc += (double)fmaxf(md[(size_t)t * A_NMEL + m], floor_db);
+    for (int t0 = q; t0 < T; t0 += 4 * 8) {  // 8 loads in flight, summed in frame order
+      float v[8];
+#pragma unroll
+      for (int j = 0; j < 8; ++j) v[j] = t0 + 4 * j < T ? md[(size_t)(t0 + 4 * j) * A_NMEL + m] : 0.f;
+#pragma unroll
+      for (int j = 0; j < 8; ++j)
+        if (t0 + 4 * j < T) sacc += (double)fmaxf(v[j], floor_db);
+    }
     band4[q][m] = sacc;
   }
   const int n = soff[T];
   const bool in_lds = n <= A_NLDS;
-  if (in_lds)  // the peak magnitudes, compacted into LDS for the median
-    for (int t = wave; t < T; t += 8) {
-      const int o = soff[t], c = soff[t + 1] - o;
-      for (int i = lane; i < c; i += 64) smag[o + i] = cd[(size_t)t * A_CMAX + i].y;
+  if (in_lds) {  // the peaks compacted into LDS: magnitude (for the median) and tuning bin
+    static_assert(A_CMAX <= 3 * 64, "three loads per lane cover a frame's peaks");
+    for (int t0 = wave; t0 < T; t0 += 8 * 4) {  // four frames' loads in flight per wave
+      float2 v[4][3];
+#pragma unroll
+      for (int f = 0; f < 4; ++f) {
+        const int tf = t0 + 8 * f;
+        const int c = tf < T ? soff[tf + 1] - soff[tf] : 0;
+#pragma unroll
+        for (int j = 0; j < 3; ++j)
+          v[f][j] = lane + 64 * j < c ? cd[(size_t)tf * A_CMAX + lane + 64 * j] : make_float2(0.f, 0.f);
+      }
+#pragma unroll
+      for (int f = 0; f < 4; ++f) {
+        const int tf = t0 + 8 * f;
+        const int o = tf < T ? soff[tf] : 0, c = tf < T ? soff[tf + 1] - o : 0;
+#pragma unroll
+        for (int j = 0; j < 3; ++j)
+          if (lane + 64 * j < c) {
+            smag[o + lane + 64 * j] = v[f][j].y;
+            sbin[o + lane + 64 * j] = (unsigned char)tuning_bin(v[f][j].x);
+          }
+      }
     }
+  }
   __syncthreads();
   if (tid < tb.n_mfcc) {
     double c = 0.0;
-    for (int m = 0; m < A_NMEL; ++m)
-      c += tb.dct[tid * A_NMEL + m] * ((band4[0][m] + band4[1][m] + band4[2][m] + band4[3][m]) / (double)T);
+    for (int m0 = 0; m0 < A_NMEL; m0 += 16) {  // 16 DCT loads in flight, summed in m order
+      double d[16];
+#pragma unroll
+      for (int j = 0; j < 16; ++j) d[j] = tb.dct[tid * A_NMEL + m0 + j];
+#pragma unroll
+      for (int j = 0; j < 16; ++j) {
+        const int m = m0 + j;
+        c += d[j] * ((band4[0][m] + band4[1][m] + band4[2][m] + band4[3][m]) / (double)T);
+      }
+    }
     feat[(size_t)b * F + tid] = (float)c;
   }
 
+  if constexpr (STOP == 1) return;
   // ---- estimate_tuning: median peak magnitude, residual histogram, argmax
   float med = 0.f;
   if (n > 0) {
@@ -430,28 +533,28 @@ __global__ __launch_bounds__(512) void audio_clip_kernel(const float* __restrict
     if (n & 1) {
       med = v1;
     } else {
-      const unsigned k2 = radix_select(sm, n, cd, soff, T, (unsigned)(n / 2), hist, sh);
+      const unsigned k2 = next_order_key(sm, n, cd, soff, T, k1, (unsigned)((n - 1) / 2), reinterpret_cast<unsigned*>(hist));
       med = (v1 + fkey_inv(k2)) / 2.0f;
     }
   }
+  if constexpr (STOP == 2) {
+    if (tid == 0) feat[b] = med;
+    return;
+  }
   for (int i = tid; i < A_NTUNE; i += 512) counts[i] = 0;
   __syncthreads();
-  for (int t = wave; t < T; t += 8) {
-    const int c = soff[t + 1] - soff[t];
-    for (int i = lane; i < c; i += 64) {
-      const float2 pm = cd[(size_t)t * A_CMAX + i];
-      if (!(pm.y >= med) || !(pm.x > 0.f)) continue;
-      const float o = (float)log2((double)(pm.x / 27.5f));
-      const float x = 12.0f * o;
-      float r = x - floorf(x);  // np.mod(x, 1.0), x > 0
-      if (r >= 0.5f) r -= 1.0f;
-      const double rd = (double)r;
-      int bi = (int)floor((rd + 0.5) * 100.0);
-      bi = min(max(bi, 0), A_NTUNE - 1);
-      // exact edges: edges[i] = i * 0.01 + (-0.5) (numpy linspace), last bin closed
-      while (bi > 0 && rd < (double)bi * 0.01 + (-0.5)) --bi;
-      while (bi < A_NTUNE - 1 && rd >= (double)(bi + 1) * 0.01 + (-0.5)) ++bi;
-      atomicAdd(&counts[bi], 1);
+  if (in_lds) {
+    for (int i = tid; i < n; i += 512)
+      if (smag[i] >= med && sbin[i] != 255) atomicAdd(&counts[sbin[i]], 1);
+  } else {
+    for (int t = wave; t < T; t += 8) {
+      const int c = soff[t + 1] - soff[t];
+      for (int i = lane; i < c; i += 64) {
+        const float2 pm = cd[(size_t)t * A_CMAX + i];
+        if (!(pm.y >= med)) continue;
+        const int bi = tuning_bin(pm.x);
+        if (bi != 255) atomicAdd(&counts[bi], 1);
+      }
     }
   }
   __syncthreads();
@@ -469,25 +572,32 @@ __global__ __launch_bounds__(512) void audio_clip_kernel(const float* __restrict
   __syncthreads();
 
   // ---- chroma at that tuning: per frame raw = fb . P, / max |raw|, frame mean
+  if constexpr (STOP == 3) return;
   // the tuning's filterbank (48 KB) staged into the peak-magnitude buffer, free after the median
   float* fb = smag;
   {
     const float* fbg = tb.chroma + (size_t)s_tidx * A_NCHROMA * A_NBIN;
-    for (int i = tid; i < A_NCHROMA * A_NBIN; i += 512) fb[i] = fbg[i];
+    constexpr int NI = (A_NCHROMA * A_NBIN + 511) / 512;  // 25 loads per thread, all in flight
+    float v[NI];
+#pragma unroll
+    for (int j = 0; j < NI; ++j) v[j] = tid + 512 * j < A_NCHROMA * A_NBIN ? fbg[tid + 512 * j] : 0.f;
+#pragma unroll
+    for (int j = 0; j < NI; ++j)
+      if (tid + 512 * j < A_NCHROMA * A_NBIN) fb[tid + 512 * j] = v[j];
   }
   __syncthreads();
-  double cacc[A_NCHROMA];
-#pragma unroll
-  for (int c = 0; c < A_NCHROMA; ++c) cacc[c] = 0.0;
+  // lane c (< 12) keeps chroma c's running sum: one float64 divide per lane and frame, and no
+  // 12-double array per lane (the kernel was at 256 VGPRs with scratch spills)
+  double cacc = 0.0;
+  constexpr int KI = (A_NBIN + 63) / 64;
   for (int t = wave; t < T; t += 8) {
     const float* P = pow_in + ((size_t)b * T + t) * A_NBIN;
-    float part[A_NCHROMA];
-#pragma unroll
-    for (int c = 0; c < A_NCHROMA; ++c) part[c] = 0.f;
-    constexpr int KI = (A_NBIN + 63) / 64;
     float pv[KI];  // the frame's power column, all loads in flight at once
 #pragma unroll
     for (int i = 0; i < KI; ++i) pv[i] = lane + 64 * i < A_NBIN ? P[lane + 64 * i] : 0.f;
+    float part[A_NCHROMA];
+#pragma unroll
+    for (int c = 0; c < A_NCHROMA; ++c) part[c] = 0.f;
 #pragma unroll
     for (int i = 0; i < KI; ++i) {
       const int k = lane + 64 * i;
@@ -501,15 +611,20 @@ __global__ __launch_bounds__(512) void audio_clip_kernel(const float* __restrict
 #pragma unroll
       for (int o = 32; o > 0; o >>= 1) part[c] += __shfl_xor(part[c], o, 64);
     double m = 0.0;
+    float mine = 0.f;
 #pragma unroll
-    for (int c = 0; c < A_NCHROMA; ++c) m = fmax(m, fabs((double)part[c]));
+    for (int c = 0; c < A_NCHROMA; ++c) {
+      m = fmax(m, fabs((double)part[c]));
+      if (lane == c) mine = part[c];
+    }
     if (m < (double)FLT_MIN) m = 1.0;
-#pragma unroll
-    for (int c = 0; c < A_NCHROMA; ++c) cacc[c] += (double)(float)((double)part[c] / m);
+    cacc += (double)(float)((double)mine / m);
   }
-  if (lane == 0)
-#pragma unroll
-    for (int c = 0; c < A_NCHROMA; ++c) chroma_acc[wave][c] = cacc[c];
+  if (lane < A_NCHROMA) chroma_acc[wave][lane] = cacc;
+  if constexpr (STOP == 4) {
+    if (lane == 0) feat[b * F + wave] = (float)cacc;
+    return;
+  }
   // ---- spectral means: zcr, centroid, rolloff, rms (frames over the block)
   double sp[4] = {0.0, 0.0, 0.0, 0.0};
   for (int t = tid; t < T; t += 512)
@@ -725,13 +840,24 @@ int AudioModel::forward(const float* wave, int B, int L, float* feat, float* tun
     case 4: hipLaunchKernelGGL(audio_frame_kernel<4>, dim3(T, B), dim3(256), 0, s, wave, L, T, tb, pw, mdb, scal, cand, cc); break;
     case 8: hipLaunchKernelGGL(audio_frame_kernel<8>, dim3(T, B), dim3(256), 0, s, wave, L, T, tb, pw, mdb, scal, cand, cc); break;
     case 15: hipLaunchKernelGGL(audio_frame_kernel<15>, dim3(T, B), dim3(256), 0, s, wave, L, T, tb, pw, mdb, scal, cand, cc); break;
-    default: hipLaunchKernelGGL(audio_frame_kernel<0>, dim3(T, B), dim3(256), 0, s, wave, L, T, tb, pw, mdb, scal, cand, cc);
+    default: hipLaunchKernelGGL(audio_frame_kernel<0>, dim3(T, B), dim3(256), 0, s, wave, L, T, tb, pw, mdb, scal, cand, cc);  // 0, and 32..128 (clip-kernel probes)
   }
 #else
   hipLaunchKernelGGL(audio_frame_kernel<0>, dim3(T, B), dim3(256), 0, s, wave, L, T, tb, pw, mdb, scal, cand, cc);
 #endif
   MEC_LAUNCH_CHECK();
-  hipLaunchKernelGGL(audio_clip_kernel, dim3(B), dim3(512), 0, s, pw, mdb, scal, cand, cc, T, tb, feat,
+#ifdef MEC_PROBES
+  if (opt().audio_debug >= 32) {
+    const int F = n_mfcc + A_NCHROMA + 4;
+    switch (opt().audio_debug >> 5) {
+      case 1: hipLaunchKernelGGL(audio_clip_kernel<1>, dim3(B), dim3(512), 0, s, pw, mdb, scal, cand, cc, T, tb, feat, F, tuning); break;
+      case 2: hipLaunchKernelGGL(audio_clip_kernel<2>, dim3(B), dim3(512), 0, s, pw, mdb, scal, cand, cc, T, tb, feat, F, tuning); break;
+      case 3: hipLaunchKernelGGL(audio_clip_kernel<3>, dim3(B), dim3(512), 0, s, pw, mdb, scal, cand, cc, T, tb, feat, F, tuning); break;
+      default: hipLaunchKernelGGL(audio_clip_kernel<4>, dim3(B), dim3(512), 0, s, pw, mdb, scal, cand, cc, T, tb, feat, F, tuning);
+    }
+  } else
+#endif
+  hipLaunchKernelGGL(audio_clip_kernel<0>, dim3(B), dim3(512), 0, s, pw, mdb, scal, cand, cc, T, tb, feat,
                      n_mfcc + A_NCHROMA + 4, tuning);
   MEC_LAUNCH_CHECK();
   MEC_TRY(prof.end(TAG_AUDIO, s));

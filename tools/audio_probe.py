@@ -1,5 +1,7 @@
 """Time the audio frame kernel's probe builds (libmec_hip_probes.so, option audio_debug):
-1 no FFT stages, 2 no rolloff cumsum, 4 no mel / peak search, 8 no spectrum split, 15 all."""
+1 no FFT stages, 2 no rolloff cumsum, 4 no mel / peak search, 8 no spectrum split, 15 all;
+32 / 64 / 96 / 128: the clip kernel stops after MFCC / median / tuning histogram / chroma.
+    python tools/audio_probe.py B [values...]"""
 import os
 import sys
 
@@ -16,7 +18,7 @@ dev = torch.device('cuda', 0)
 B = int(sys.argv[1]) if len(sys.argv) > 1 else 256
 fx = engine.AudioFeaturizer(device=dev)
 wv = torch.from_numpy(np.random.default_rng(0).standard_normal((B, 66150)).astype(np.float32)).to(dev)
-for dbg in (0, 1, 2, 4, 8, 15, 0):
+for dbg in [int(v) for v in sys.argv[2:]] or (0, 1, 2, 4, 8, 15, 0):
     fx.set_option('audio_debug', dbg)
     fx.forward(wv)
     torch.cuda.synchronize()
