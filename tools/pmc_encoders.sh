@@ -5,7 +5,7 @@ cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
 export TMPDIR=/tmp
 for e in ${ENCS:-text image image_mbv2 speech fusion}; do
   O=gpurun_out/pmcenc_$e; rm -rf $O; mkdir -p $O
-  CMD="python3 tools/encoder_profile.py --enc $e --iters 3"
+  CMD="python3 tools/encoder_profile.py --enc $e --iters 3 --batch ${BATCH:-256}"
   timeout -k 10 180 rocprofv3 --kernel-trace -d $O/trace -o run -- $CMD > $O/trace.log 2>&1 || { echo "trace $e rc=$?"; exit 1; }
   i=0
   for SET in "FETCH_SIZE GRBM_GUI_ACTIVE" "WRITE_SIZE GRBM_GUI_ACTIVE" "SQ_INSTS_MFMA SQ_VALU_MFMA_BUSY_CYCLES GRBM_GUI_ACTIVE"; do
