@@ -140,6 +140,8 @@ int mec_conv_f32(const float* x, const float* w, const float* bias, const float*
  *   "gemm_bn_tag" tag*100000+id   force a tile for one launch class (e.g. 3 = BERT O-proj)
  *   "gemm_f32_tile" [0]|1..8  force one fp32 GEMM tile (0 = autotune; 5..8 = 1..4 on 16x16x4)
  *   "gemm_f32_tag" tag*100000+id  pin an fp32 tile for one launch class (default: BERT FFN1 -> 8)
+ *   "gemm_f32_family" 0|[16]|32  fp32 tiles of one MFMA shape only (16x16x4 / 32x32x2): one k order
+ *                          for every shape, so rows do not depend on the batch size
  *   "gemm_prefetch_r" 0|[1]  f16 residual prefetch in short-K GEMMs
  *   "gemm_group_m" 0|2|4|[8]|16  ping-pong GEMM tile order inside each XCD's tile range (0: row-major,
  *                          G: G-panel groups of M walked M-fastest, fewer weight re-fetches)

@@ -263,6 +263,10 @@ int set_option(Options& o, const std::string& k, int value) {
   const bool probe = kProbes;
   if (k == "gemm_impl" && (value == 1 || value == 2)) { o.gemm_impl = value; return 0; }
   if (k == "fusion_r" && (value == 1 || value == 2 || value == 4)) { o.fusion_r = value; return 0; }
+  if (k == "gemm_f32_family" && (value == 0 || value == 16 || value == 32)) {
+    o.gemm_f32_family = value;
+    return 0;
+  }
   if (k == "gemm_group_m" && (value == 0 || value == 2 || value == 4 || value == 8 || value == 16)) {
     o.gemm_group_m = value;
     return 0;

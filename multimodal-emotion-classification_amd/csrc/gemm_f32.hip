@@ -264,10 +264,17 @@ static std::array<int, 11> f32_key(const GemmParams& p) {
   return {1, p.amode, p.M, p.N, p.K, p.H, p.W, p.C, p.ks, p.stride, p.pad};
 }
 
+// MFMA family allowed by opt().gemm_f32_family (0: both; 16: ids 5..8 on 16x16x4; 32: ids 1..4
+// on 32x32x2). The two families sum in different k orders, so one family for every shape makes
+// a row's result independent of the batch size (the tuned tile may change with M, its bits not).
+static bool family_ok(int id) {
+  const int fam = opt().gemm_f32_family;
+  return fam == 0 || (fam == 16 ? id >= 5 : id <= 4);
+}
+
 static int heuristic_tile(const GemmParams& p) {
-  if (p.N % 128) return 3;
-  const long tiles = (long)((p.M + 255) / 256) * (p.N / 128);
-  return tiles >= 512 ? 1 : 2;
+  const int id = (p.N % 128) ? 3 : ((long)((p.M + 255) / 256) * (p.N / 128) >= 512 ? 1 : 2);
+  return opt().gemm_f32_family == 16 ? id + 4 : id;
 }
 
 // First launch of a shape: time every legal tile (median of 3 launches, hipEvents on the
@@ -279,7 +286,7 @@ static int tune_tile(const GemmParams& p, hipStream_t s, int* out) {
   float best = 1e30f;
   int best_id = heuristic_tile(p);
   for (int id = 1; id <= 8; ++id) {
-    if (p.N % tile_n(id)) continue;
+    if (p.N % tile_n(id) || !family_ok(id)) continue;
     MEC_TRY(launch_tile(p, s, id));
     MEC_HIP(hipEventRecord(ev[0], s));
     for (int r = 0; r < REPS; ++r) {
@@ -314,7 +321,8 @@ int launch_gemm_f32(const GemmParams& p, hipStream_t s, Prof* prof, int tag) {
   }
   const auto key = f32_key(p);
   int id = opt().gemm_f32_tile;
-  if (!id && tag > 0 && tag < TAG_COUNT && opt().gemm_f32_tag[tag] && p.N % tile_n(opt().gemm_f32_tag[tag]) == 0) {
+  if (!id && tag > 0 && tag < TAG_COUNT && opt().gemm_f32_tag[tag] && p.N % tile_n(opt().gemm_f32_tag[tag]) == 0 &&
+      family_ok(opt().gemm_f32_tag[tag])) {
     id = opt().gemm_f32_tag[tag];
     tune_cache().put(key, id);  // so mec_model_gemm_query reports the tile that runs
   }

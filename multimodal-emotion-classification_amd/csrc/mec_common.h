@@ -75,6 +75,10 @@ struct Options {
   int gemm_autotune = 1;
   int gemm_prefetch_r = 1;  // f16 residual prefetch in short-K GEMMs
   int gemm_f32_tile = 0;    // forced fp32 GEMM tile id (0 = autotune)
+  // fp32 autotune family: 0 both, 16 = 16x16x4 tiles only, 32 = 32x32x2 only. 16 (default): one k
+  // order for every shape, so the fp32 path is batch-invariant bit for bit, at no measured cost
+  // (ResNet50 20.73 vs 20.77 ms, BERT 45.95 vs 45.85 ms at B = 256; tools/ab_f32_family.py)
+  int gemm_f32_family = 16;
   // fp32 engine, per launch class: BERT FFN1 pinned to 256x256 on 16x16x4 (it and the 32x32x2
   // form time within 0.3%, so the autotune flipped between them run to run)
   int gemm_f32_tag[TAG_COUNT] = {0, 0, 0, 0, /*TAG_BERT_FFN1*/ 8};

@@ -228,3 +228,21 @@ def test_mobilenet_v2_fp32_vs_oracle(dev, B):
     ferr = float(np.abs(feat[sub] - rf).max() / np.abs(rf).max())
     print(f'  feat rel err {ferr:.3g}, logits max|d| {np.abs(logits[sub] - rl).max():.3g}')
     assert agree == len(sub) and err <= FP32_PROB_TOL and ferr <= FP32_FEAT_RTOL
+
+
+@pytest.mark.parametrize('enc,B', [('image', 256), ('text', 128)])
+def test_fp32_batch_invariance(dev, enc, B):
+    """With the fp32 autotune held to one MFMA family (gemm_f32_family 16, the default) every
+    shape sums in one k order: rows of a full-size batch equal the same rows run as B = 16, bit
+    for bit, although the tuned tiles differ between the two batch sizes."""
+    if enc == 'image':
+        m = engine.ImageEncoder(device=dev, precision='fp32')
+        args = (engine.to_device(syn.image_inputs(B, seed=41), dev),)
+    else:
+        m = engine.TextEncoder(device=dev, precision='fp32')
+        ids, mask = syn.text_inputs(B, 128, seed=41, ragged=True)
+        args = (engine.to_device(ids, dev), engine.to_device(mask, dev))
+    big = [t[:16].cpu() for t in m.forward(*args)]
+    small = [t.cpu() for t in m.forward(*(a[:16] for a in args))]
+    for i, (a, b) in enumerate(zip(big, small)):
+        assert torch.equal(a, b), f'{enc} output {i}: rows of B={B} differ from the B=16 run'
