@@ -151,6 +151,7 @@ int mec_conv_f32(const float* x, const float* w, const float* bias, const float*
  *   "pw_chain" 0|1|[2]     layer1 seam kernels (1: the 256->64 seams, 2: also 256->128)
  *   "pw_chain_form" [0]|1|2  seam weight placement (LDS / registers)
  *   "bert_qkv_attn" 0|[1]  fused BERT QKV projection + attention
+ *   "bert_ln_rows" 1|[2]|4  BERT LayerNorm rows per wave (all loads of a wave's rows in flight first)
  *   "bert_oproj_ln" [0]|1|3  BERT O-projection + residual + LayerNorm 1 in one full-row kernel
  *                          (1: Wo staged in LDS, 3: Wo read into registers; both measured slower)
  *   "resnet_chunk" [0]|n   ResNet layers 1-2 over n-image chunks

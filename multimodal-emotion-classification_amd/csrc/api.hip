@@ -267,6 +267,10 @@ int set_option(Options& o, const std::string& k, int value) {
     o.gemm_f32_family = value;
     return 0;
   }
+  if (k == "bert_ln_rows" && (value == 1 || value == 2 || value == 4)) {
+    o.bert_ln_rows = value;
+    return 0;
+  }
   if (k == "gemm_group_m" && (value == 0 || value == 2 || value == 4 || value == 8 || value == 16)) {
     o.gemm_group_m = value;
     return 0;

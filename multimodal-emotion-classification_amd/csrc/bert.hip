@@ -77,6 +77,9 @@ __global__ __launch_bounds__(256) void bert_embed_ln_kernel(const int32_t* __res
 }
 
 // ----------------------------------------------------------------------------- LayerNorm
+// RW rows per wave (RW = 2: both rows' loads in flight before either reduction; option
+// bert_ln_rows). Each row's arithmetic is the same at any RW: same bits.
+template <int RW>
 __global__ __launch_bounds__(256) void bert_layernorm_kernel(const float* x, int M,
                                                              const float* __restrict__ g,
                                                              const float* __restrict__ b, float* h32,
@@ -84,14 +87,18 @@ __global__ __launch_bounds__(256) void bert_layernorm_kernel(const float* x, int
   // h32 may be null: the consumer of the f32 output (the next residual add) then
   // re-derives it from x and `stats` in its GEMM epilogue (GemmParams::r_stats)
   const int lane = threadIdx.x & 63;
-  const int row = blockIdx.x * 4 + (threadIdx.x >> 6);
-  if (row >= M) return;
-  float v[12];
+  const int row0 = (blockIdx.x * 4 + (threadIdx.x >> 6)) * RW;
+  if (row0 >= M) return;
+  float v[RW][12];
   float4 gg[3], bb[3];
 #pragma unroll
-  for (int j = 0; j < 3; ++j) {
-    const float4 t = *reinterpret_cast<const float4*>(x + (size_t)row * BH + j * 256 + lane * 4);
-    v[4 * j + 0] = t.x; v[4 * j + 1] = t.y; v[4 * j + 2] = t.z; v[4 * j + 3] = t.w;
+  for (int r = 0; r < RW; ++r) {
+    const int row = min(row0 + r, M - 1);
+#pragma unroll
+    for (int j = 0; j < 3; ++j) {
+      const float4 t = *reinterpret_cast<const float4*>(x + (size_t)row * BH + j * 256 + lane * 4);
+      v[r][4 * j + 0] = t.x; v[r][4 * j + 1] = t.y; v[r][4 * j + 2] = t.z; v[r][4 * j + 3] = t.w;
+    }
   }
   // gamma/beta issued together with the row loads: after the reductions they would sit
   // behind the (possibly aliasing) stores, one load->store round trip per float4
@@ -100,29 +107,44 @@ __global__ __launch_bounds__(256) void bert_layernorm_kernel(const float* x, int
     gg[j] = *reinterpret_cast<const float4*>(g + j * 256 + lane * 4);
     bb[j] = *reinterpret_cast<const float4*>(b + j * 256 + lane * 4);
   }
-  float s = 0.f;
 #pragma unroll
-  for (int i = 0; i < 12; ++i) s += v[i];
-  const float mean = wave_sum(s) * (1.0f / BH);
-  float q = 0.f;
+  for (int r = 0; r < RW; ++r) {
+    const int row = row0 + r;
+    if (row >= M) break;
+    float s = 0.f;
 #pragma unroll
-  for (int i = 0; i < 12; ++i) { const float d = v[i] - mean; q += d * d; }
-  const float rstd = 1.0f / sqrtf(wave_sum(q) * (1.0f / BH) + 1e-12f);
-  if (stats && lane == 0) stats[row] = make_float2(mean, rstd);
+    for (int i = 0; i < 12; ++i) s += v[r][i];
+    const float mean = wave_sum(s) * (1.0f / BH);
+    float q = 0.f;
 #pragma unroll
-  for (int j = 0; j < 3; ++j) {
-    const int c = j * 256 + lane * 4;
-    float4 o;
-    o.x = __builtin_fmaf((v[4 * j + 0] - mean) * rstd, gg[j].x, bb[j].x);
-    o.y = __builtin_fmaf((v[4 * j + 1] - mean) * rstd, gg[j].y, bb[j].y);
-    o.z = __builtin_fmaf((v[4 * j + 2] - mean) * rstd, gg[j].z, bb[j].z);
-    o.w = __builtin_fmaf((v[4 * j + 3] - mean) * rstd, gg[j].w, bb[j].w);
-    if (h32) *reinterpret_cast<float4*>(h32 + (size_t)row * BH + c) = o;
-    if (h16) {  // null on the fp32 path
-      half4 hh = {(f16)o.x, (f16)o.y, (f16)o.z, (f16)o.w};
-      *reinterpret_cast<half4*>(h16 + (size_t)row * BH + c) = hh;
+    for (int i = 0; i < 12; ++i) { const float d = v[r][i] - mean; q += d * d; }
+    const float rstd = 1.0f / sqrtf(wave_sum(q) * (1.0f / BH) + 1e-12f);
+    if (stats && lane == 0) stats[row] = make_float2(mean, rstd);
+#pragma unroll
+    for (int j = 0; j < 3; ++j) {
+      const int c = j * 256 + lane * 4;
+      float4 o;
+      o.x = __builtin_fmaf((v[r][4 * j + 0] - mean) * rstd, gg[j].x, bb[j].x);
+      o.y = __builtin_fmaf((v[r][4 * j + 1] - mean) * rstd, gg[j].y, bb[j].y);
+      o.z = __builtin_fmaf((v[r][4 * j + 2] - mean) * rstd, gg[j].z, bb[j].z);
+      o.w = __builtin_fmaf((v[r][4 * j + 3] - mean) * rstd, gg[j].w, bb[j].w);
+      if (h32) *reinterpret_cast<float4*>(h32 + (size_t)row * BH + c) = o;
+      if (h16) {  // null on the fp32 path
+        half4 hh = {(f16)o.x, (f16)o.y, (f16)o.z, (f16)o.w};
+        *reinterpret_cast<half4*>(h16 + (size_t)row * BH + c) = hh;
+      }
     }
   }
+}
+
+static void launch_ln_rows(const float* x, int M, const float* g, const float* b, float* h32, f16* h16, float2* st,
+                           hipStream_t s) {
+  if (opt().bert_ln_rows == 4)
+    hipLaunchKernelGGL(bert_layernorm_kernel<4>, dim3((M + 15) / 16), dim3(256), 0, s, x, M, g, b, h32, h16, st);
+  else if (opt().bert_ln_rows == 2)
+    hipLaunchKernelGGL(bert_layernorm_kernel<2>, dim3((M + 7) / 8), dim3(256), 0, s, x, M, g, b, h32, h16, st);
+  else
+    hipLaunchKernelGGL(bert_layernorm_kernel<1>, dim3((M + 3) / 4), dim3(256), 0, s, x, M, g, b, h32, h16, st);
 }
 
 // Host launchers (also used by the fp32 path, bert_f32.hip). One wave per token row.
@@ -140,7 +162,7 @@ int launch_bert_embed_ln(const int32_t* ids, int M, int L, const float* emb, flo
 
 int launch_bert_layernorm(const float* x, int M, const float* g, const float* b, float* h32, f16* h16, float2* stats,
                           hipStream_t s) {
-  hipLaunchKernelGGL(bert_layernorm_kernel, dim3((M + 3) / 4), dim3(256), 0, s, x, M, g, b, h32, h16, stats);
+  launch_ln_rows(x, M, g, b, h32, h16, stats, s);
   MEC_LAUNCH_CHECK();
   return 0;
 }
@@ -902,7 +924,7 @@ int TextModel::forward(const int32_t* ids, const int32_t* mask, int B, int L, fl
       if (!first) { g.r_stats = st2; g.r_g = pg2; g.r_b = pg2 + BH; }  // else: the embedding LN, written in full
       MEC_TRY(launch_gemm(g, s, &prof, TAG_BERT_OPROJ));
       MEC_TRY(prof.begin(TAG_BERT_LN, s));
-      hipLaunchKernelGGL(bert_layernorm_kernel, rows_grid, dim3(256), 0, s, t32, M, g1, b1, nullptr, h16, st1);
+      launch_ln_rows(t32, M, g1, b1, nullptr, h16, st1, s);
       MEC_LAUNCH_CHECK();
       MEC_TRY(prof.end(TAG_BERT_LN, s));
     }
@@ -916,8 +938,7 @@ int TextModel::forward(const int32_t* ids, const int32_t* mask, int B, int L, fl
     MEC_TRY(prof.begin(TAG_BERT_LN, s));
     // the last LN's f32 output feeds the pooler / CLS feature, so it is written in full
     // (in place: each wave holds its row in registers before writing it)
-    hipLaunchKernelGGL(bert_layernorm_kernel, rows_grid, dim3(256), 0, s, h32, M, g2, b2, last ? h32 : nullptr, h16,
-                       st2);
+    launch_ln_rows(h32, M, g2, b2, last ? h32 : nullptr, h16, st2, s);
     MEC_LAUNCH_CHECK();
     MEC_TRY(prof.end(TAG_BERT_LN, s));
   }

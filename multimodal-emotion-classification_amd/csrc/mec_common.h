@@ -93,6 +93,7 @@ struct Options {
   int pw_chain = 2;         // layer1 seam kernels (pw_chain.hip)
   int pw_chain_form = 0;
   int bert_qkv_attn = 1;    // fused BERT QKV projection + attention
+  int bert_ln_rows = 2;     // BERT LayerNorm rows per wave (1 | 2 | 4): 27.0 / 25.7 / 26.3 us at B = 256
   int bert_oproj_ln = 0;    // O-projection + residual + LayerNorm 1 in one kernel (1 | 3)
   int mbv2_impl = 0;
   // ping-pong GEMM tile order inside each XCD's contiguous tile range: 0 = row-major (all N

@@ -324,3 +324,20 @@ def test_pw_chain_bit_identical(dev, B):
     for o in outs[1:]:
         for a, b in zip(o, outs[0]):
             assert torch.equal(a, b)
+
+
+@pytest.mark.parametrize('precision', ['f16', 'fp32'])
+def test_bert_layernorm_rows_per_wave_bit_identical(dev, precision):
+    """bert_layernorm_kernel<RW> (bert_ln_rows 1 / 2 / 4): each row's arithmetic is the same at
+    any rows-per-wave, so the encoder's outputs are the same bits."""
+    from mec import engine, synthetic as syn
+    m = engine.TextEncoder(device=dev, precision=precision)
+    ids, mask = syn.text_inputs(9, 128, seed=77, ragged=True)
+    args = (engine.to_device(ids, dev), engine.to_device(mask, dev))
+    outs = []
+    for rw in (1, 2, 4):
+        m.set_option('bert_ln_rows', rw)
+        outs.append([t.cpu() for t in m.forward(*args)])
+    for o in outs[1:]:
+        for a, b in zip(outs[0], o):
+            assert torch.equal(a, b)
