@@ -1,31 +1,41 @@
-"""Benchmark: fused tri-modal samples/s @ batch 256 per GPU; per-modality logits max-abs-err
-(BASELINE.json metric).
+"""Benchmark: fused tri-modal samples/s; per-modality logits max-abs-err (BASELINE.json metric).
 
 One step = one pass of the whole hot path over one synthetic batch already resident in
 HBM: speech DNN + BERT-base (L=128) + ResNet50 (48x48 u8 -> 224) encoders, then the
 attention-MLP fusion, then (N>1) the RCCL all-gather of the 34-float result rows.
-Weak scaling: every rank processes its own batch (256 at N=1; 1024 per rank at N>1, i.e.
-BASELINE configs[4]'s global 8192 on 8 GPUs). Consecutive batches are pipelined
+Weak scaling: every rank processes its own batch (256 at N=1 = BASELINE configs[3]; 1024 per
+rank at N>1 = configs[4]'s global 8192 on 8 GPUs). Consecutive batches are pipelined
 (engine.FusedPipeline): batch i's fusion and gather overlap batch i+1's encoders; the timed
 region ends after the last batch's gather (device synchronize).
 
-The path runs at two precisions, each timed and checked on the same inputs, and rank 0
-prints one JSON line per precision:
-  1. "f16"  BERT / ResNet50 on f16 MFMA operands, fp32 accumulation, LayerNorm, softmax, GELU,
-           residual stream and heads (the fast path, north_star's >=10k/s mode);
-  2. "fp32" every operand and product in fp32 (v_mfma_f32_32x32x2_f32), the reference's own
-           precision: the same-precision counterpart, printed second.
-Each line carries `parity`: the oracle (CPU fp32 restatement of the reference) run on a fixed
-subset of the timed batch — logits / probs max-abs-err and argmax agreement per modality,
-the fused output checked end to end against o_f(o_s, o_t, o_i).
+The path runs at two precisions on the same inputs; rank 0 prints ONE JSON line:
+  headline  "fp32": every operand and product in fp32 (v_mfma_f32_16x16x4_f32 / 32x32x2_f32),
+            the reference's own precision (inference/text_inference.py:91-93,
+            inference/image_inference.py:116-118) -- `value` is this path's throughput;
+  nested    "f16_fast_path": BERT / ResNet50 on f16 MFMA operands with fp32 accumulation,
+            LayerNorm, softmax, GELU, residual stream and heads (north_star's probs <= 1e-3 bar;
+            narrower than the reference's arithmetic, so reported beside the headline, not as it).
+Each carries `parity`: the oracle (CPU fp32 restatement of the reference) on rows of the timed
+batch -- every row at B <= 256, rows from every quarter of the batch beyond -- with logits /
+probs max-abs-err, argmax agreement and the count of at-risk rows (oracle top-2 margin below
+twice the measured probs error), the fused output checked end to end against o_f(o_s, o_t, o_i).
+At N>1 rank 0 also checks two gathered rows of EVERY rank against the oracle run on that rank's
+inputs (the all-gather's order and content).
 
     python bench.py [--gpus N] [--steps K] [--warmup W] [--batch B] [--precision both|f16|fp32]
-    python -m torch.distributed.run --nproc-per-node N ... bench.py --gpus N
+
+With --gpus N > 1 and no WORLD_SIZE in the environment, bench.py starts
+`python -m torch.distributed.run --nproc-per-node N ... bench.py` as a child process BEFORE any
+GPU call and exits with its status (one process per GPU; the driver's own torchrun launch
+sets WORLD_SIZE and skips this). With no GPU visible (or --stub) each rank runs a stub step on
+the CPU over gloo -- the launcher, sharding, all-gather order and max-over-ranks timing only;
+its line has `value` null.
 """
 import argparse
 import json
 import os
-import statistics
+import socket
+import subprocess
 import sys
 import time
 
@@ -36,15 +46,15 @@ import numpy as np  # noqa: E402
 import torch  # noqa: E402
 import torch.distributed as dist  # noqa: E402
 
+METRIC = 'fused tri-modal samples/sec @ batch 256; per-modality logits max-abs-err'
 # Algorithmic work (BASELINE.md "Work per unit")
 FLOP_PER_SAMPLE = {'text': 2 * 11_174_221_056, 'image': 2 * 4_088_188_416, 'speech': 2 * 463_296,
                    'fusion': 2 * 2_020_000}
 # MI355X_MICROARCH.md: dense f16 MFMA ~2.5 PF; f32-input MFMA 157.3 TF (= the f32 vector peak)
 PEAK_TFLOPS = {'f16': 2500.0, 'fp32': 157.3}
 DTYPE = {'f16': 'f16 MFMA operands / fp32 accumulate, LN & softmax & residual fp32; speech+fusion fp32',
-         'fp32': 'fp32 (v_mfma_f32_32x32x2_f32 exact-f32 GEMMs; every operand and product fp32)'}
-# rows of the timed batch the oracle recomputes: batch edges, tile edges and a spread
-PARITY_ROWS = [0, 1, 63, 64, 100, 127, 128, 129, 170, 191, 200, 230, 254, 255]
+         'fp32': 'fp32 (exact-f32 MFMA GEMMs; every operand and product fp32)'}
+ROW = 34  # packed result row: 3x7 modality probs | 7 fused probs | 3 attention | 3 decision weights
 
 
 def tile_name(tile: int, M: int) -> str:
@@ -70,7 +80,7 @@ def tile_name_f32(tile: int, M: int) -> str:
     return f'gemm_f32_kernel<{bm}x{bn}x32, {mf}> grid={((M + bm - 1) // bm) * (3072 // bn)}'
 
 
-def parse():
+def parse(argv=None):
     ap = argparse.ArgumentParser()
     ap.add_argument('--gpus', type=int, default=1)
     ap.add_argument('--steps', type=int, default=10)
@@ -79,7 +89,9 @@ def parse():
     ap.add_argument('--precision', default='both', choices=['both', 'f16', 'fp32'])
     ap.add_argument('--no-cpu-baseline', action='store_true')
     ap.add_argument('--no-parity', action='store_true')
-    ap.add_argument('--cpu-batch', type=int, default=32, help='fused samples per CPU-oracle run')
+    ap.add_argument('--oracle-rows', type=int, default=256,
+                    help='check every row of the batch against the oracle up to this batch size; '
+                         'beyond it, rows from every quarter (parity_rows)')
     ap.add_argument('--serial', action='store_true', help='run the encoders on one stream (A/B of the concurrency)')
     ap.add_argument('--no-pipeline', action='store_true',
                     help="run each batch's fusion on the main stream (A/B of the cross-batch overlap)")
@@ -87,7 +99,51 @@ def parse():
     ap.add_argument('--text-priority', type=int, default=1, help='0: BERT on the default-priority stream (A/B)')
     ap.add_argument('--image-priority', type=int, default=0,
                     help='1: speech + image stream at high priority, BERT at normal (A/B)')
-    return ap.parse_args()
+    ap.add_argument('--stub', action='store_true',
+                    help='CPU stub step over gloo (launcher / gather check; automatic with no GPU visible)')
+    ap.add_argument('--json-out', default=None, help='also write the result line to this file (rank 0)')
+    return ap.parse_args(argv)
+
+
+# ----------------------------------------------------------------------------- launcher
+
+
+def _free_port() -> int:
+    s = socket.socket()
+    s.bind(('127.0.0.1', 0))
+    p = s.getsockname()[1]
+    s.close()
+    return p
+
+
+def launch(a, argv) -> int:
+    """--gpus N > 1 without WORLD_SIZE: run N ranks through torch.distributed.run as a CHILD
+    process (never exec: this process has not touched the GPU, and must not replace itself)."""
+    cmd = [sys.executable, '-m', 'torch.distributed.run', '--nnodes=1', f'--nproc-per-node={a.gpus}',
+           '--master-addr', '127.0.0.1', f'--master-port={_free_port()}', os.path.abspath(__file__)] + list(argv)
+    env = dict(os.environ)
+    env.setdefault('HSA_ENABLE_IPC_MODE_LEGACY', '0')
+    return subprocess.run(cmd, env=env).returncode
+
+
+def parity_rows(B: int, limit: int):
+    """Rows the oracle recomputes: all of them up to `limit`; beyond, the batch edges, the
+    64/128/256-row tile edges of every quarter of the batch and a seeded spread (so rows
+    256..B-1 of a 1024-per-rank batch are covered)."""
+    if B <= limit:
+        return list(range(B))
+    rows = {0, 1, 2, B - 2, B - 1}
+    for q in range(4):
+        base = q * B // 4
+        for off in (0, 1, 63, 64, 127, 128, 255):
+            if base + off < B:
+                rows.add(base + off)
+    rng = np.random.default_rng(B)
+    rows.update(int(r) for r in rng.choice(B, size=min(B, 16), replace=False))
+    return sorted(rows)
+
+
+# ----------------------------------------------------------------------------- oracle side
 
 
 def host_cpus():
@@ -112,10 +168,11 @@ def host_cpus():
     return threads, (len(phys) or None), avail
 
 
-def cpu_baseline(batch: int):
-    """the CPU oracle (fp32 torch-CPU restatement of the reference arithmetic, our
-    'port') on a bounded fused batch: 2 warm-up runs, then the median of 5 timed runs, at
-    torch.set_num_threads(threads usable by this process)."""
+def oracle_run(x, ids, mask, gray, rows, timed: bool):
+    """The CPU oracle (fp32 torch-CPU / numpy restatement of the reference arithmetic) on `rows`
+    of the batch: per modality (feat, logits, probs) and the fused chain o_f(o_s, o_t, o_i)
+    (inference/multimodal_fusion.py:271-278). timed=True also returns the cpu_baseline record:
+    one warm-up pass on 2 rows, then ONE timed pass over all `rows`."""
     sys.path.insert(0, ROOT)
     from mec import synthetic as syn
     from oracle import fusion as o_f, image as o_i, speech as o_s, text as o_t
@@ -123,52 +180,80 @@ def cpu_baseline(batch: int):
     prev = torch.get_num_threads()
     torch.set_num_threads(threads)
     w = {k: syn.weights(k) for k in ('speech', 'text', 'image', 'fusion')}
-    x = syn.speech_inputs(batch, seed=0)
-    ids, mask = syn.text_inputs(batch, 128, seed=0)
-    gray = syn.image_inputs(batch, seed=0)
+    r = np.asarray(rows)
 
-    def one():
-        sf, _, sp = o_s.forward(w['speech'], x)
-        tf, _, tp = o_t.forward(w['text'], ids, mask)
-        imf, _, ip = o_i.forward(w['image'], gray)
-        o_f.forward(w['fusion'], sf, tf, imf, sp, tp, ip)
+    def chain(sel):
+        rs = o_s.forward(w['speech'], x[sel])
+        rt = o_t.forward(w['text'], ids[sel], mask[sel])
+        ri = o_i.forward(w['image'], gray[sel])
+        rf = o_f.forward(w['fusion'], rs[0], rt[0], ri[0], rs[2], rt[2], ri[2])
+        return {'speech': rs, 'text': rt, 'image': ri, 'fusion': rf}
 
-    for _ in range(2):
-        one()
-    ts = []
-    for _ in range(5):
+    cb = None
+    if timed:
+        chain(r[:2])
         t0 = time.perf_counter()
-        one()
-        ts.append(time.perf_counter() - t0)
+    ref = chain(r)
+    if timed:
+        el = time.perf_counter() - t0
+        cb = {'value': len(r) / el, 'unit': 'fused samples/s', 'cores': threads, 'kind': 'port',
+              'sample': f'one fused batch of {len(r)} samples (L=128 full rows, 48x48 u8) through oracle/ '
+                        f'fp32 torch-CPU, after a 2-sample warm-up ({el:.1f} s)',
+              'threads_note': 'torch threads = OMP_NUM_THREADS, the CPU share the GPU box gives one GPU '
+                              '(the host itself has more cores: host_physical_cores)',
+              'host_physical_cores': phys, 'host_logical_cpus_in_affinity': avail}
     torch.set_num_threads(prev)
-    med = statistics.median(ts)
-    return {'value': batch / med, 'unit': 'fused samples/s', 'cores': threads, 'kind': 'port',
-            'sample': f'fused batch of {batch} (L=128 full rows, 48x48 u8) through oracle/ fp32 torch-CPU, '
-                      f'median of 5 runs after 2 warm-ups ({med:.2f} s/run)',
-            'host_physical_cores': phys, 'host_logical_cpus_in_affinity': avail}
+    return ref, cb
 
 
-def parity(out, x, ids, mask, gray, rows):
-    """Oracle on `rows` of the timed batch: per modality logits / probs max-abs-err and argmax
-    agreement; fused end to end (the oracle fusion on the ORACLE encoders' outputs,
-    inference/multimodal_fusion.py:271-278)."""
+def parity(out, ref, rows):
+    """Per modality logits / probs max-abs-err, argmax agreement and at-risk rows against the
+    oracle outputs `ref` for `rows` of the timed batch; fusion = the end-to-end oracle chain."""
+    torch.cuda.synchronize()
+    idx = torch.as_tensor(rows, device=out['fusion'][1].device)
+    g = {k: [t.index_select(0, idx).cpu().numpy() for t in v] for k, v in out.items()}
+    res = {}
+    for name, (gl, gp), (rl, rp) in (('speech', g['speech'][1:3], ref['speech'][1:3]),
+                                      ('text', g['text'][1:3], ref['text'][1:3]),
+                                      ('image', g['image'][1:3], ref['image'][1:3]),
+                                      ('fusion', g['fusion'][0:2], ref['fusion'][0:2])):
+        perr = float(np.abs(gp - rp).max())
+        s = np.sort(rp, axis=1)
+        margin = s[:, -1] - s[:, -2]
+        res[name] = {'logits_max_abs_err': float(np.abs(gl - rl).max()), 'probs_max_abs_err': perr,
+                     'argmax_agree': f'{int((gp.argmax(1) == rp.argmax(1)).sum())}/{len(rows)}',
+                     'min_oracle_top2_margin': float(margin.min()),
+                     'at_risk_rows': int((margin < 2 * perr).sum())}
+    for k, j in (('attention_weights', 2), ('decision_weights', 3)):
+        res['fusion'][k + '_max_abs_err'] = float(np.abs(g['fusion'][j] - ref['fusion'][j]).max())
+    res['rows'] = (f'all {len(rows)} rows of the timed batch' if len(rows) == out['fusion'][1].shape[0]
+                   else f'{len(rows)} rows spread over the timed batch (first {rows[:4]}, last {rows[-3:]})')
+    res['fused_reference'] = 'end-to-end oracle chain o_f(o_s, o_t, o_i) (multimodal_fusion.py:271-278)'
+    return res
+
+
+def gather_check(gathered, world, B):
+    """Rank 0: two rows of every rank's shard in the gathered [world*B, 34] block against the
+    oracle run on that rank's own (seed = rank) inputs."""
     sys.path.insert(0, ROOT)
     from mec import synthetic as syn
-    from oracle import fusion as o_f, image as o_i, speech as o_s, text as o_t
-    torch.cuda.synchronize()
-    g = {k: [t[rows].cpu().numpy() for t in v] for k, v in out.items()}
-    rs = o_s.forward(syn.weights('speech'), x[rows])
-    rt = o_t.forward(syn.weights('text'), ids[rows], mask[rows])
-    ri = o_i.forward(syn.weights('image'), gray[rows])
-    rf = o_f.forward(syn.weights('fusion'), rs[0], rt[0], ri[0], rs[2], rt[2], ri[2])
-    res = {}
-    for name, (gl, gp), (rl, rp) in (('speech', g['speech'][1:3], rs[1:3]), ('text', g['text'][1:3], rt[1:3]),
-                                      ('image', g['image'][1:3], ri[1:3]), ('fusion', g['fusion'][0:2], rf[0:2])):
-        res[name] = {'logits_max_abs_err': float(np.abs(gl - rl).max()),
-                     'probs_max_abs_err': float(np.abs(gp - rp).max()),
-                     'argmax_agree': f'{int((gp.argmax(1) == rp.argmax(1)).sum())}/{len(rows)}'}
-    res['rows'] = f'{len(rows)} fixed rows of the timed batch; fusion = end-to-end oracle chain'
-    return res
+    errs, agree, n = [], 0, 0
+    for r in range(world):
+        x = syn.speech_inputs(B, seed=r)
+        ids, mask = syn.text_inputs(B, 128, seed=r, ragged=False)
+        gray = syn.image_inputs(B, seed=r)
+        sel = [0, B - 1]
+        ref, _ = oracle_run(x, ids, mask, gray, sel, timed=False)
+        want = np.concatenate([ref['speech'][2], ref['text'][2], ref['image'][2], ref['fusion'][1],
+                               ref['fusion'][2], ref['fusion'][3]], axis=1)
+        got = gathered[[r * B + s for s in sel]]
+        errs.append(float(np.abs(got - want).max()))
+        agree += int((got[:, 21:28].argmax(1) == want[:, 21:28].argmax(1)).sum())
+        n += len(sel)
+    return {'rows_per_rank': 2, 'ranks': world, 'max_abs_err_vs_oracle': max(errs), 'fused_argmax_agree': f'{agree}/{n}'}
+
+
+# ----------------------------------------------------------------------------- GPU run
 
 
 def per_config(pipe, dev, precision, iters=10):
@@ -185,7 +270,6 @@ def per_config(pipe, dev, precision, iters=10):
             'text_bert_b128': (128, lambda: pipe.text.forward(ids, mask))}
     # speech from waveforms (§8(f) row 4): GPU features (csrc/audio.hip) then the DNN, B = 32
     # clips of 3 s at 22050 Hz (config.py:57-58)
-    sys.path.insert(0, ROOT)
     af = engine.AudioFeaturizer(device=dev)
     wv = torch.from_numpy(np.random.default_rng(7).standard_normal((32, 66150)).astype(np.float32)).to(dev)
     runs['speech_waveform_b32'] = (32, lambda: pipe.speech.forward(af.forward(wv)))
@@ -210,29 +294,30 @@ def per_config(pipe, dev, precision, iters=10):
     with torch.cuda.stream(s):
         pipe.speech.forward(xs)
     torch.cuda.synchronize()
-    g = torch.cuda.CUDAGraph()
-    with torch.cuda.graph(g, stream=s):
+    gr = torch.cuda.CUDAGraph()
+    with torch.cuda.graph(gr, stream=s):
         for _ in range(20):
             pipe.speech.forward(xs)
-    g.replay()
+    gr.replay()
     torch.cuda.synchronize()
     e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
     e0.record()
     for _ in range(iters):
-        g.replay()
+        gr.replay()
     e1.record()
     torch.cuda.synchronize()
     ms = e0.elapsed_time(e1) / (iters * 20)
     out['speech_b32_graph'] = {'samples_per_s': 32 / ms * 1e3, 'ms_per_batch': ms}
-    del g
+    del gr
     mb.close()
     af.close()
     return out
 
 
-def run(a, precision, B, world, rank, dev):
-    """Time K pipelined steps at one precision; returns the result line (rank 0) or None."""
-    from mec import _lib, dist as mdist, engine, synthetic as syn
+def run(a, precision, B, world, rank, dev, inputs):
+    """Time K pipelined steps at one precision; returns (result line or None, last outputs,
+    gathered rows or None)."""
+    from mec import _lib, dist as mdist, engine
     # the product library: no probe build (probe option values skip work and return wrong
     # results), and every knob of the pipeline's handles at its default (handles own their knobs)
     # apart from the pipeline's own pin (BERT FFN2 on the ping-pong tile in the concurrent step)
@@ -241,10 +326,7 @@ def run(a, precision, B, world, rank, dev):
     pipe = engine.FusedPipeline(seed=1234, device=dev, concurrent=not a.serial, pipelined=not a.no_pipeline,
                                 text_priority=bool(a.text_priority), image_priority=bool(a.image_priority),
                                 precision=precision)
-    x_np = syn.speech_inputs(B, seed=rank)
-    ids_np, mask_np = syn.text_inputs(B, 128, seed=rank, ragged=False)
-    gray_np = syn.image_inputs(B, seed=rank)
-    x, ids, mask, gray = (engine.to_device(v, dev) for v in (x_np, ids_np, mask_np, gray_np))
+    x, ids, mask, gray = (engine.to_device(v, dev) for v in inputs)
     gather_ev = []
     last = {}
 
@@ -257,6 +339,7 @@ def run(a, precision, B, world, rank, dev):
             rows = mdist.all_gather_rows(rows, world * B)
             e1.record()
             gather_ev.append((e0, e1))
+        last['rows'] = rows
         return rows
 
     def step():
@@ -264,10 +347,13 @@ def run(a, precision, B, world, rank, dev):
 
     for _ in range(a.warmup):
         step()
+    # fence: every warm-up kernel (all streams) retires BEFORE the opening profiler marker, so a
+    # rocprofv3 window between the two markers holds exactly the timed steps' dispatches
+    torch.cuda.synchronize()
     gather_ev.clear()
     # hipEvent timing of the dominant kernel (BERT FFN1 GEMM) inside the timed region
     pipe.text.prof_enable('bert_ffn1')
-    torch.cuda._sleep(1)  # marker dispatch for tools/prof_summary.py --window spin (outside the timing)
+    torch.cuda._sleep(1)  # opening marker for tools/prof_summary.py --window spin (outside the timing)
     if world > 1:
         dist.barrier()
     torch.cuda.synchronize()
@@ -279,6 +365,7 @@ def run(a, precision, B, world, rank, dev):
     torch.cuda.synchronize()
     el = time.perf_counter() - t0
     torch.cuda._sleep(1)  # closing marker
+    pipe.check()  # an after-the-fact kernel error (mec_model_check) fails the run, never a silent NaN
     ffn_ms, ffn_n = pipe.text.prof_read()
     gather_ms = [e0.elapsed_time(e1) for e0, e1 in gather_ev]
     # the same kernel with BERT alone on the GPU (no concurrent image stream), untimed region
@@ -292,10 +379,11 @@ def run(a, precision, B, world, rank, dev):
     if world > 1:
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
     el = float(t.item())
+    gathered = last['rows'].cpu().numpy() if world > 1 else None
     if rank != 0:
         for m in pipe.models():
             m.close()
-        return None
+        return None, None, None
 
     M = B * 128
     peak = PEAK_TFLOPS[precision]
@@ -322,19 +410,21 @@ def run(a, precision, B, world, rank, dev):
             'frac': (achieved / peak) if achieved else None, 'traffic': traffic, 'traffic_source': tsrc,
             'algorithmic_flop_per_launch': ffn_flop,
             'algorithmic_bytes_per_launch': ebytes * (M * 768 + 3072 * 768 + M * 3072),
-            'avg_launch_ms': avg_s * 1e3, 'launches': ffn_n,
+            'avg_launch_ms': avg_s * 1e3, 'launches': ffn_n, 'launches_expected': 12 * a.steps,
             'note': 'achieved: live in the timed region (CUs shared with the image stream); '
                     'achieved_isolated: BERT alone',
             'achieved_isolated': iso, 'frac_isolated': (iso / peak) if iso else None}
     total = world * B * a.steps
     flop = sum(FLOP_PER_SAMPLE.values()) * total
     res = {
-        'metric': 'fused tri-modal samples/sec @ batch 256; per-modality logits max-abs-err',
+        'metric': METRIC,
         'value': total / el, 'unit': 'samples/s', 'n_gpus': world, 'steps': a.steps, 'warmup': a.warmup,
         'ms_per_step': el / a.steps * 1e3, 'higher_is_better': True, 'scaling': 'weak', 'vs_baseline': None,
         'dtype': DTYPE[precision], 'precision': precision,
         'data': 'synthetic (seeded inputs: 56-d features, 128-token ids, 48x48 u8; seeded synthetic weights)',
-        'config': {'workload': 'fused tri-modal: speech DNN + BERT-base L=128 + ResNet50@224 + attention fusion',
+        'config': {'workload': 'fused tri-modal: speech DNN + BERT-base L=128 + ResNet50@224 + attention fusion'
+                               + (' (BASELINE configs[3])' if world == 1 and B == 256 else
+                                  ' (BASELINE configs[4] per-rank shard)' if B == 1024 else ''),
                    'batch_per_gpu': B, 'global_batch': world * B, 'seq_len': 128,
                    'parallelism': f'dp{world} (sample-sharded, all-gather of 34-float rows)'},
         'achieved_tflops_whole_step': flop / el / 1e12,
@@ -345,39 +435,125 @@ def run(a, precision, B, world, rank, dev):
         res['distributed'] = {'world_size': dist.get_world_size(), 'backend': dist.get_backend(),
                               'rccl_version': '.'.join(map(str, torch.cuda.nccl.version())),
                               'all_gather_ms_per_step': (sum(gather_ms) / len(gather_ms)) if gather_ms else None,
-                              'all_gather_bytes_per_step': world * B * 34 * 4}
-    if not a.no_parity and 'out' in last:
-        rows = [r for r in PARITY_ROWS if r < B]
-        res['parity'] = parity(last['out'], x_np, ids_np, mask_np, gray_np, rows)
+                              'all_gather_bytes_per_step': world * B * ROW * 4}
     if world == 1 and not a.no_configs:
         res['per_config'] = per_config(pipe, dev, precision)
-    for m in pipe.models():
-        m.close()
-    return res
+    out = last.get('out')
+    return res, (out, pipe), gathered
 
 
-def main():
-    a = parse()
-    world = int(os.environ.get('WORLD_SIZE', '1'))
-    rank = int(os.environ.get('RANK', '0'))
-    local = int(os.environ.get('LOCAL_RANK', '0'))
+def main_gpu(a, world, rank, local):
+    from mec import synthetic as syn
     if world > 1:
         torch.cuda.set_device(local)
         dist.init_process_group('nccl', device_id=torch.device('cuda', local))
     dev = torch.device('cuda', local)
     torch.cuda.set_device(dev)
     B = a.batch or (256 if world == 1 else 1024)
+    inputs = (syn.speech_inputs(B, seed=rank), *syn.text_inputs(B, 128, seed=rank, ragged=False),
+              syn.image_inputs(B, seed=rank))
     precs = ['f16', 'fp32'] if a.precision == 'both' else [a.precision]
-    lines = [run(a, p, B, world, rank, dev) for p in precs]
+    lines, outs, gathered = {}, {}, {}
+    for p in precs:
+        res, o, gth = run(a, p, B, world, rank, dev, inputs)
+        lines[p], outs[p], gathered[p] = res, o, gth
     if rank == 0:
-        if world == 1 and not a.no_cpu_baseline:
-            cb = cpu_baseline(a.cpu_batch)
-            for r in lines:
-                r['cpu_baseline'] = cb
-        for r in lines:  # f16 (the fast path) first, then its fp32 same-precision counterpart
-            print(json.dumps(r), flush=True)
+        rows = parity_rows(B, a.oracle_rows)
+        need_oracle = not a.no_parity or (world == 1 and not a.no_cpu_baseline)
+        ref, cb = (oracle_run(*inputs, rows, timed=(world == 1 and not a.no_cpu_baseline))
+                   if need_oracle else (None, None))
+        for p in precs:
+            out, pipe = outs[p]
+            if not a.no_parity and out is not None:
+                lines[p]['parity'] = parity(out, ref, rows)
+                if world > 1:
+                    lines[p]['parity']['all_gather_rows'] = gather_check(gathered[p], world, B)
+            for m in pipe.models():
+                m.close()
+            if cb is not None:
+                lines[p]['cpu_baseline'] = cb
+        head = lines['fp32'] if 'fp32' in lines else lines[precs[0]]
+        if 'fp32' in lines and 'f16' in lines:
+            f = lines['f16']
+            head['f16_fast_path'] = {k: f[k] for k in ('value', 'unit', 'ms_per_step', 'dtype',
+                                                       'achieved_tflops_whole_step', 'whole_step_frac_of_peak',
+                                                       'roofline', 'parity', 'per_config', 'distributed') if k in f}
+        print(json.dumps(head), flush=True)
+        if a.json_out:
+            with open(a.json_out, 'w') as fh:
+                json.dump(head, fh)
+    if world > 1:
+        dist.barrier()
+        dist.destroy_process_group()
+
+
+# ----------------------------------------------------------------------------- CPU stub
+
+
+def stub_rows(lo: int, hi: int) -> torch.Tensor:
+    """Deterministic stand-in for the packed 34-float result rows of samples [lo, hi)."""
+    g = torch.arange(lo, hi, dtype=torch.float64)[:, None] * ROW + torch.arange(ROW, dtype=torch.float64)[None]
+    return torch.sin(g).float()
+
+
+def main_stub(a, world, rank):
+    """No GPU: the launcher, sharding, all-gather order and max-over-ranks timing over gloo."""
+    from mec import dist as mdist
+    if world > 1:
+        dist.init_process_group('gloo')
+    B = a.batch or (8 if world == 1 else 16)
+    rows = None
+    for i in range(a.warmup + a.steps):
+        if i == a.warmup:
+            if world > 1:
+                dist.barrier()
+            t0 = time.perf_counter()
+        lo, hi = mdist.shard(world * B, world, rank)
+        rows = stub_rows(lo, hi)
+        if world > 1:
+            rows = mdist.all_gather_rows(rows, world * B)
+    if world > 1:
+        dist.barrier()
+    el = time.perf_counter() - t0
+    t = torch.tensor([el], dtype=torch.float64)
+    if world > 1:
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+    ok = bool(torch.equal(rows, stub_rows(0, world * B)))
+    if rank == 0:
+        line = {'metric': METRIC, 'value': None, 'unit': 'samples/s', 'n_gpus': world, 'steps': a.steps,
+                'warmup': a.warmup, 'ms_per_step': float(t.item()) / max(a.steps, 1) * 1e3,
+                'higher_is_better': True, 'scaling': 'weak', 'vs_baseline': None, 'dtype': None,
+                'data': 'stub: no GPU visible, CPU stand-in rows', 'stub': True,
+                'config': {'workload': 'launcher / sharding / all-gather check (no encoders run)',
+                           'batch_per_gpu': B, 'global_batch': world * B,
+                           'parallelism': f'dp{world} (gloo)'},
+                'distributed': {'world_size': dist.get_world_size() if world > 1 else 1,
+                                'backend': dist.get_backend() if world > 1 else None,
+                                'gathered_rows_in_order': ok}}
+        print(json.dumps(line), flush=True)
+        if a.json_out:
+            with open(a.json_out, 'w') as fh:
+                json.dump(line, fh)
     if world > 1:
         dist.destroy_process_group()
+    if not ok:
+        raise SystemExit('bench.py stub: gathered rows out of order')
+
+
+def main(argv=None):
+    argv = sys.argv[1:] if argv is None else argv
+    a = parse(argv)
+    if 'WORLD_SIZE' not in os.environ and a.gpus > 1:
+        sys.exit(launch(a, argv))
+    world = int(os.environ.get('WORLD_SIZE', '1'))
+    rank = int(os.environ.get('RANK', '0'))
+    local = int(os.environ.get('LOCAL_RANK', '0'))
+    if a.stub or torch.cuda.device_count() == 0:  # device_count does not initialise the GPU
+        if not a.stub:
+            print('bench.py: no GPU visible -- running the CPU stub step (value null)', file=sys.stderr)
+        main_stub(a, world, rank)
+    else:
+        main_gpu(a, world, rank, local)
 
 
 if __name__ == '__main__':

@@ -135,7 +135,6 @@ int mec_conv_f32(const float* x, const float* w, const float* bias, const float*
  * default that handles created AFTERWARDS copy (and that the handle-less kernel entry points
  * use). Every pair of settings of one knob gives bit-identical outputs, except "fusion_r" 4 vs
  * 1|2 and "conv3x3_halo" 0 vs 1 (fp32 reassociation, both within the oracle tolerance).
- *   "gemm_impl" 1|[2]      register-staged / glds GEMM engine
  *   "gemm_bn" [0]|id       force one f16 GEMM tile (0 = autotune), "gemm_autotune" 0|[1]
  *   "gemm_bn_tag" tag*100000+id   force a tile for one launch class (e.g. 3 = BERT O-proj)
  *   "gemm_f32_tile" [0]|1..8  force one fp32 GEMM tile (0 = autotune; 5..8 = 1..4 on 16x16x4)
@@ -152,18 +151,15 @@ int mec_conv_f32(const float* x, const float* w, const float* bias, const float*
  *   "pw_chain_form" [0]|1|2  seam weight placement (LDS / registers)
  *   "bert_qkv_attn" 0|[1]  fused BERT QKV projection + attention
  *   "bert_ln_rows" 1|[2]|4  BERT LayerNorm rows per wave (all loads of a wave's rows in flight first)
- *   "bert_oproj_ln" [0]|1|3  BERT O-projection + residual + LayerNorm 1 in one full-row kernel
- *                          (1: Wo staged in LDS, 3: Wo read into registers; both measured slower)
  *   "resnet_chunk" [0]|n   ResNet layers 1-2 over n-image chunks
- *   "resnet_fused_tail" [0]|1, "mbv2_impl" [0]|1|2
+ *   "mbv2_impl" [0]|1|2    MobileNetV2 block form: 0 = time both per block shape, 1 = workgroup, 2 = wave
  *   "fusion_r" 1|2|[4]     samples per fusion workgroup
  *   "fusion_split" 0|[1]   fusion as 3 launches (per-modality projection, cross-attention, head)
- *   "speech_impl" [0]|1    speech DNN: 0 = layer-split launch (speech_flow_kernel, in-launch
- *                          hand-offs between 16-sample stages), 1 = one workgroup per 4 samples
  * Probe values, which skip work to time a kernel's parts and return WRONG results, exist only
  * in the -DMEC_PROBES build (libmec_hip_probes.so, `make probes`; tools/ only): "gemm_debug"
- * 1..5, "conv3x3_debug" / "stem_debug" 1|2|4|7, "bert_qkv_attn" 2|3, "bert_oproj_ln" 2|4,
- * "audio_debug" 1|2|4|8|15, "speech_debug" 1. The product library rejects them (-1). */
+ * 1..5, "conv3x3_debug" / "stem_debug" 1|2|4|7, "bert_qkv_attn" 2|3,
+ * "audio_debug" 1|2|4|8|15, "speech_debug" 1, "speech_spin_limit" >= 0 (the speech DNN's
+ * hand-off wait limit: forces expired waits). The product library rejects them (-1). */
 int mec_set_option(const char* key, int value);
 int mec_model_set_option(mec_model* m, const char* key, int value);
 
@@ -179,6 +175,14 @@ int mec_gemm_query(int amode, int M, int N, int K);
 int mec_gemm_f32_query(int amode, int M, int N, int K);
 /* The tile a handle's own autotuner chose for a shape it ran (its precision's engine); 0 = not seen. */
 int mec_model_gemm_query(mec_model* m, int amode, int M, int N, int K);
+
+/* Errors a kernel can only report after the fact, since the handle's last check: 0 = none,
+ * -1 = mec_last_error() says what (and the flag is cleared). Call once the stream that ran
+ * the handle's forwards has been synchronized. Speech: a stage hand-off wait of
+ * speech_flow_kernel expired (that forward's probs are NaN); no such condition exists for the
+ * other kinds (always 0). No reference counterpart: the reference's Keras predict has no
+ * asynchronous failure (inference/speech_inference.py:69). */
+int mec_model_check(mec_model* m);
 
 /* hipEvent timing hook: time every launch of kernel class `tag`. */
 int mec_prof_enable(mec_model* m, int tag);

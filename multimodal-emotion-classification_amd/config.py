@@ -34,3 +34,9 @@ class Config:
     # Build-only: seed for deterministic synthetic weights when no trained
     # checkpoint exists (the reference ships none: .gitignore:25-30).
     SYNTHETIC_SEED = os.environ.get('MEC_SYNTHETIC_SEED')
+
+    # Build-only: arithmetic of the drop-in classes' BERT / ResNet50 / MobileNetV2 forwards.
+    # 'fp32' (default) is the reference's own (inference/text_inference.py:91-93,
+    # inference/image_inference.py:116-118); 'f16' is the fast path (f16 MFMA operands, fp32
+    # accumulation; probs within 1e-3). Speech, fusion and audio are fp32 either way.
+    PRECISION = os.environ.get('MEC_PRECISION', 'fp32')

@@ -258,10 +258,9 @@ int mec_conv_f16(const void* x, const void* w, const float* bias, const void* R,
 
 namespace mec {
 // One knob of `o` (include/mec.h lists them). The probe-build values (*_debug, bert_qkv_attn
-// 2 | 3, bert_oproj_ln 2 | 4) return wrong results and exist only in -DMEC_PROBES builds.
+// 2 | 3, speech_spin_limit >= 0) return wrong results and exist only in -DMEC_PROBES builds.
 int set_option(Options& o, const std::string& k, int value) {
   const bool probe = kProbes;
-  if (k == "gemm_impl" && (value == 1 || value == 2)) { o.gemm_impl = value; return 0; }
   if (k == "fusion_r" && (value == 1 || value == 2 || value == 4)) { o.fusion_r = value; return 0; }
   if (k == "gemm_f32_family" && (value == 0 || value == 16 || value == 32)) {
     o.gemm_f32_family = value;
@@ -276,7 +275,7 @@ int set_option(Options& o, const std::string& k, int value) {
     return 0;
   }
   if (k == "fusion_split" && (value == 0 || value == 1)) { o.fusion_split = value; return 0; }
-  if (k == "speech_impl" && (value == 0 || value == 1)) { o.speech_impl = value; return 0; }
+  if (k == "speech_spin_limit" && (value == -1 || (probe && value >= 0))) { o.speech_spin_limit = value; return 0; }
   if (k == "gemm_debug" && (value == 0 || (probe && value >= 1 && value <= 5))) { o.gemm_debug = value; return 0; }
   if (k == "gemm_autotune" && (value == 0 || value == 1)) { o.gemm_autotune = value; return 0; }
   if (k == "gemm_f32_tile" && value >= 0 && value <= 8) { o.gemm_f32_tile = value; return 0; }
@@ -285,7 +284,6 @@ int set_option(Options& o, const std::string& k, int value) {
     return 0;
   }
   if (k == "gemm_prefetch_r" && (value == 0 || value == 1)) { o.gemm_prefetch_r = value; return 0; }
-  if (k == "resnet_fused_tail" && (value == 0 || value == 1)) { o.resnet_fused_tail = value; return 0; }
   if (k == "mbv2_impl" && value >= 0 && value <= 2) { o.mbv2_impl = value; return 0; }
   if (k == "conv3x3_direct" && (value == 0 || value == 1)) { o.conv3x3_direct = value; return 0; }
   if (k == "conv3x3_halo" && (value == 0 || value == 1)) { o.conv3x3_halo = value; return 0; }
@@ -293,10 +291,6 @@ int set_option(Options& o, const std::string& k, int value) {
   if (k == "resnet_chunk" && value >= 0) { o.resnet_chunk = value; return 0; }
   if (k == "bert_qkv_attn" && (value == 0 || value == 1 || (probe && (value == 2 || value == 3)))) {
     o.bert_qkv_attn = value;
-    return 0;
-  }
-  if (k == "bert_oproj_ln" && (value == 0 || value == 1 || value == 3 || (probe && (value == 2 || value == 4)))) {
-    o.bert_oproj_ln = value;
     return 0;
   }
   if (k == "stem_debug" && (value == 0 || (probe && (value == 1 || value == 2 || value == 4 || value == 7)))) {
@@ -391,6 +385,11 @@ int mec_prof_enable(mec_model* m, int tag) {
   m->impl->prof.tag = tag;
   m->impl->prof.reset();
   return 0;
+}
+
+int mec_model_check(mec_model* m) {
+  if (!m || !m->impl) { set_error("mec_model_check: null handle"); return -1; }
+  return m->impl->check();
 }
 
 int mec_prof_read(mec_model* m, double* total_ms, int* count) {

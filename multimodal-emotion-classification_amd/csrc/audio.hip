@@ -60,6 +60,7 @@ struct AudioTables {
   const float* chroma;    // [100][12][1025] float32 filterbanks, one per tuning bin
   int lo_bin, hi_bin;     // piptrack freq mask [lo, hi): 150 <= f < 4000
   int n_mfcc;
+  double sr;              // sample rate (piptrack's pitch = (bin + shift) * sr / n_fft)
 };
 
 __device__ __forceinline__ int bitrev10(int x) { return (int)(__builtin_bitreverse32((unsigned)x) >> 22); }
@@ -229,7 +230,7 @@ __global__ __launch_bounds__(256) void audio_frame_kernel(const float* __restric
       const float bb = (s2 - s0) / 2.f;
       const float shift = fabsf(bb) >= fabsf(a) ? 0.f : -bb / a;
       const float dskew = (0.5f * bb) * shift;  // 0.5 * np.gradient * shift
-      const float pitch = (float)((((double)k + (double)shift) * 22050.0) / (double)A_NFFT);
+      const float pitch = (float)((((double)k + (double)shift) * tb.sr) / (double)A_NFFT);
       const int slot = atomicAdd(&ncand, 1);
       if (slot < A_CMAX) cand[fr * A_CMAX + slot] = make_float2(pitch, s1 + dskew);
     }
@@ -774,6 +775,11 @@ int AudioModel::create(const float* blob, size_t n) {
     if (150.0 <= freq[k] && freq[k] < std::min(4000.0, (double)sr / 2)) { lo = std::min(lo, k); hi = std::max(hi, k + 1); }
   lo_bin = std::max(lo, A_BAND_LO);
   hi_bin = std::min(hi, A_BAND_HI);
+  // a frame's peaks are local maxima of the band (no two adjacent bins), so at most
+  // ceil(band / 2) of them; the per-frame peak list holds A_CMAX (sr >= ~21.6 kHz)
+  MEC_REQUIRE((hi_bin - lo_bin + 1) / 2 <= A_CMAX,
+              "audio: sample_rate too low for the per-frame peak list (piptrack band 150-4000 Hz holds more than "
+              "184 local maxima below ~21.6 kHz); resample to Config.SAMPLE_RATE (22050) first");
   // one device block: doubles first (8-B alignment), then ints / floats
   off_hann = 0;
   off_tw = off_hann + A_NFFT * 8;
@@ -832,6 +838,7 @@ int AudioModel::forward(const float* wave, int B, int L, float* feat, float* tun
   tb.lo_bin = lo_bin;
   tb.hi_bin = hi_bin;
   tb.n_mfcc = n_mfcc;
+  tb.sr = (double)sr;
   MEC_TRY(prof.begin(TAG_AUDIO, s));
 #ifdef MEC_PROBES
   switch (opt().audio_debug) {

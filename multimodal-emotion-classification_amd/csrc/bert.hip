@@ -463,287 +463,6 @@ __global__ __launch_bounds__(512, 1) void bert_qkv_attn_kernel(const f16* __rest
 }
 
 
-// ----------------------------------------------------------------------------- O-proj + LN1
-// The attention output projection, its residual add and LayerNorm 1 in one kernel: a
-// full-row tile (64 tokens x all 768 features) so the row statistics never leave the CU.
-//   t32 = (ctx16 . Wo^T + bo) + R          R = h32, or the deferred LN2 of the previous layer
-//   h16 = f16(fma((t32 - mean) * rstd, g1, b1)),  st1 = (mean, rstd)     (eps 1e-12)
-// Unfused this is the O-proj GEMM (f32 t32 out) plus bert_layernorm_kernel, which re-reads
-// the 100-MB t32 (B = 256). 8 waves, wave w owns features 96w..96w+95 of all 64 tokens
-// (acc[4][6] 16x16 blocks, out^T = Wo . ctx^T so a lane holds 4 consecutive features of one
-// token); K = 768 in 32-deep stages of 64 A rows + 768 B rows staged by global_load_lds
-// (64-B rows, chunk kc at kc ^ ((row >> 1) & 3)), two stages (2 x 52 KB of LDS).
-// The row mean/variance are two-pass like the LN kernel's, but summed in a different order,
-// so h16/st1 agree with the unfused pair to rounding, not bit for bit.
-// Measured slower than the pair (122 vs 87 + 27 us at B = 256), so off by default: the
-// 64-B stage rows halve the L2 -> LDS DMA efficiency (main loop alone 69 us, 2 rounds of
-// 256 CUs), and at one 8-wave block per CU (256 VGPRs per lane for the 64 x 96 wave tile)
-// the 490-KB HBM epilogue of every block runs in lockstep with nothing to overlap it.
-constexpr int OL_BM = 64, OL_BK = 32, OL_NK = BH / OL_BK, OL_ROWS = OL_BM + BH;
-constexpr int OL_STAGE = OL_ROWS * OL_BK;  // halfs per stage
-constexpr int OL_PIECES = OL_ROWS / 16;    // 16-row global_load_lds pieces per stage (52)
-
-__device__ __forceinline__ int olswz(int row, int kc) { return kc ^ ((row >> 1) & 3); }
-
-// RST: the residual is the previous layer's deferred LN2 (else h32 as is); DBG 1: probe build
-// that stops after the main loop (wrong results)
-template <bool RST, int DBG = 0, bool BD = false>
-__global__ __launch_bounds__(512, 1) void bert_oproj_ln_kernel(const f16* __restrict__ ctx,
-                                                               const f16* __restrict__ wo,
-                                                               const float* __restrict__ bo,
-                                                               const float* __restrict__ R,
-                                                               const float2* __restrict__ r_stats,
-                                                               const float* __restrict__ r_g,
-                                                               const float* __restrict__ r_b,
-                                                               const float* __restrict__ g1,
-                                                               const float* __restrict__ b1,
-                                                               float* __restrict__ t32, f16* __restrict__ h16,
-                                                               float2* __restrict__ st1) {
-  __shared__ __attribute__((aligned(16))) f16 smem[BD ? 3 * OL_BM * 64 : 2 * OL_STAGE];
-  __shared__ float red[8][OL_BM];
-  __shared__ __attribute__((aligned(16))) float sPar[5][BH];  // bo, r_g, r_b, g1, b1
-  typedef __attribute__((address_space(3))) void* lds_p;
-  const int tid = threadIdx.x, lane = tid & 63;
-  const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
-  const int l16 = lane & 15, lq = lane >> 4;
-  const int m0 = blockIdx.x * OL_BM;
-  // per-feature epilogue parameters into LDS once (visible after the main loop's barriers),
-  // so the epilogue's only global loads are the residual rows
-  for (int t = tid; t < 5 * BH / 4; t += 512) {
-    const int a = t / (BH / 4), c = (t - a * (BH / 4)) * 4;
-    const float* src = a == 0 ? bo : a == 1 ? r_g : a == 2 ? r_b : a == 3 ? g1 : b1;
-    float4 v = make_float4(0.f, 0.f, 0.f, 0.f);
-    if (RST || (a != 1 && a != 2)) v = *reinterpret_cast<const float4*>(src + c);
-    *reinterpret_cast<float4*>(&sPar[a][c]) = v;
-  }
-
-  floatx4 acc[4][6];
-#pragma unroll
-  for (int i = 0; i < 4; ++i)
-#pragma unroll
-    for (int j = 0; j < 6; ++j) acc[i][j] = floatx4{0.f, 0.f, 0.f, 0.f};
-  if constexpr (BD) {
-    // Direct-B form: only the A tile (64 tokens x 64 k, 128-B rows, aswz chunks, 3 stages,
-    // one 1-KB DMA piece per wave) goes through LDS. Wave w's Wo rows 96w..96w+95 are private
-    // to it, so they go L2 -> VGPRs one K step ahead (two register sets), each lane reading
-    // 32 contiguous bytes per row (4 lanes = one 128-B line). The k order inside a 64-deep
-    // step is permuted (lane lq, half s2 <-> k 16lq + 8s2 .. +7) identically for A and B.
-    constexpr int NK = BH / 64;
-    const int arow = wave * 8 + (lane >> 3), ach = lane & 7;
-    const uint32_t aoff = (uint32_t)((m0 + arow) * BH + aswz(arow, ach) * 8);
-    auto issueA = [&](int kt, int st) {
-      __builtin_amdgcn_global_load_lds((const void*)(ctx + aoff + kt * 64), (lds_p)(smem + st * (OL_BM * 64) + wave * 512),
-                                       16, 0, 0);
-    };
-    const f16* wrow = wo + (size_t)(96 * wave + l16) * BH + lq * 16;
-    half8 bb[2][6][2];
-    auto loadB = [&](int set, int kt) {
-#pragma unroll
-      for (int j = 0; j < 6; ++j)
-#pragma unroll
-        for (int s2 = 0; s2 < 2; ++s2)
-          bb[set][j][s2] = *reinterpret_cast<const half8*>(wrow + (size_t)j * 16 * BH + kt * 64 + s2 * 8);
-    };
-    issueA(0, 0);
-    loadB(0, 0);
-    issueA(1, 1);
-#pragma unroll
-    for (int kt = 0; kt < NK; ++kt) {
-      // outstanding in issue order: A(kt), B(kt) x12, A(kt+1)
-      if (kt + 1 < NK)
-        asm volatile("s_waitcnt vmcnt(1)" ::: "memory");
-      else
-        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-      __builtin_amdgcn_s_barrier();  // A stage kt landed for every wave; stage kt-1 is free
-      if (kt + 1 < NK) loadB((kt + 1) & 1, kt + 1);
-      if (kt + 2 < NK) issueA(kt + 2, (kt + 2) % 3);
-      const f16* sA = smem + (kt % 3) * (OL_BM * 64);
-#pragma unroll
-      for (int s2 = 0; s2 < 2; ++s2) {
-        half8 af[4];
-#pragma unroll
-        for (int i = 0; i < 4; ++i) {
-          const int r = 16 * i + l16;
-          af[i] = *reinterpret_cast<const half8*>(sA + r * 64 + aswz(r, 2 * lq + s2) * 8);
-        }
-#pragma unroll
-        for (int i = 0; i < 4; ++i)
-#pragma unroll
-          for (int j = 0; j < 6; ++j)
-            acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_f16(bb[kt & 1][j][s2], af[i], acc[i][j], 0, 0, 0);
-      }
-    }
-    __syncthreads();
-  } else {
-    // piece p = it * 8 + wave covers stage rows 16p .. 16p+15; lane -> (row lane>>2, chunk lane&3)
-    const int lrow = lane >> 2, pch = lane & 3;
-    const bool extra = wave < OL_PIECES - 48;  // 52 pieces: waves 0-3 load a 7th
-    // a 16-row piece is all A (pieces 0-3: it 0 on waves 0-3) or all B, so the source base is
-    // wave-uniform and each lane keeps a 32-bit element offset per piece (no 64-bit pointers)
-    const f16* src_it0 = wave < OL_BM / 16 ? ctx : wo;
-    uint32_t off[7];
-  #pragma unroll
-    for (int it = 0; it < 7; ++it) {
-      const int Rw = (it * 8 + wave) * 16 + lrow;
-      const int c = olswz(Rw, pch);
-      off[it] = Rw < OL_BM ? (uint32_t)((m0 + Rw) * BH + c * 8)
-                           : (uint32_t)((Rw < OL_ROWS ? Rw - OL_BM : 0) * BH + c * 8);
-    }
-    auto issue = [&](int kt, int st) {
-      f16* base = smem + st * OL_STAGE;
-  #pragma unroll
-      for (int it = 0; it < 6; ++it)
-        __builtin_amdgcn_global_load_lds((const void*)((it == 0 ? src_it0 : wo) + off[it] + kt * OL_BK),
-                                         (lds_p)(base + (it * 8 + wave) * 16 * OL_BK), 16, 0, 0);
-      if (extra)
-        __builtin_amdgcn_global_load_lds((const void*)(wo + off[6] + kt * OL_BK),
-                                         (lds_p)(base + (48 + wave) * 16 * OL_BK), 16, 0, 0);
-    };
-
-    issue(0, 0);
-    issue(1, 1);
-  #pragma unroll 1
-    for (int kt = 0; kt < OL_NK; ++kt) {
-      if (kt + 1 < OL_NK) {
-        if (extra)
-          asm volatile("s_waitcnt vmcnt(7)" ::: "memory");
-        else
-          asm volatile("s_waitcnt vmcnt(6)" ::: "memory");
-      } else {
-        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-      }
-      __builtin_amdgcn_s_barrier();  // stage kt landed for every wave
-      const f16* sA = smem + (kt & 1) * OL_STAGE;
-      half8 af[4], bf[6];
-  #pragma unroll
-      for (int i = 0; i < 4; ++i) {
-        const int r = 16 * i + l16;
-        af[i] = *reinterpret_cast<const half8*>(sA + r * OL_BK + olswz(r, lq) * 8);
-      }
-  #pragma unroll
-      for (int j = 0; j < 6; ++j) {
-        const int rr = OL_BM + 96 * wave + 16 * j + l16;
-        bf[j] = *reinterpret_cast<const half8*>(sA + rr * OL_BK + olswz(rr, lq) * 8);
-      }
-      __builtin_amdgcn_sched_barrier(0);
-      asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
-      __builtin_amdgcn_s_barrier();  // every wave is done reading stage kt
-      if (kt + 2 < OL_NK) issue(kt + 2, kt & 1);
-      __builtin_amdgcn_sched_barrier(0);
-  #pragma unroll
-      for (int i = 0; i < 4; ++i)
-  #pragma unroll
-        for (int j = 0; j < 6; ++j)
-          acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_f16(bf[j], af[i], acc[i][j], 0, 0, 0);
-    }
-  }
-
-  if constexpr (DBG == 1) {
-    float t = 0.f;
-#pragma unroll
-    for (int i = 0; i < 4; ++i)
-#pragma unroll
-      for (int j = 0; j < 6; ++j) t += acc[i][j][0] + acc[i][j][1] + acc[i][j][2] + acc[i][j][3];
-    if (t == 12345.678f) h16[tid] = (f16)t;
-    return;
-  }
-  // ---- epilogue: v = (acc + bo) + R' kept in acc; row sums over 8 waves through LDS.
-  // Every residual load of the lane (24 float4) is issued before the first is consumed.
-  float4 r4[4][6];
-#pragma unroll
-  for (int i = 0; i < 4; ++i)
-#pragma unroll
-    for (int j = 0; j < 6; ++j)
-      r4[i][j] = *reinterpret_cast<const float4*>(R + (size_t)(m0 + 16 * i + l16) * BH + 96 * wave + 16 * j + 4 * lq);
-  float2 rst[4];
-  if constexpr (RST) {
-#pragma unroll
-    for (int i = 0; i < 4; ++i) rst[i] = r_stats[m0 + 16 * i + l16];
-  }
-  float s[4] = {0.f, 0.f, 0.f, 0.f};
-#pragma unroll
-  for (int j = 0; j < 6; ++j) {
-    const int n = 96 * wave + 16 * j + 4 * lq;
-    const float4 bv = *reinterpret_cast<const float4*>(&sPar[0][n]);
-    const float4 gv = *reinterpret_cast<const float4*>(&sPar[1][n]);
-    const float4 btv = *reinterpret_cast<const float4*>(&sPar[2][n]);
-    const float bb[4] = {bv.x, bv.y, bv.z, bv.w}, rg[4] = {gv.x, gv.y, gv.z, gv.w},
-                rb[4] = {btv.x, btv.y, btv.z, btv.w};
-#pragma unroll
-    for (int i = 0; i < 4; ++i) {
-      float rv[4] = {r4[i][j].x, r4[i][j].y, r4[i][j].z, r4[i][j].w};
-      if constexpr (RST) {
-#pragma unroll
-        for (int e = 0; e < 4; ++e) rv[e] = __builtin_fmaf((rv[e] - rst[i].x) * rst[i].y, rg[e], rb[e]);
-      }
-#pragma unroll
-      for (int e = 0; e < 4; ++e) {
-        const float v = (acc[i][j][e] + bb[e]) + rv[e];
-        acc[i][j][e] = v;
-        s[i] += v;
-      }
-    }
-  }
-  float mean[4], rstd[4];
-#pragma unroll
-  for (int i = 0; i < 4; ++i) {
-    s[i] += __shfl_xor(s[i], 16);
-    s[i] += __shfl_xor(s[i], 32);
-    if (lq == 0) red[wave][16 * i + l16] = s[i];
-  }
-  __syncthreads();
-#pragma unroll
-  for (int i = 0; i < 4; ++i) {
-    float t = 0.f;
-#pragma unroll
-    for (int w = 0; w < 8; ++w) t += red[w][16 * i + l16];
-    mean[i] = t * (1.0f / BH);
-  }
-  __syncthreads();  // red is reused for the variance
-  float q[4] = {0.f, 0.f, 0.f, 0.f};
-#pragma unroll
-  for (int j = 0; j < 6; ++j)
-#pragma unroll
-    for (int i = 0; i < 4; ++i)
-#pragma unroll
-      for (int e = 0; e < 4; ++e) {
-        const float d = acc[i][j][e] - mean[i];
-        q[i] += d * d;
-      }
-#pragma unroll
-  for (int i = 0; i < 4; ++i) {
-    q[i] += __shfl_xor(q[i], 16);
-    q[i] += __shfl_xor(q[i], 32);
-    if (lq == 0) red[wave][16 * i + l16] = q[i];
-  }
-  __syncthreads();
-#pragma unroll
-  for (int i = 0; i < 4; ++i) {
-    float t = 0.f;
-#pragma unroll
-    for (int w = 0; w < 8; ++w) t += red[w][16 * i + l16];
-    rstd[i] = 1.0f / sqrtf(t * (1.0f / BH) + 1e-12f);
-    if (wave == 0 && lq == 0) st1[m0 + 16 * i + l16] = make_float2(mean[i], rstd[i]);
-  }
-#pragma unroll
-  for (int j = 0; j < 6; ++j) {
-    const int n = 96 * wave + 16 * j + 4 * lq;
-    const float4 gv = *reinterpret_cast<const float4*>(&sPar[3][n]);
-    const float4 bv = *reinterpret_cast<const float4*>(&sPar[4][n]);
-    const float gg[4] = {gv.x, gv.y, gv.z, gv.w}, bb[4] = {bv.x, bv.y, bv.z, bv.w};
-#pragma unroll
-    for (int i = 0; i < 4; ++i) {
-      const size_t off = (size_t)(m0 + 16 * i + l16) * BH + n;
-      *reinterpret_cast<float4*>(t32 + off) = make_float4(acc[i][j][0], acc[i][j][1], acc[i][j][2], acc[i][j][3]);
-      half4 hv;
-#pragma unroll
-      for (int e = 0; e < 4; ++e) hv[e] = (f16)__builtin_fmaf((acc[i][j][e] - mean[i]) * rstd[i], gg[e], bb[e]);
-      *reinterpret_cast<half4*>(h16 + off) = hv;
-    }
-  }
-}
-
-
 // ----------------------------------------------------------------------------- model
 // prm layout per layer (floats): bqkv 2304 | bo 768 | ln1g 768 | ln1b 768 | bi 3072 | bo2 768 |
 // ln2g 768 | ln2b 768  => 9984 ; then head: WpT 768*768 | bp 768 | WcT 768*7 | bc 7
@@ -894,31 +613,7 @@ int TextModel::forward(const int32_t* ids, const int32_t* mask, int B, int L, fl
     // f32 stream ping-pong: O-proj reads h32 and writes t32, FFN2 reads t32 and writes h32,
     // so no GEMM reads its own output (a launch stays idempotent: the tile autotuner
     // re-runs candidates on the same buffers)
-    if (opt().bert_oproj_ln && M % OL_BM == 0) {
-      MEC_TRY(prof.begin(TAG_BERT_OPROJ, s));
-      if (first && opt().bert_oproj_ln == 3)
-        hipLaunchKernelGGL((bert_oproj_ln_kernel<false, 0, true>), dim3(M / OL_BM), dim3(512), 0, s, ctx16, wo, bo,
-                           h32, nullptr, nullptr, nullptr, g1, b1, t32, h16, st1);
-      else if (first)
-        hipLaunchKernelGGL(bert_oproj_ln_kernel<false>, dim3(M / OL_BM), dim3(512), 0, s, ctx16, wo, bo, h32,
-                           nullptr, nullptr, nullptr, g1, b1, t32, h16, st1);
-      else if (opt().bert_oproj_ln == 3)
-        hipLaunchKernelGGL((bert_oproj_ln_kernel<true, 0, true>), dim3(M / OL_BM), dim3(512), 0, s, ctx16, wo, bo, h32,
-                           st2, pg2, pg2 + BH, g1, b1, t32, h16, st1);
-#ifdef MEC_PROBES
-      else if (opt().bert_oproj_ln == 4)
-        hipLaunchKernelGGL((bert_oproj_ln_kernel<true, 1, true>), dim3(M / OL_BM), dim3(512), 0, s, ctx16, wo, bo, h32,
-                           st2, pg2, pg2 + BH, g1, b1, t32, h16, st1);
-      else if (opt().bert_oproj_ln == 2)
-        hipLaunchKernelGGL((bert_oproj_ln_kernel<true, 1>), dim3(M / OL_BM), dim3(512), 0, s, ctx16, wo, bo, h32, st2,
-                           pg2, pg2 + BH, g1, b1, t32, h16, st1);
-#endif
-      else
-        hipLaunchKernelGGL(bert_oproj_ln_kernel<true>, dim3(M / OL_BM), dim3(512), 0, s, ctx16, wo, bo, h32, st2,
-                           pg2, pg2 + BH, g1, b1, t32, h16, st1);
-      MEC_LAUNCH_CHECK();
-      MEC_TRY(prof.end(TAG_BERT_OPROJ, s));
-    } else {
+    {
       g = GemmParams();
       g.A = ctx16; g.B = wo; g.bias = bo; g.R = h32; g.r_f32 = 1; g.C32 = t32; g.M = M; g.N = BH; g.K = BH;
       if (!first) { g.r_stats = st2; g.r_g = pg2; g.r_b = pg2 + BH; }  // else: the embedding LN, written in full

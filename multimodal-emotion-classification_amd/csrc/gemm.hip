@@ -1,212 +1,17 @@
-// fp16-operand / fp32-accumulate MFMA GEMM for gfx950 — the first, register-staged engine
-// (128x128 tiles), kept selectable (mec_set_option("gemm_impl", 1)) as the A/B baseline of
-// gemm_glds.hip, which is the default. Two A-operand views:
+// f16-operand / fp32-accumulate GEMM dispatch for gfx950: routes each GEMM / implicit-GEMM
+// conv to the halo-tile 3x3 conv kernels (conv3x3.hip, conv3x3_halo.hip) where they apply, else
+// to the glds pipelined engine (gemm_glds.hip). A-operand views:
 //   A_PLAIN  A[M,K] row-major (BERT projections/FFN, ResNet 1x1 stride-1 convs)
 //   A_CONV   implicit im2col of an NHWC f16 tensor (ResNet 3x3 convs, strided 1x1
 //            downsample convs); K ordered (kh, kw, c), C % 64 == 0 so a 64-deep K tile
 //            never straddles two filter taps
-// B is the weight matrix [N,K] (K contiguous = torch Linear layout). Epilogue fuses
-// bias (folded BN shift), residual add, ReLU/GELU(erf), f16 and/or f32 stores.
-//
-// Tile: BM x BN x 64, 256 threads = 4 waves in 2x2, each wave (BM/2)x(BN/2) of
-// v_mfma_f32_32x32x16_f16. Double-buffered LDS, register-staged prefetch (one barrier
-// per K tile), XOR-swizzled 128-B rows (conflict-free ds_read_b128), XCD-aware block
-// remap so the blocks sharing an A panel share an L2.
+//   A_DUAL   [A | A2] concatenated along K (a bottleneck's conv3 + its downsample)
+// B is the weight matrix [N,K] (K contiguous = torch Linear layout).
 #include "mec_common.h"
 
 namespace mec {
 
 constexpr int GBK = 64;
-
-__device__ __forceinline__ int swz(int row, int kc) { return kc ^ ((row >> 1) & 7); }
-
-__device__ __forceinline__ float gelu_erf(float x) {
-  return x * 0.5f * (1.0f + erff(x * 0.70710678118654752440f));
-}
-
-template <int BM, int BN, int AM>
-__global__ __launch_bounds__(256, 2) void gemm_f16_kernel(const GemmParams p) {
-  constexpr int TILE_A = BM * GBK;
-  constexpr int TILE_B = BN * GBK;
-  constexpr int AI = BM / 32;
-  constexpr int BI = BN / 32;
-  constexpr int TI = BM / 64;
-  constexpr int TJ = BN / 64;
-  __shared__ __attribute__((aligned(16))) f16 smem[2 * (TILE_A + TILE_B)];
-
-  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
-  const int wm = wave >> 1, wn = wave & 1;
-  const int M = p.M, N = p.N, K = p.K;
-  const int nbn = N / BN;
-  const int nbm = (M + BM - 1) / BM;
-  const int nwg = nbm * nbn;
-  int bid = blockIdx.x;
-  {
-    const int xcd = bid & 7, q = nwg >> 3, r = nwg & 7;
-    bid = (xcd < r ? xcd * (q + 1) : r * (q + 1) + (xcd - r) * q) + (bid >> 3);
-  }
-  const int bm = bid / nbn, bn = bid - (bid / nbn) * nbn;
-  const int m0 = bm * BM, n0 = bn * BN;
-
-  const int kc = tid & 7;
-  const int rbase = tid >> 3;
-
-  // ---- per-thread A row state
-  const f16* a_plain[AI];
-  size_t a_img[AI];
-  int a_ih0[AI], a_iw0[AI];
-  bool a_in[AI];
-#pragma unroll
-  for (int i = 0; i < AI; ++i) {
-    const int m = m0 + rbase + 32 * i;
-    a_in[i] = m < M;
-    const int mc = a_in[i] ? m : (M - 1);
-    if constexpr (AM == A_PLAIN) {
-      a_plain[i] = reinterpret_cast<const f16*>(p.A) + (size_t)mc * K + kc * 8;
-    } else {
-      const int ohw = p.OH * p.OW;
-      const int n = mc / ohw;
-      const int rem = mc - n * ohw;
-      const int oh = rem / p.OW;
-      const int ow = rem - oh * p.OW;
-      a_ih0[i] = oh * p.stride - p.pad;
-      a_iw0[i] = ow * p.stride - p.pad;
-      a_img[i] = (size_t)n * p.H * p.W * p.C;
-    }
-  }
-  const f16* b_src[BI];
-#pragma unroll
-  for (int j = 0; j < BI; ++j) b_src[j] = p.B + (size_t)(n0 + rbase + 32 * j) * K + kc * 8;
-
-  uint4 ra[AI], rb[BI];
-
-  auto load_tile = [&](int kt) {
-    const int k0 = kt * GBK;
-    if constexpr (AM == A_PLAIN) {
-#pragma unroll
-      for (int i = 0; i < AI; ++i) {
-        uint4 v = *reinterpret_cast<const uint4*>(a_plain[i] + k0);
-        ra[i] = a_in[i] ? v : make_uint4(0, 0, 0, 0);
-      }
-    } else if constexpr (AM == A_CONV) {
-      const int tap = k0 / p.C;
-      const int c0 = k0 - tap * p.C;
-      const int kh = tap / p.ks;
-      const int kw = tap - kh * p.ks;
-      const f16* X = reinterpret_cast<const f16*>(p.A);
-#pragma unroll
-      for (int i = 0; i < AI; ++i) {
-        const int ih = a_ih0[i] + kh, iw = a_iw0[i] + kw;
-        const bool ok = a_in[i] && ih >= 0 && ih < p.H && iw >= 0 && iw < p.W;
-        const f16* src = X + a_img[i] + ((size_t)(ok ? ih : 0) * p.W + (ok ? iw : 0)) * p.C + c0 + kc * 8;
-        uint4 v = *reinterpret_cast<const uint4*>(src);
-        ra[i] = ok ? v : make_uint4(0, 0, 0, 0);
-      }
-    }
-#pragma unroll
-    for (int j = 0; j < BI; ++j) rb[j] = *reinterpret_cast<const uint4*>(b_src[j] + k0);
-  };
-
-  auto store_tile = [&](int buf) {
-    f16* sA = smem + buf * (TILE_A + TILE_B);
-    f16* sB = sA + TILE_A;
-#pragma unroll
-    for (int i = 0; i < AI; ++i) {
-      const int r = rbase + 32 * i;
-      *reinterpret_cast<uint4*>(sA + r * GBK + swz(r, kc) * 8) = ra[i];
-    }
-#pragma unroll
-    for (int j = 0; j < BI; ++j) {
-      const int r = rbase + 32 * j;
-      *reinterpret_cast<uint4*>(sB + r * GBK + swz(r, kc) * 8) = rb[j];
-    }
-  };
-
-  floatx16 acc[TI][TJ];
-#pragma unroll
-  for (int i = 0; i < TI; ++i)
-#pragma unroll
-    for (int j = 0; j < TJ; ++j)
-#pragma unroll
-      for (int e = 0; e < 16; ++e) acc[i][j][e] = 0.f;
-
-  const int nk = K / GBK;
-  load_tile(0);
-  store_tile(0);
-  __syncthreads();
-
-  const int lr = lane & 31, lh = lane >> 5;
-  for (int kt = 0; kt < nk; ++kt) {
-    const int cur = kt & 1;
-    if (kt + 1 < nk) load_tile(kt + 1);
-    const f16* sA = smem + cur * (TILE_A + TILE_B);
-    const f16* sB = sA + TILE_A;
-#pragma unroll
-    for (int s = 0; s < 4; ++s) {
-      const int kcs = 2 * s + lh;
-      half8 af[TI], bf[TJ];
-#pragma unroll
-      for (int i = 0; i < TI; ++i) {
-        const int r = wm * (BM / 2) + i * 32 + lr;
-        af[i] = *reinterpret_cast<const half8*>(sA + r * GBK + swz(r, kcs) * 8);
-      }
-#pragma unroll
-      for (int j = 0; j < TJ; ++j) {
-        const int r = wn * (BN / 2) + j * 32 + lr;
-        bf[j] = *reinterpret_cast<const half8*>(sB + r * GBK + swz(r, kcs) * 8);
-      }
-#pragma unroll
-      for (int i = 0; i < TI; ++i)
-#pragma unroll
-        for (int j = 0; j < TJ; ++j)
-          acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_f16(af[i], bf[j], acc[i][j], 0, 0, 0);
-    }
-    if (kt + 1 < nk) store_tile(cur ^ 1);
-    __syncthreads();
-  }
-
-  // ---- epilogue
-#pragma unroll
-  for (int j = 0; j < TJ; ++j) {
-    const int col = n0 + wn * (BN / 2) + j * 32 + lr;
-    const float bv = p.bias ? p.bias[col] : 0.f;
-#pragma unroll
-    for (int i = 0; i < TI; ++i) {
-#pragma unroll
-      for (int e = 0; e < 16; ++e) {
-        const int row = m0 + wm * (BM / 2) + i * 32 + (e & 3) + 8 * (e >> 2) + 4 * lh;
-        if (row < M) {
-          const size_t idx = (size_t)row * N + col;
-          float v = acc[i][j][e] + bv;
-          if (p.R && p.r_stats) {
-            const float2 st = p.r_stats[row];
-            v += __builtin_fmaf((reinterpret_cast<const float*>(p.R)[idx] - st.x) * st.y, p.r_g[col], p.r_b[col]);
-          } else if (p.R) {
-            v += p.r_f32 ? reinterpret_cast<const float*>(p.R)[idx] : (float)reinterpret_cast<const f16*>(p.R)[idx];
-          }
-          if (p.act == ACT_RELU) v = fmaxf(v, 0.f);
-          else if (p.act == ACT_GELU) v = gelu_erf(v);
-          else if (p.act == ACT_RELU6) v = fminf(fmaxf(v, 0.f), 6.f);
-          if (p.C16) p.C16[idx] = (f16)v;
-          if (p.C32) p.C32[idx] = v;
-        }
-      }
-    }
-  }
-}
-
-template <int BM, int BN>
-static int launch_mode(const GemmParams& p, hipStream_t s) {
-  const int nwg = ((p.M + BM - 1) / BM) * (p.N / BN);
-  dim3 grid(nwg), block(256);
-  switch (p.amode) {
-    case A_PLAIN: hipLaunchKernelGGL((gemm_f16_kernel<BM, BN, A_PLAIN>), grid, block, 0, s, p); break;
-    case A_CONV: hipLaunchKernelGGL((gemm_f16_kernel<BM, BN, A_CONV>), grid, block, 0, s, p); break;
-    default: set_error("bad amode"); return -1;
-  }
-  MEC_LAUNCH_CHECK();
-  return 0;
-}
 
 // Per launch class (profiling tag): forced tile id, 0 = autotune. The BERT O-projection
 // (32768 x 768 x 768, f32 deferred-LN residual) is pinned to 128 x 128: its candidates time
@@ -226,7 +31,6 @@ int launch_gemm(const GemmParams& p, hipStream_t s, Prof* prof, int tag) {
   } else if (p.amode == A_DUAL) {
     MEC_REQUIRE(p.A2 && p.K1 > 0 && p.K1 % 64 == 0 && p.C % 64 == 0 && p.K == p.K1 + p.C && p.ks == 1 && p.pad == 0,
                 "dual gemm: need K = K1 + C, K1 % 64 == 0, C % 64 == 0, 1x1 unpadded second source");
-    MEC_REQUIRE(opt().gemm_impl == 2, "dual gemm needs the glds engine");
   } else {
     MEC_REQUIRE(p.amode == A_PLAIN, "gemm: unknown A mode");
   }
@@ -239,10 +43,8 @@ int launch_gemm(const GemmParams& p, hipStream_t s, Prof* prof, int tag) {
            p.H == p.W && p.OH == p.H && p.OW == p.W && conv3x3_halo_supported(p.H, p.C, p.N) && p.act == ACT_RELU &&
            !p.R && p.bias && p.C16 && !p.C32 && p.M % (p.H * p.W) == 0)
     rc = launch_conv3x3_halo(reinterpret_cast<const f16*>(p.A), p.B, p.bias, p.C16, p.M / (p.H * p.W), p.H, p.C, s);
-  else if (opt().gemm_impl == 2)
-    rc = launch_gemm_glds(p, s, opt().gemm_bn ? opt().gemm_bn : (tag > 0 && tag < TAG_COUNT ? opt().gemm_bn_tag[tag] : 0));
   else
-    rc = (p.N % 128 == 0) ? launch_mode<128, 128>(p, s) : launch_mode<128, 64>(p, s);
+    rc = launch_gemm_glds(p, s, opt().gemm_bn ? opt().gemm_bn : (tag > 0 && tag < TAG_COUNT ? opt().gemm_bn_tag[tag] : 0));
   if (rc) return rc;
   if (prof) MEC_TRY(prof->end(tag, s));
   return 0;

@@ -260,8 +260,12 @@ static int launch_tile(const GemmParams& p, hipStream_t s, int id) {
 }
 
 // Cache key: engine 1 (this engine) + the shape, in the calling handle's tune_cache().
+// engine slot: 1 + the MFMA family allowed when the shape was tuned, so changing
+// gemm_f32_family on a handle never reuses a tile of the other family (other k order)
+static int f32_engine() { return 1 + opt().gemm_f32_family; }
+
 static std::array<int, 11> f32_key(const GemmParams& p) {
-  return {1, p.amode, p.M, p.N, p.K, p.H, p.W, p.C, p.ks, p.stride, p.pad};
+  return {f32_engine(), p.amode, p.M, p.N, p.K, p.H, p.W, p.C, p.ks, p.stride, p.pad};
 }
 
 // MFMA family allowed by opt().gemm_f32_family (0: both; 16: ids 5..8 on 16x16x4; 32: ids 1..4
@@ -304,7 +308,7 @@ static int tune_tile(const GemmParams& p, hipStream_t s, int* out) {
   return 0;
 }
 
-int gemm_f32_tuned(int amode, int M, int N, int K) { return tune_cache().find_shape(1, amode, M, N, K); }
+int gemm_f32_tuned(int amode, int M, int N, int K) { return tune_cache().find_shape(f32_engine(), amode, M, N, K); }
 
 int launch_gemm_f32(const GemmParams& p, hipStream_t s, Prof* prof, int tag) {
   MEC_REQUIRE(p.M > 0 && p.N > 0 && p.K > 0, "gemm_f32: empty shape");

@@ -67,10 +67,12 @@ enum KernelTag : int {
 // Tuning knobs (mec_set_option / mec_model_set_option, include/mec.h). Every model handle
 // owns a copy, taken from the process defaults when it is created, and kernels read the
 // options of the handle whose call they serve (opt()), so handles never perturb each other.
-// Every setting of a knob gives the same results, except the probe-build values (compiled only
-// with -DMEC_PROBES: they skip work to time a kernel's parts and return wrong results).
+// Every setting of a knob gives the same results bit for bit, with these exceptions:
+//   * conv3x3_halo 0 vs 1 and fusion_r 4 vs 1|2 sum in other fp32 orders (same values to
+//     rounding, not the same bits; include/mec.h);
+//   * the probe-build values (compiled only with -DMEC_PROBES: they skip work to time a
+//     kernel's parts and return wrong results).
 struct Options {
-  int gemm_impl = 2;        // 1 = register-staged 128x128 engine, 2 = glds pipelined engine
   int gemm_bn = 0;          // forced f16 GEMM tile id (0 = autotune)
   int gemm_autotune = 1;
   int gemm_prefetch_r = 1;  // f16 residual prefetch in short-K GEMMs
@@ -88,13 +90,11 @@ struct Options {
   int conv3x3_direct = 1;   // ResNet layer1 conv2 on the halo-tile kernel (conv3x3.hip)
   int conv3x3_halo = 1;     // layers 2-3 stride-1 conv2 on the halo kernel (conv3x3_halo.hip)
   int stem_gray_f32 = 1;    // fp32 gray stem as one conv + pool kernel (else im2col + GEMM + pool)
-  int resnet_fused_tail = 0;
   int resnet_chunk = 0;
   int pw_chain = 2;         // layer1 seam kernels (pw_chain.hip)
   int pw_chain_form = 0;
   int bert_qkv_attn = 1;    // fused BERT QKV projection + attention
   int bert_ln_rows = 2;     // BERT LayerNorm rows per wave (1 | 2 | 4): 27.0 / 25.7 / 26.3 us at B = 256
-  int bert_oproj_ln = 0;    // O-projection + residual + LayerNorm 1 in one kernel (1 | 3)
   int mbv2_impl = 0;
   // ping-pong GEMM tile order inside each XCD's contiguous tile range: 0 = row-major (all N
   // panels of one M panel in turn), G = groups of G M panels walked M-fastest, so the 32
@@ -103,8 +103,8 @@ struct Options {
   int gemm_group_m = 8;
   int fusion_r = 4;         // samples per fusion workgroup
   int fusion_split = 1;     // fusion as 3 launches
-  int speech_impl = 0;      // 0 = layer-split dataflow kernel (speech_flow_kernel), 1 = one WG per 4 samples
   int gemm_debug = 0, conv3x3_debug = 0, stem_debug = 0, audio_debug = 0, speech_debug = 0;  // probe builds only
+  int speech_spin_limit = -1;  // probe builds only: speech_flow_kernel wait limit (forces expired waits)
 };
 
 // GEMM autotuner results: tile id per (engine, shape), per handle.

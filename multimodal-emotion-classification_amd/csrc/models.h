@@ -23,6 +23,9 @@ struct Model {
   TuneCache tune;                    // this handle's GEMM autotune results
   Prof prof;
   virtual ~Model() {}
+  // errors a kernel could only report after the fact (mec_model_check): 0 = none since the last
+  // check. Call after the stream that ran the handle's forwards has been synchronized.
+  virtual int check() { return 0; }
 };
 
 // ---------------------------------------------------------------- speech DNN
@@ -30,11 +33,15 @@ struct SpeechModel : Model {
   DevBuf w;  // fp32: mean, scale, {W,b,inv,shift} x5, W6, b6
   size_t off_mean = 0, off_scale = 0, off_W[6] = {}, off_b[6] = {}, off_inv[5] = {}, off_shift[5] = {};
   // speech_flow_kernel: hand-off buffers of layers 0-3 (f32 [16 * chunks, N_l]) and the
-  // per-chunk arrival counters (zero between launches: the last stage resets them) + error word
+  // per-chunk arrival counters + the launch's error word (zeroed on the stream before every
+  // launch); host_err: host-mapped pinned flag a launch with an expired wait raises
   DevBuf flow_act, flow_sync;
   int flow_chunks = 0;
+  unsigned* host_err = nullptr;
+  ~SpeechModel() override;
   int create(const float* blob, size_t n);
   int forward(const float* x, int B, float* feat, float* logits, float* probs, hipStream_t s);
+  int check() override;
 };
 
 // ---------------------------------------------------------------- speech features (audio.hip)
@@ -155,9 +162,6 @@ struct MobileNetModel : ImageNet {
 };
 
 int resize_u8(const uint8_t* in, int B, int H, int W, uint8_t* out, int OH, int OW, hipStream_t s);
-// ResNet bottleneck conv2 + conv3 + residual + ReLU (stride-1 blocks, w = 64 @ 56 or 128 @ 28)
-int launch_bneck_tail(const f16* t1, const f16* x, const f16* w2, const float* b2, const f16* w3, const float* b3,
-                      f16* y, int B, int H, int w, hipStream_t s);
 // layer1 seam: conv3 (64 -> 256) + residual + ReLU, then the next block's conv1 (256 -> N2)
 int launch_pw_chain(const f16* t2, const f16* xin, const f16* w3, const float* b3, const f16* w1, const float* b1,
                     f16* xout, f16* t1, int M, int N2, hipStream_t s);

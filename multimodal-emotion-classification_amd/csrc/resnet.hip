@@ -10,11 +10,6 @@
 
 namespace mec {
 
-// mec_set_option("resnet_fused_tail", 0|1): layer1's stride-1 blocks through bottleneck.hip.
-// Off by default: bit-identical to the unfused path but slower at B=256 — 315 us per block
-// against 105 + 170 us for the conv2 and conv3 GEMMs (rocprofv3, tools/encoder_profile.py
-// --opt resnet_fused_tail=1). It moves fewer bytes (about 3 TB/s at 315 us) but runs one
-// 4-wave workgroup per CU, so LDS-read and barrier latency inside a tile is exposed.
 // Images per layer1-2 pass (0 = whole batch). Measured at B = 256 (tools/encoder_profile.py
 // --opt resnet_chunk=N): 0 -> 4.23-4.25 ms, 128 -> 4.38, 64 -> 4.44-4.49, 32 -> 5.08: the
 // smaller GEMMs lose more than the cache residency gains, so chunking is off.
@@ -585,15 +580,6 @@ int ImageModel::forward_u8(const uint8_t* img, int B, int H, int W, int C, float
         MEC_TRY(launch_gemm(g, s, &prof, TAG_RESNET_CONV1X1));
       }
       conv1_done = false;
-      if (!bk.has_ds && opt().resnet_fused_tail && wd == 64 && H == 56) {
-        // conv2 + conv3 + residual + ReLU in one kernel (bottleneck.hip)
-        MEC_TRY(prof.begin(TAG_RESNET_CONV3X3, s));
-        MEC_TRY(launch_bneck_tail(t1, in, Wt + bk.c2.w_off, P + bk.c2.b_off, Wt + bk.c3.w_off, P + bk.c3.b_off, out,
-                                  nb, H, wd, s));
-        MEC_TRY(prof.end(TAG_RESNET_CONV3X3, s));
-        std::swap(cur, other);
-        continue;
-      }
       g = GemmParams();
       g.amode = A_CONV; g.A = t1; g.B = Wt + bk.c2.w_off; g.bias = P + bk.c2.b_off; g.act = ACT_RELU; g.C16 = t2;
       g.M = nb * OH * OH; g.N = wd; g.K = 9 * wd;

@@ -22,58 +22,13 @@ struct SpeechW {
   const float* shift[5];
 };
 
-constexpr int SPEECH_R = 4;
-constexpr int SF_THREADS = 512;
-__constant__ int kSpeechDims[6] = {56, 512, 512, 256, 128, 64};
+constexpr int SF_THREADS = 512;  // fusion kernels
 
-__global__ __launch_bounds__(512) void speech_kernel(SpeechW w, const float* __restrict__ x, int B,
-                                                     float* feat, float* logits, float* probs) {
-  constexpr int R = SPEECH_R, LD = 512;
-  __shared__ __attribute__((aligned(16))) float bufA[R * LD], bufB[R * LD], red[4 * R * SF_THREADS];
-  const int tid = threadIdx.x;
-  const int r0 = blockIdx.x * R;
-  const int nr = min(R, B - r0);
-  for (int idx = tid; idx < R * 56; idx += blockDim.x) {
-    const int r = idx / 56, k = idx - r * 56;
-    // sklearn StandardScaler.transform: (X - mean_) / scale_
-    bufA[r * LD + k] = r < nr ? (x[(size_t)(r0 + r) * 56 + k] - w.mean[k]) / w.scale[k] : 0.f;
-  }
-  __syncthreads();
-  float* in = bufA;
-  float* out = bufB;
-  for (int l = 0; l < 5; ++l) {
-    const int K = kSpeechDims[l], N = kSpeechDims[l + 1];
-    block_linear<R>(in, LD, K, w.W[l], N, w.b[l], N, out, LD, red, BACT_NONE);
-    for (int idx = tid; idx < R * N; idx += blockDim.x) {
-      const int r = idx / N, n = idx - r * N;
-      // tf.nn.batch_normalization: x * inv + (beta - mean * inv), inv = rsqrt(var+eps)*gamma
-      const float v = out[r * LD + n] * w.inv[l][n] + w.shift[l][n];
-      out[r * LD + n] = fmaxf(v, 0.f);
-    }
-    __syncthreads();
-    float* t = in; in = out; out = t;
-  }
-  for (int idx = tid; idx < nr * 64; idx += blockDim.x) {
-    const int r = idx / 64, n = idx - r * 64;
-    feat[(size_t)(r0 + r) * 64 + n] = in[r * LD + n];
-  }
-  block_linear<R>(in, LD, 64, w.W[5], 7, w.b[5], 7, out, LD, red, BACT_NONE);
-  for (int idx = tid; idx < nr * 7; idx += blockDim.x) {
-    const int r = idx / 7, n = idx - r * 7;
-    logits[(size_t)(r0 + r) * 7 + n] = out[r * LD + n];
-  }
-  __syncthreads();
-  block_softmax_small<R>(out, LD, 7, nullptr, 0);
-  for (int idx = tid; idx < nr * 7; idx += blockDim.x) {
-    const int r = idx / 7, n = idx - r * 7;
-    probs[(size_t)(r0 + r) * 7 + n] = out[r * LD + n];
-  }
-}
-
-// ---- speech_flow_kernel: the same network with every layer split by output columns over
+// ---- speech_flow_kernel: the network with every layer split by output columns over
 // workgroups, so each weight byte is read by one workgroup per 16-sample chunk instead of
-// by every workgroup (speech_kernel streams all 1.85 MB of weights through each CU, which
-// bounds it at ~40 us for any batch). Per chunk of 16 samples, five stages:
+// by every workgroup (a one-workgroup-per-4-samples form streamed all 1.85 MB of weights
+// through each CU, which bounded it at ~40 us for any batch). Per chunk of 16 samples, five
+// stages:
 //   stage 0  L0  56->512   8 WGs x 64 columns (4 waves = 4 column tiles, K 56 padded to 64)
 //   stage 1  L1 512->512  32 WGs x 16 columns (4 waves = 4 K quarters, summed in LDS)
 //   stage 2  L2 512->256  16 WGs x 16 columns
@@ -87,9 +42,11 @@ __global__ __launch_bounds__(512) void speech_kernel(SpeechW w, const float* __r
 // per-stage counter; the consumer polls that counter with one lane (sc1 dword loads + s_sleep)
 // and every wave reads its inputs with sc1 loads. Blocks are numbered stage-major, so every
 // producer precedes its consumers in dispatch order; every spin is bounded (an expired wait
-// sets the sticky error word and the stage proceeds; the chunk's probs then come out NaN).
-// The last stage of a chunk resets the chunk's counters: by then every wait on them is over
-// (each stage arrives only after its own wait and reads). Measured hop on MI355X, B = 32:
+// sets the launch's error word and the stage proceeds; the chunk's probs then come out NaN,
+// and the last stage raises the handle's host-visible error flag, which mec_model_check
+// reports). The counters and the error word are zeroed by a memset on the stream before
+// every launch, so an expired wait (whose late producer may still arrive after the chunk's
+// last stage) never leaks a count or an error into the next launch. Measured hop on MI355X, B = 32:
 // ~1.9 us from the last arrival to the wait's exit, ~1.2 us for the sc1 input loads.
 // (Tagged 8-B granules polled directly, with or without the counter, measured no faster at
 // B = 32 and up to 2x slower at B = 256, where 1,040 polling blocks flood the memory system.)
@@ -104,8 +61,10 @@ __host__ __device__ constexpr int spf_groups(int st) {
 struct SpeechFlow {
   float* act[4];               // stage outputs, f32 [16 * chunks, N_l]
   unsigned* cnt;               // [chunks][4] arrival counters, SPF_LINE apart
-  unsigned* err;               // sticky: a wait expired
+  unsigned* err;               // this launch: a wait expired
+  unsigned* host_err;          // host-mapped pinned flag of the handle (mec_model_check)
   int chunks;
+  int spin_limit;              // SPF_SPIN_LIMIT (probe builds: option speech_spin_limit)
 };
 
 typedef float f32x4 __attribute__((ext_vector_type(4)));
@@ -187,7 +146,7 @@ __device__ __forceinline__ void spf_stage(const SpeechW& w, const SpeechFlow& f,
       const unsigned* c = f.cnt + (size_t)(chunk * 4 + ST - 1) * SPF_LINE;
       for (int spins = 0; __hip_atomic_load(c, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) < spf_groups(ST - 1);) {
         __builtin_amdgcn_s_sleep(1);
-        if (++spins > SPF_SPIN_LIMIT) {
+        if (++spins > f.spin_limit) {
           __hip_atomic_fetch_or(f.err, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
           break;
         }
@@ -263,9 +222,6 @@ __device__ __forceinline__ void spf_stage(const SpeechW& w, const SpeechFlow& f,
   } else {
     __syncthreads();
     stamp(4);
-    if (tid == 0)  // every wait of this chunk is over: reset its counters for the next launch
-      for (int s = 0; s < 4; ++s)
-        __hip_atomic_store(f.cnt + (size_t)(chunk * 4 + s) * SPF_LINE, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     if constexpr (DBG) {
       stamp(5);
       return;
@@ -280,8 +236,9 @@ __device__ __forceinline__ void spf_stage(const SpeechW& w, const SpeechFlow& f,
       sh.lg[row][o] = s + sh.w5[64 * 7 + o];
     }
     __syncthreads();
+    const bool bad = __hip_atomic_load(f.err, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) != 0;
+    if (bad && tid == 0) __hip_atomic_store(f.host_err, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
     if (tid < nr) {
-      const bool bad = __hip_atomic_load(f.err, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) != 0;
       const float* z = sh.lg[tid];
       float m = z[0];
       for (int o = 1; o < 7; ++o) m = fmaxf(m, z[o]);
@@ -347,6 +304,18 @@ int SpeechModel::create(const float* blob, size_t n) {
   return upload(w, h.data(), h.size() * sizeof(float));
 }
 
+SpeechModel::~SpeechModel() {
+  if (host_err) (void)hipHostFree(host_err);
+}
+
+int SpeechModel::check() {
+  if (!host_err || !*reinterpret_cast<volatile unsigned*>(host_err)) return 0;
+  *host_err = 0;
+  set_error("speech: a stage hand-off wait expired (spin limit) in a forward since the last check; "
+            "that forward's probs are NaN");
+  return -1;
+}
+
 int SpeechModel::forward(const float* x, int B, float* feat, float* logits, float* probs, hipStream_t s) {
   MEC_REQUIRE(B >= 0, "speech: B < 0");
   if (B == 0) return 0;
@@ -357,22 +326,19 @@ int SpeechModel::forward(const float* x, int B, float* feat, float* logits, floa
   p.scale = base + off_scale;
   for (int l = 0; l < 6; ++l) { p.W[l] = base + off_W[l]; p.b[l] = base + off_b[l]; }
   for (int l = 0; l < 5; ++l) { p.inv[l] = base + off_inv[l]; p.shift[l] = base + off_shift[l]; }
-  if (opt().speech_impl == 1) {
-    MEC_TRY(prof.begin(TAG_SPEECH, s));
-    hipLaunchKernelGGL(speech_kernel, dim3((B + SPEECH_R - 1) / SPEECH_R), dim3(SF_THREADS), 0, s, p, x, B, feat,
-                       logits, probs);
-    MEC_LAUNCH_CHECK();
-    MEC_TRY(prof.end(TAG_SPEECH, s));
-    return 0;
-  }
   const int nch = (B + SPF_SB - 1) / SPF_SB;
   MEC_REQUIRE(nch <= (1 << 24) / SPF_WG_PER_CHUNK, "speech: batch too large");
-  if (nch > flow_chunks) {  // grown: counters start at zero
+  if (nch > flow_chunks) {
     MEC_TRY(flow_act.ensure((size_t)nch * SPF_SB * (512 + 512 + 256 + 128) * sizeof(float)));
     MEC_TRY(flow_sync.ensure(((size_t)nch * 4 + 1) * SPF_LINE * sizeof(unsigned)));
-    MEC_HIP(hipMemsetAsync(flow_sync.p, 0, flow_sync.bytes, s));
     flow_chunks = nch;
   }
+  if (!host_err) {
+    MEC_HIP(hipHostMalloc(reinterpret_cast<void**>(&host_err), sizeof(unsigned), hipHostMallocMapped));
+    *host_err = 0;
+  }
+  // every launch starts from zeroed counters and error word (one memset on the stream)
+  MEC_HIP(hipMemsetAsync(flow_sync.p, 0, ((size_t)flow_chunks * 4 + 1) * SPF_LINE * sizeof(unsigned), s));
   SpeechFlow fl;
   float* a = flow_act.as<float>();
   const size_t rows = (size_t)flow_chunks * SPF_SB;
@@ -382,7 +348,12 @@ int SpeechModel::forward(const float* x, int B, float* feat, float* logits, floa
   fl.act[3] = a + rows * 1280;
   fl.cnt = flow_sync.as<unsigned>();
   fl.err = fl.cnt + (size_t)flow_chunks * 4 * SPF_LINE;
+  MEC_HIP(hipHostGetDevicePointer(reinterpret_cast<void**>(&fl.host_err), host_err, 0));
   fl.chunks = nch;
+  fl.spin_limit = SPF_SPIN_LIMIT;
+#ifdef MEC_PROBES
+  if (opt().speech_spin_limit >= 0) fl.spin_limit = opt().speech_spin_limit;  // probe: force expiries
+#endif
   MEC_TRY(prof.begin(TAG_SPEECH, s));
 #ifdef MEC_PROBES
   if (opt().speech_debug) {

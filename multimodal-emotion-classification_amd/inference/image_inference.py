@@ -40,7 +40,7 @@ _KINDS = {'resnet50': 'image', 'mobilenet_v2': 'image_mbv2'}
 
 
 class ImageInference:
-    def __init__(self, weights=None, seed=None, device=None, backbone='resnet50'):
+    def __init__(self, weights=None, seed=None, device=None, backbone='resnet50', precision=None):
         if backbone not in _KINDS:
             raise ValueError(f'backbone must be one of {sorted(_KINDS)}')
         self.emotions = Config.EMOTIONS
@@ -48,7 +48,8 @@ class ImageInference:
         self.model = None
         w = checkpoints.resolve(_KINDS[backbone], weights, seed)
         if w is not None:  # raises MecError without HIP/GPU
-            self.model = engine.IMAGE_BACKBONES[backbone](w, device=device)
+            self.model = engine.IMAGE_BACKBONES[backbone](w, device=device,
+                                                          precision=checkpoints.precision(precision))
         self.device = self.model.device if self.model is not None else None
 
     def _fallback(self) -> Dict:

@@ -29,14 +29,14 @@ _MODS = ('speech', 'text', 'image')
 
 
 class MultimodalFusion:
-    def __init__(self, weights=None, seed=None, device=None):
+    def __init__(self, weights=None, seed=None, device=None, precision=None):
         weights = weights or {}
         self.emotions = Config.EMOTIONS
         self.weights = [0.3, 0.35, 0.35]  # speech, text, image (reference :23)
         self.fusion_model = None
         self.speech_inference = SpeechInference(weights.get('speech'), seed, device)
-        self.text_inference = TextInference(weights.get('text'), seed, device)
-        self.image_inference = ImageInference(weights.get('image'), seed, device)
+        self.text_inference = TextInference(weights.get('text'), seed, device, precision=precision)
+        self.image_inference = ImageInference(weights.get('image'), seed, device, precision=precision)
         w = checkpoints.resolve('fusion', weights.get('fusion'), seed)
         if w is not None:
             self.fusion_model = engine.FusionHead(w, device=device)  # raises MecError without HIP/GPU

@@ -81,7 +81,9 @@ class SpeechInference:
     def _forward(self, features: np.ndarray):
         x = np.asarray(features, dtype=np.float32).reshape(1, 56)
         feat, logits, probs = self.model.forward(engine.to_device(x, self.device))
-        return feat.cpu().numpy()[0], probs.cpu().numpy()[0]
+        feat, probs = feat.cpu().numpy()[0], probs.cpu().numpy()[0]  # synchronizes the stream
+        self.model.check()  # an expired in-kernel wait raises MecError instead of NaN probs
+        return feat, probs
 
     @staticmethod
     def _as_dict(emotions, probs: np.ndarray) -> Dict:

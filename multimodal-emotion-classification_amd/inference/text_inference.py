@@ -69,13 +69,13 @@ def encode_batch(tokenizer, texts):
 
 
 class TextInference:
-    def __init__(self, weights=None, seed=None, device=None, tokenizer=None):
+    def __init__(self, weights=None, seed=None, device=None, tokenizer=None, precision=None):
         self.emotions = Config.EMOTIONS
         self.model = None
         self.preprocessor = _Cleaner()
         w = checkpoints.resolve('text', weights, seed)
-        if w is not None:
-            self.model = engine.TextEncoder(w, device=device)  # raises MecError without HIP/GPU
+        if w is not None:  # raises MecError without HIP/GPU
+            self.model = engine.TextEncoder(w, device=device, precision=checkpoints.precision(precision))
         self.tokenizer = tokenizer if tokenizer is not None else (_local_tokenizer() if self.model else None)
         self._fast = None  # built on first batched call
         self.device = self.model.device if self.model is not None else None

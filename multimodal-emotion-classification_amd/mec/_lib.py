@@ -48,6 +48,7 @@ SIGNATURES = {
     'mec_model_gemm_query': (c_int, [c_vp, c_int, c_int, c_int, c_int]),
     'mec_gemm_query': (c_int, [c_int, c_int, c_int, c_int]),
     'mec_gemm_f32_query': (c_int, [c_int, c_int, c_int, c_int]),
+    'mec_model_check': (c_int, [c_vp]),
     'mec_prof_enable': (c_int, [c_vp, c_int]),
     'mec_prof_read': (c_int, [c_vp, c_dp, ctypes.POINTER(c_int)]),
 }

@@ -78,6 +78,14 @@ def load_checkpoint(kind: str):
     raise ValueError(kind)
 
 
+def precision(value=None) -> str:
+    """The drop-in classes' arithmetic: an explicit argument, else Config.PRECISION / MEC_PRECISION,
+    else 'fp32' (the reference's own; its config.py has no PRECISION)."""
+    if value is not None:
+        return value
+    return getattr(Config, 'PRECISION', None) or os.environ.get('MEC_PRECISION') or 'fp32'
+
+
 def resolve(kind: str, weights=None, seed=None):
     if weights is not None:
         return weights

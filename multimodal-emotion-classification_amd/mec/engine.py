@@ -92,6 +92,12 @@ class HipModel:
         """One tuning knob of THIS handle (mec_model_set_option; include/mec.h lists them)."""
         _lib.check(self.lib.mec_model_set_option(self.handle, key.encode(), int(value)), f'set_option({key}={value})')
 
+    def check(self):
+        """Raise MecError if a kernel of this handle flagged an error after the fact since the
+        last check (mec_model_check; speech: an expired hand-off wait, whose forward's probs are
+        NaN). Call once the stream that ran the forwards has been synchronized."""
+        _lib.check(self.lib.mec_model_check(self.handle), f'{self.kind} forward')
+
     def gemm_tile(self, M: int, N: int, K: int, amode: int = 0) -> int:
         """The tile this handle's autotuner chose for a GEMM shape it has run (0 = not seen)."""
         return self.lib.mec_model_gemm_query(self.handle, amode, M, N, K)
@@ -385,6 +391,13 @@ class FusedPipeline:
         """Make `stream` (default: the current one) wait for the last batch's fusion."""
         if self.pipelined:
             (stream or torch.cuda.current_stream(self.device)).wait_stream(self._tail)
+
+    def check(self):
+        """Synchronize the device, then raise MecError if any handle flagged an after-the-fact
+        kernel error since the last check (mec_model_check)."""
+        torch.cuda.synchronize(self.device)
+        for m in self.models():
+            m.check()
 
     @staticmethod
     def pack_rows(out) -> torch.Tensor:

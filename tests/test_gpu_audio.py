@@ -112,3 +112,21 @@ def test_audio_long_clip_median_from_hbm(fx, dev):
     got, gt = _run(fx, dev, wave)
     ref, rt = oa.features_batch(wave)
     _compare('30 s noise', got, gt, ref, rt)
+
+
+def test_audio_features_at_44100_hz(dev):
+    """A handle at another sample rate (AudioModel::create takes 8-96 kHz): every sr-dependent
+    table and piptrack's pitch = (bin + shift) * sr / n_fft follow the handle's rate."""
+    fx44 = engine.AudioFeaturizer(sample_rate=44100, device=dev)
+    wave = oa.synthetic_clips(3, seed=17, n=44100 * 2, kind='mixed')
+    got, gt = _run(fx44, dev, wave)
+    ref, rt = oa.features_batch(wave, sr=44100)
+    _compare('44.1 kHz', got, gt, ref, rt)
+
+
+def test_audio_rate_too_low_for_the_peak_list_is_rejected(dev):
+    """Below ~21.6 kHz the 150-4000 Hz piptrack band holds more local maxima per frame than the
+    per-frame peak list: the handle refuses the rate instead of dropping peaks."""
+    from mec._lib import MecError
+    with pytest.raises(MecError, match='sample_rate too low'):
+        engine.AudioFeaturizer(sample_rate=16000, device=dev)

@@ -202,20 +202,6 @@ def test_resize_bit_exact_many(dev):
     assert np.array_equal(out.cpu().numpy(), resize_bilinear_u8(gray))
 
 
-def test_fused_bottleneck_tail_bit_identical(dev):
-    """bottleneck.hip (conv2 + conv3 + residual in one kernel, opt-in) == the GEMM path."""
-    from mec import _lib, engine, synthetic as syn
-    lib = _lib.load()
-    m = engine.ImageEncoder(device=dev)
-    g = engine.to_device(syn.image_inputs(5, seed=41), dev)
-    outs = []
-    for v in (0, 1):
-        m.set_option('resnet_fused_tail', v)
-        outs.append([t.cpu() for t in m.forward(g)])
-    for a, b in zip(*outs):
-        assert torch.equal(a, b)
-
-
 @pytest.mark.parametrize('B', [1, 7, 256])
 def test_fusion_split_bit_identical(dev, B):
     """The three-launch fusion (projection / cross-attention per modality, then the head)

@@ -70,6 +70,16 @@ def test_model_option_and_query_need_a_handle():
     assert b'null model' in lib.mec_last_error()
     assert lib.mec_model_gemm_query(None, 0, 256, 256, 256) == -1
     assert lib.mec_precision(None) == -1
+    assert lib.mec_model_check(None) == -1
+    assert b'null handle' in lib.mec_last_error()
+
+
+def test_removed_knobs_are_unknown():
+    """The measured-slower opt-in paths of round 2 (register-staged GEMM engine, fused
+    bottleneck tail, O-proj + LN kernel, one-kernel speech DNN) are gone from the library."""
+    lib = _lib.load()
+    for k in (b'gemm_impl', b'resnet_fused_tail', b'bert_oproj_ln', b'speech_impl'):
+        assert lib.mec_set_option(k, 0) == -1 and b'unknown' in lib.mec_last_error().lower(), k
 
 
 def test_c_abi_argument_errors_without_gpu():
@@ -91,23 +101,22 @@ def test_option_validation_without_gpu():
     lib = _lib.load()
     assert lib.mec_build_flags() == 0, 'the product library must not be a probe build'
     probes = [(b'gemm_debug', 1), (b'gemm_debug', 2), (b'gemm_debug', 4), (b'gemm_debug', 5), (b'stem_debug', 1), (b'conv3x3_debug', 2),
-              (b'bert_qkv_attn', 2), (b'bert_qkv_attn', 3), (b'bert_oproj_ln', 2), (b'bert_oproj_ln', 4),
+              (b'bert_qkv_attn', 2), (b'bert_qkv_attn', 3), (b'speech_spin_limit', 0), (b'speech_spin_limit', 100),
               (b'speech_debug', 1), (b'audio_debug', 15)]
     for k, v in probes:
         assert lib.mec_set_option(k, v) == -1, (k, v)
         assert b'MEC_PROBES' in lib.mec_last_error()
     ok = [(b'fusion_r', 1), (b'fusion_r', 4), (b'fusion_split', 0), (b'fusion_split', 1),
-          (b'bert_qkv_attn', 0), (b'bert_qkv_attn', 1), (b'bert_oproj_ln', 0), (b'bert_oproj_ln', 1),
+          (b'bert_qkv_attn', 0), (b'bert_qkv_attn', 1), (b'speech_spin_limit', -1),
           (b'gemm_bn', 40256), (b'gemm_bn', 0),
           (b'gemm_bn_tag', 3 * 100000 + 40256), (b'gemm_bn_tag', 3 * 100000 + 11128),
-          (b'gemm_debug', 0), (b'gemm_f32_tile', 3), (b'gemm_f32_tile', 0), (b'bert_oproj_ln', 3),
-          (b'speech_impl', 1), (b'speech_impl', 0), (b'speech_debug', 0),
+          (b'gemm_debug', 0), (b'gemm_f32_tile', 3), (b'gemm_f32_tile', 0), (b'speech_debug', 0),
           (b'gemm_group_m', 0), (b'gemm_group_m', 16), (b'gemm_group_m', 8),
           (b'gemm_f32_family', 0), (b'gemm_f32_family', 32), (b'gemm_f32_family', 16),
           (b'bert_ln_rows', 1), (b'bert_ln_rows', 4), (b'bert_ln_rows', 2)]
-    bad = [(b'bert_ln_rows', 3), (b'gemm_f32_family', 8), (b'gemm_group_m', 3), (b'gemm_group_m', -1), (b'gemm_group_m', 32), (b'gemm_f32_tile', 9), (b'fusion_r', 3), (b'fusion_split', 2), (b'bert_qkv_attn', 4), (b'bert_oproj_ln', 5), (b'gemm_bn', 12345),
+    bad = [(b'bert_ln_rows', 3), (b'gemm_f32_family', 8), (b'gemm_group_m', 3), (b'gemm_group_m', -1), (b'gemm_group_m', 32), (b'gemm_f32_tile', 9), (b'fusion_r', 3), (b'fusion_split', 2), (b'bert_qkv_attn', 4), (b'gemm_bn', 12345),
            (b'gemm_bn', 42256), (b'gemm_bn_tag', 11128), (b'gemm_bn_tag', 15 * 100000 + 256),
-           (b'gemm_bn_tag', 3 * 100000 + 999), (b'gemm_bn_tag', -1), (b'gemm_debug', 6), (b'speech_impl', 2)]
+           (b'gemm_bn_tag', 3 * 100000 + 999), (b'gemm_bn_tag', -1), (b'gemm_debug', 6), (b'speech_spin_limit', -2)]
     try:
         for k, v in ok:
             assert lib.mec_set_option(k, v) == 0, (k, v)
@@ -115,7 +124,7 @@ def test_option_validation_without_gpu():
             assert lib.mec_set_option(k, v) == -1, (k, v)
             assert b'bad value' in lib.mec_last_error()
     finally:  # the defaults
-        for k, v in [(b'fusion_r', 4), (b'fusion_split', 1), (b'bert_qkv_attn', 1), (b'bert_oproj_ln', 0), (b'speech_impl', 0),
+        for k, v in [(b'fusion_r', 4), (b'fusion_split', 1), (b'bert_qkv_attn', 1), (b'speech_spin_limit', -1),
                      (b'gemm_f32_tile', 0),
                      (b'gemm_bn', 0),
                      (b'gemm_bn_tag', 3 * 100000 + 11128), (b'gemm_debug', 0), (b'gemm_group_m', 8),

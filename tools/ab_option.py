@@ -1,6 +1,6 @@
 """Interleaved A/B of a library option (mec_model_set_option) on one encoder at B=256.
 
-    python tools/ab_option.py --enc image --opt resnet_fused_tail --values 0 1
+    python tools/ab_option.py --enc image --opt pw_chain --values 0 2
 
 Each round times every value back to back (hipEvents, --iters calls), median of rounds; the
 encoder's outputs under each value are compared with the first value's."""

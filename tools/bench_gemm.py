@@ -1,6 +1,6 @@
 """Microbenchmark of the GEMM / implicit-GEMM conv engines on the hot path's real shapes.
 
-    python tools/bench_gemm.py [--impl 1 2] [--bn 0 64 128 256] [--iters 20]
+    python tools/bench_gemm.py [--bn 0 64 128 256] [--iters 20]
 
 Interleaves variants in one process (guide rule 24), random operands (rule 25).
 """
@@ -48,7 +48,7 @@ def p(t):
 
 def main():
     ap = argparse.ArgumentParser()
-    ap.add_argument('--impl', type=int, nargs='+', default=[1, 2])
+    ap.add_argument("--impl", type=int, nargs="+", default=[2], help="ignored: one engine (glds)")
     ap.add_argument('--bn', type=int, nargs='+', default=[0])
     ap.add_argument('--iters', type=int, default=10)
     ap.add_argument('--rounds', type=int, default=5)
@@ -105,13 +105,12 @@ def main():
             ms = e0.elapsed_time(e1) / a.iters
             r = {'shape': name, 'impl': 'torch.mm', 'us': round(ms * 1e3, 1), 'tflops': round(flop / ms / 1e9, 1)}
             print(json.dumps(r), flush=True)
-        variants = [(i, b, d, f) for i in a.impl for b in (a.bn if i == 2 else [0]) for d in a.debug
+        variants = [(2, b, d, f) for b in a.bn for d in a.debug
                     for f in a.prefetch]
 
         def setv(impl, bn, dbg, pf=1):
             lib.mec_set_option(b'gemm_prefetch_r', pf)
             lib.mec_set_option(b'gemm_debug', dbg)
-            lib.mec_set_option(b'gemm_impl', impl)
             lib.mec_set_option(b'gemm_bn', bn)
 
         ok = []
@@ -159,7 +158,6 @@ def main():
                 r['tuned'] = lib.mec_gemm_query(0, M, N, K)
             res.append(r)
             print(json.dumps(r), flush=True)
-    lib.mec_set_option(b'gemm_impl', 2)
     lib.mec_set_option(b'gemm_debug', 0)
     lib.mec_set_option(b'gemm_bn', 0)
 

@@ -11,6 +11,6 @@ run() {  # precision, option, values...
   grep '^{' gpurun_out/ab_tmp.txt | tee -a $out
 }
 run f16 conv3x3_halo 1 0 && run f16 conv3x3_direct 1 0 && run f16 pw_chain 2 1 0 && \
-run f16 gemm_prefetch_r 1 0 && run f16 fusion_r 4 2 1 && run f16 bert_oproj_ln 0 1 3 && \
+run f16 gemm_prefetch_r 1 0 && run f16 fusion_r 4 2 1 && \
 run fp32 gemm_f32_tag 500000 500004 500008 500001 500005 && \
 run fp32 gemm_f32_tag 300000 300004 300008 300001 300005 300002 300006
