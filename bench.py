@@ -8,13 +8,17 @@ rank at N>1 = configs[4]'s global 8192 on 8 GPUs). Consecutive batches are pipel
 (engine.FusedPipeline): batch i's fusion and gather overlap batch i+1's encoders; the timed
 region ends after the last batch's gather (device synchronize).
 
-The path runs at two precisions on the same inputs; rank 0 prints ONE JSON line:
+The path runs at three precisions on the same inputs; rank 0 prints ONE JSON line:
   headline  "fp32": every operand and product in fp32 (v_mfma_f32_16x16x4_f32 / 32x32x2_f32),
             the reference's own precision (inference/text_inference.py:91-93,
             inference/image_inference.py:116-118) -- `value` is this path's throughput;
   nested    "f16_fast_path": BERT / ResNet50 on f16 MFMA operands with fp32 accumulation,
             LayerNorm, softmax, GELU, residual stream and heads (north_star's probs <= 1e-3 bar;
-            narrower than the reference's arithmetic, so reported beside the headline, not as it).
+            narrower than the reference's arithmetic, so reported beside the headline, not as it);
+  nested    "fp32x3_path": the fp32 path's arithmetic with every GEMM / conv operand carried as an
+            exact f16 hi + lo pair (22 of fp32's 24 significand bits) and each product as
+            hi.hi + hi.lo + lo.hi on the f16 MFMA into one fp32 accumulator, held to the fp32
+            path's parity bars.
 Each carries `parity`: the oracle (CPU fp32 restatement of the reference) on rows of the timed
 batch -- every row at B <= 256, rows from every quarter of the batch beyond -- with logits /
 probs max-abs-err, argmax agreement and the count of at-risk rows (oracle top-2 margin below
@@ -51,9 +55,14 @@ METRIC = 'fused tri-modal samples/sec @ batch 256; per-modality logits max-abs-e
 FLOP_PER_SAMPLE = {'text': 2 * 11_174_221_056, 'image': 2 * 4_088_188_416, 'speech': 2 * 463_296,
                    'fusion': 2 * 2_020_000}
 # MI355X_MICROARCH.md: dense f16 MFMA ~2.5 PF; f32-input MFMA 157.3 TF (= the f32 vector peak)
-PEAK_TFLOPS = {'f16': 2500.0, 'fp32': 157.3}
+PEAK_TFLOPS = {'f16': 2500.0, 'fp32': 157.3, 'fp32x3': 2500.0}
+# fp32x3: every GEMM FLOP is three f16 MFMA FLOPs (hi.hi + hi.lo + lo.hi), priced against the f16 peak
+MFMA_FLOP_PER_FLOP = {'f16': 1, 'fp32': 1, 'fp32x3': 3}
 DTYPE = {'f16': 'f16 MFMA operands / fp32 accumulate, LN & softmax & residual fp32; speech+fusion fp32',
-         'fp32': 'fp32 (exact-f32 MFMA GEMMs; every operand and product fp32)'}
+         'fp32': 'fp32 (exact-f32 MFMA GEMMs; every operand and product fp32)',
+         'fp32x3': 'fp32 emulated on the f16 MFMA: each fp32 GEMM operand an exact f16 hi+lo pair (22 of 24 '
+                   'significand bits), hi.hi + hi.lo + lo.hi into one fp32 accumulator; LN, softmax, attention, '
+                   'GELU, residual stream, heads, speech and fusion fp32'}
 ROW = 34  # packed result row: 3x7 modality probs | 7 fused probs | 3 attention | 3 decision weights
 
 
@@ -86,7 +95,8 @@ def parse(argv=None):
     ap.add_argument('--steps', type=int, default=10)
     ap.add_argument('--warmup', type=int, default=3)
     ap.add_argument('--batch', type=int, default=0, help='samples per rank (default 256 at N=1, 1024 at N>1)')
-    ap.add_argument('--precision', default='both', choices=['both', 'f16', 'fp32'])
+    ap.add_argument('--precision', default='all', choices=['all', 'both', 'f16', 'fp32', 'fp32x3'],
+                    help="all: fp32 (headline) + f16 + fp32x3 (nested); both: fp32 + f16")
     ap.add_argument('--no-cpu-baseline', action='store_true')
     ap.add_argument('--no-parity', action='store_true')
     ap.add_argument('--oracle-rows', type=int, default=256,
@@ -273,7 +283,7 @@ def per_config(pipe, dev, precision, iters=10):
     af = engine.AudioFeaturizer(device=dev)
     wv = torch.from_numpy(np.random.default_rng(7).standard_normal((32, 66150)).astype(np.float32)).to(dev)
     runs['speech_waveform_b32'] = (32, lambda: pipe.speech.forward(af.forward(wv)))
-    mb = engine.MobileNetImageEncoder(device=dev, precision=precision)
+    mb = engine.MobileNetImageEncoder(device=dev, precision='fp32' if precision == 'fp32x3' else precision)
     runs['image_mobilenet_v2_b256'] = (256, lambda: mb.forward(g))
     out = {}
     for name, (b, fn) in runs.items():
@@ -387,7 +397,8 @@ def run(a, precision, B, world, rank, dev, inputs):
 
     M = B * 128
     peak = PEAK_TFLOPS[precision]
-    ffn_flop = 2.0 * M * 3072 * 768
+    mf = MFMA_FLOP_PER_FLOP[precision]
+    ffn_flop = 2.0 * M * 3072 * 768 * mf  # MFMA FLOPs per launch (fp32x3: three f16 products per product)
     avg_s = (ffn_ms / max(ffn_n, 1)) / 1e3
     achieved = ffn_flop / avg_s / 1e12 if ffn_n else None
     iso = ffn_flop / ((iso_ms / max(iso_n, 1)) / 1e3) / 1e12 if iso_n else None
@@ -395,6 +406,9 @@ def run(a, precision, B, world, rank, dev, inputs):
     if precision == 'f16':
         kname = tile_name(tile, M) + ' + GELU'
         ebytes, tfile = 2, 'ffn1_traffic.json'
+    elif precision == 'fp32x3':
+        kname = tile_name(tile, M) + ' split-f16 (3 K passes) + erf-GELU, hi/lo f16 out'
+        ebytes, tfile = 4, 'ffn1_x3_traffic.json'
     else:
         kname = tile_name_f32(tile, M) + ' + erf-GELU'
         ebytes, tfile = 4, 'ffn1_f32_traffic.json'
@@ -408,7 +422,7 @@ def run(a, precision, B, world, rank, dev, inputs):
     roof = {'bound': 'mfma', 'kernel': f'{kname} (BERT FFN1, M={M} N=3072 K=768)',
             'achieved': achieved, 'peak': peak, 'unit': 'TFLOP/s',
             'frac': (achieved / peak) if achieved else None, 'traffic': traffic, 'traffic_source': tsrc,
-            'algorithmic_flop_per_launch': ffn_flop,
+            'algorithmic_flop_per_launch': ffn_flop / mf, 'mfma_flop_per_launch': ffn_flop,
             'algorithmic_bytes_per_launch': ebytes * (M * 768 + 3072 * 768 + M * 3072),
             'avg_launch_ms': avg_s * 1e3, 'launches': ffn_n, 'launches_expected': 12 * a.steps,
             'note': 'achieved: live in the timed region (CUs shared with the image stream); '
@@ -428,7 +442,7 @@ def run(a, precision, B, world, rank, dev, inputs):
                    'batch_per_gpu': B, 'global_batch': world * B, 'seq_len': 128,
                    'parallelism': f'dp{world} (sample-sharded, all-gather of 34-float rows)'},
         'achieved_tflops_whole_step': flop / el / 1e12,
-        'whole_step_frac_of_peak': flop / el / 1e12 / peak,
+        'whole_step_frac_of_peak': flop * mf / el / 1e12 / peak,
         'roofline': roof,
     }
     if world > 1:
@@ -452,7 +466,7 @@ def main_gpu(a, world, rank, local):
     B = a.batch or (256 if world == 1 else 1024)
     inputs = (syn.speech_inputs(B, seed=rank), *syn.text_inputs(B, 128, seed=rank, ragged=False),
               syn.image_inputs(B, seed=rank))
-    precs = ['f16', 'fp32'] if a.precision == 'both' else [a.precision]
+    precs = {'all': ['f16', 'fp32x3', 'fp32'], 'both': ['f16', 'fp32']}.get(a.precision, [a.precision])
     lines, outs, gathered = {}, {}, {}
     for p in precs:
         res, o, gth = run(a, p, B, world, rank, dev, inputs)
@@ -473,11 +487,12 @@ def main_gpu(a, world, rank, local):
             if cb is not None:
                 lines[p]['cpu_baseline'] = cb
         head = lines['fp32'] if 'fp32' in lines else lines[precs[0]]
-        if 'fp32' in lines and 'f16' in lines:
-            f = lines['f16']
-            head['f16_fast_path'] = {k: f[k] for k in ('value', 'unit', 'ms_per_step', 'dtype',
-                                                       'achieved_tflops_whole_step', 'whole_step_frac_of_peak',
-                                                       'roofline', 'parity', 'per_config', 'distributed') if k in f}
+        for p, key in (('f16', 'f16_fast_path'), ('fp32x3', 'fp32x3_path')):
+            if 'fp32' in lines and p in lines:
+                f = lines[p]
+                head[key] = {k: f[k] for k in ('value', 'unit', 'ms_per_step', 'dtype',
+                                               'achieved_tflops_whole_step', 'whole_step_frac_of_peak',
+                                               'roofline', 'parity', 'per_config', 'distributed') if k in f}
         print(json.dumps(head), flush=True)
         if a.json_out:
             with open(a.json_out, 'w') as fh:

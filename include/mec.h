@@ -51,9 +51,13 @@ int mec_create(int kind, const float* host_blob, size_t n, int device, mec_model
  * image backbones on f16 MFMA operands with fp32 accumulation, LayerNorm, softmax, GELU,
  * residual stream and heads. MEC_PREC_FP32: every operand and product in fp32
  * (v_mfma_f32_32x32x2_f32, an exact fmaf chain), the precision the reference computes in
- * (inference/text_inference.py:91-93, inference/image_inference.py:116-118). Speech, fusion
- * and audio handles are fp32 at either setting. */
-enum { MEC_PREC_F16 = 0, MEC_PREC_FP32 = 1 };
+ * (inference/text_inference.py:91-93, inference/image_inference.py:116-118).
+ * MEC_PREC_FP32X3 (BERT, ResNet50): the fp32 path's arithmetic with every GEMM / conv operand
+ * carried as an exact pair of f16 planes (x = hi + lo, 22 significant bits against fp32's 24) and
+ * each product as hi.hi + hi.lo + lo.hi on the f16 MFMA into one fp32 accumulator; LayerNorm,
+ * softmax, attention, GELU, residual stream and heads fp32. Speech, fusion and audio handles
+ * are fp32 at every setting. */
+enum { MEC_PREC_F16 = 0, MEC_PREC_FP32 = 1, MEC_PREC_FP32X3 = 2 };
 int mec_create_ex(int kind, const float* host_blob, size_t n, int device, int precision, mec_model** out);
 /* The handle's precision (MEC_PREC_*), -1 on a null handle. */
 int mec_precision(const mec_model* m);

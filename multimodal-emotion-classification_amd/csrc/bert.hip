@@ -32,7 +32,8 @@ __global__ __launch_bounds__(256) void bert_embed_ln_kernel(const int32_t* __res
                                                             const float* __restrict__ type,
                                                             const float* __restrict__ g,
                                                             const float* __restrict__ b, float* h32,
-                                                            f16* h16) {
+                                                            f16* h16, long long lo) {
+  // lo != 0 (the fp32x3 path): h16 is a hi plane and h16 + lo the lo plane, f16(y - hi)
   const int lane = threadIdx.x & 63;
   const int row = blockIdx.x * 4 + (threadIdx.x >> 6);
   if (row >= M) return;
@@ -72,6 +73,11 @@ __global__ __launch_bounds__(256) void bert_embed_ln_kernel(const int32_t* __res
     if (h16) {  // null on the fp32 path
       half4 hh = {(f16)o.x, (f16)o.y, (f16)o.z, (f16)o.w};
       *reinterpret_cast<half4*>(h16 + (size_t)row * BH + c) = hh;
+      if (lo) {
+        half4 hl = {(f16)(o.x - (float)hh[0]), (f16)(o.y - (float)hh[1]), (f16)(o.z - (float)hh[2]),
+                    (f16)(o.w - (float)hh[3])};
+        *reinterpret_cast<half4*>(h16 + lo + (size_t)row * BH + c) = hl;
+      }
     }
   }
 }
@@ -83,7 +89,7 @@ template <int RW>
 __global__ __launch_bounds__(256) void bert_layernorm_kernel(const float* x, int M,
                                                              const float* __restrict__ g,
                                                              const float* __restrict__ b, float* h32,
-                                                             f16* h16, float2* stats) {
+                                                             f16* h16, float2* stats, long long lo) {
   // h32 may be null: the consumer of the f32 output (the next residual add) then
   // re-derives it from x and `stats` in its GEMM epilogue (GemmParams::r_stats)
   const int lane = threadIdx.x & 63;
@@ -132,37 +138,43 @@ __global__ __launch_bounds__(256) void bert_layernorm_kernel(const float* x, int
       if (h16) {  // null on the fp32 path
         half4 hh = {(f16)o.x, (f16)o.y, (f16)o.z, (f16)o.w};
         *reinterpret_cast<half4*>(h16 + (size_t)row * BH + c) = hh;
+        if (lo) {  // fp32x3 path: the lo plane
+          half4 hl = {(f16)(o.x - (float)hh[0]), (f16)(o.y - (float)hh[1]), (f16)(o.z - (float)hh[2]),
+                      (f16)(o.w - (float)hh[3])};
+          *reinterpret_cast<half4*>(h16 + lo + (size_t)row * BH + c) = hl;
+        }
       }
     }
   }
 }
 
 static void launch_ln_rows(const float* x, int M, const float* g, const float* b, float* h32, f16* h16, float2* st,
-                           hipStream_t s) {
+                           hipStream_t s, long long lo = 0) {
   if (opt().bert_ln_rows == 4)
-    hipLaunchKernelGGL(bert_layernorm_kernel<4>, dim3((M + 15) / 16), dim3(256), 0, s, x, M, g, b, h32, h16, st);
+    hipLaunchKernelGGL(bert_layernorm_kernel<4>, dim3((M + 15) / 16), dim3(256), 0, s, x, M, g, b, h32, h16, st, lo);
   else if (opt().bert_ln_rows == 2)
-    hipLaunchKernelGGL(bert_layernorm_kernel<2>, dim3((M + 7) / 8), dim3(256), 0, s, x, M, g, b, h32, h16, st);
+    hipLaunchKernelGGL(bert_layernorm_kernel<2>, dim3((M + 7) / 8), dim3(256), 0, s, x, M, g, b, h32, h16, st, lo);
   else
-    hipLaunchKernelGGL(bert_layernorm_kernel<1>, dim3((M + 3) / 4), dim3(256), 0, s, x, M, g, b, h32, h16, st);
+    hipLaunchKernelGGL(bert_layernorm_kernel<1>, dim3((M + 3) / 4), dim3(256), 0, s, x, M, g, b, h32, h16, st, lo);
 }
 
 // Host launchers (also used by the fp32 path, bert_f32.hip). One wave per token row.
-int launch_bert_embed_ln(const int32_t* ids, int M, int L, const float* emb, float* h32, f16* h16, hipStream_t s) {
+int launch_bert_embed_ln(const int32_t* ids, int M, int L, const float* emb, float* h32, f16* h16, hipStream_t s,
+                         long long lo) {
   const float* word = emb;
   const float* pos = word + (size_t)BVOCAB * BH;
   const float* type = pos + (size_t)BMAXPOS * BH;
   const float* lng = type + 2 * BH;
   const float* lnb = lng + BH;
   hipLaunchKernelGGL(bert_embed_ln_kernel, dim3((M + 3) / 4), dim3(256), 0, s, ids, M, L, word, pos, type, lng, lnb,
-                     h32, h16);
+                     h32, h16, lo);
   MEC_LAUNCH_CHECK();
   return 0;
 }
 
 int launch_bert_layernorm(const float* x, int M, const float* g, const float* b, float* h32, f16* h16, float2* stats,
-                          hipStream_t s) {
-  launch_ln_rows(x, M, g, b, h32, h16, stats, s);
+                          hipStream_t s, long long lo) {
+  launch_ln_rows(x, M, g, b, h32, h16, stats, s, lo);
   MEC_LAUNCH_CHECK();
   return 0;
 }
@@ -487,8 +499,9 @@ int TextModel::create(const float* blob, size_t n) {
   e.insert(e.end(), type, type + 2 * BH);
   e.insert(e.end(), lg, lg + BH);
   e.insert(e.end(), lb, lb + BH);
-  // f16 path: GEMM weights in f16 (wts); fp32 path: the same layout in f32 (wts32)
-  const bool f32 = prec == PREC_FP32;
+  // f16 path: GEMM weights in f16 (wts); fp32 path: the same layout in f32 (wts32); fp32x3
+  // path: built in f32, then split into f16 hi / lo planes (wts, below)
+  const bool f32 = prec != PREC_F16;
   std::vector<f16> w(f32 ? 0 : WT_LAYER * BLAYERS);
   std::vector<float> w32(f32 ? WT_LAYER * BLAYERS : 0);
   auto put = [&](size_t off, const float* src, size_t cnt) {
@@ -534,8 +547,28 @@ int TextModel::create(const float* blob, size_t n) {
   ho += (size_t)BH * 7;
   std::copy(bc, bc + 7, pr.begin() + ho);
   MEC_TRY(upload(emb, e.data(), e.size() * sizeof(float)));
-  if (f32) MEC_TRY(upload(wts32, w32.data(), w32.size() * sizeof(float)));
-  else MEC_TRY(upload(wts, w.data(), w.size() * sizeof(f16)));
+  if (prec == PREC_FP32X3) {
+    // each GEMM's B matrix (Wqkv | Wo | Wi | Wo2 of a layer) scaled by 2^e (max |w| 2^e <= 2^14,
+    // exact) and split into hi = f16(w 2^e) and lo = f16(w 2^e - hi) planes; the GEMM epilogue
+    // multiplies the accumulator by 2^-e (GemmParams::oscale)
+    const size_t total = WT_LAYER * BLAYERS;
+    std::vector<f16> hl(2 * total);
+    x3_lo = total;
+    x3_scale.assign(4 * BLAYERS, 1.f);
+    const size_t sizes[4] = {(size_t)2304 * BH, (size_t)BH * BH, (size_t)BI * BH, (size_t)BH * BI};
+    for (int l = 0; l < BLAYERS; ++l) {
+      size_t off = WT_LAYER * l;
+      for (int mtx = 0; mtx < 4; ++mtx) {
+        x3_scale[4 * l + mtx] = split_planes(w32.data() + off, sizes[mtx], hl.data() + off, hl.data() + total + off);
+        off += sizes[mtx];
+      }
+    }
+    MEC_TRY(upload(wts, hl.data(), hl.size() * sizeof(f16)));
+  } else if (f32) {
+    MEC_TRY(upload(wts32, w32.data(), w32.size() * sizeof(float)));
+  } else {
+    MEC_TRY(upload(wts, w.data(), w.size() * sizeof(f16)));
+  }
   MEC_TRY(upload(prm, pr.data(), pr.size() * sizeof(float)));
   return 0;
 }
@@ -547,6 +580,7 @@ int TextModel::forward(const int32_t* ids, const int32_t* mask, int B, int L, fl
   MEC_REQUIRE(L == ATT_L, "text: L must be 128 (padding='max_length', MAX_TEXT_LENGTH=128)");
   MEC_REQUIRE(ids && mask && cls && logits && probs, "text: null pointer");
   if (prec == PREC_FP32) return forward_f32(ids, mask, B, L, cls, logits, probs, s);
+  if (prec == PREC_FP32X3) return forward_x3(ids, mask, B, L, cls, logits, probs, s);
   const int M = B * L;
   // workspace: h32 | t32 (f32 [M,768]) ; h16 | ctx16 (f16 [M,768]) ; qkv16 [M,2304] / i16 [M,3072]
   const size_t need = (size_t)M * BH * 4 * 2 + (size_t)M * BH * 2 * 2 + (size_t)M * BI * 2 + (size_t)B * BH * 4 +
@@ -575,7 +609,7 @@ int TextModel::forward(const int32_t* ids, const int32_t* mask, int B, int L, fl
   const float* lnb = lng + BH;
   const dim3 rows_grid((M + 3) / 4);
   hipLaunchKernelGGL(bert_embed_ln_kernel, rows_grid, dim3(256), 0, s, ids, M, L, word, pos, type, lng, lnb, h32,
-                     h16);
+                     h16, 0LL);
   MEC_LAUNCH_CHECK();
   const f16* W = wts.as<f16>();
   const float* P = prm.as<float>();

@@ -32,9 +32,13 @@ __device__ __forceinline__ int kswz(int row, int c) { return c ^ (row & 15); }
 // lane-local plus one shuffle. O^T = V^T P^T: A = V[key][d] read as one f32 per lane (row-major
 // V, 32 consecutive d per half wave), B = the lane's own probabilities, in the k order the
 // score tile left them (two keys per MFMA: key f(e) + 4h of block t for lane half h).
+// SPLIT (fp32x3 path): ctx is written as f16 hi / lo planes (ctx16, ctx16 + lo) for the split
+// O-projection GEMM instead of f32.
+template <int SPLIT = 0>
 __global__ __launch_bounds__(256, 2) void bert_attention_f32_kernel(const float* __restrict__ qkv,
                                                                     const int32_t* __restrict__ mask,
-                                                                    float* __restrict__ ctx) {
+                                                                    float* __restrict__ ctx, f16* __restrict__ ctx16,
+                                                                    long long lo) {
   __shared__ __attribute__((aligned(16))) float sK[AL * DH];
   __shared__ __attribute__((aligned(16))) float sV[AL * DH];
   __shared__ float sBias[AL];
@@ -112,13 +116,26 @@ __global__ __launch_bounds__(256, 2) void bert_attention_f32_kernel(const float*
 #pragma unroll
       for (int u = 0; u < 2; ++u) o[u] = __builtin_amdgcn_mfma_f32_32x32x2f32(sV[key * DH + 32 * u + lr], p, o[u], 0, 0, 0);
     }
-  float* out = ctx + ((size_t)b * AL + q) * H + h * DH;
+  const size_t obase = ((size_t)b * AL + q) * H + h * DH;
 #pragma unroll
   for (int u = 0; u < 2; ++u)
 #pragma unroll
-    for (int g = 0; g < 4; ++g)
-      *reinterpret_cast<float4*>(out + 32 * u + 8 * g + 4 * lh) =
-          make_float4(o[u][4 * g + 0], o[u][4 * g + 1], o[u][4 * g + 2], o[u][4 * g + 3]);
+    for (int g = 0; g < 4; ++g) {
+      const size_t oi = obase + 32 * u + 8 * g + 4 * lh;
+      if constexpr (SPLIT) {
+        half4 hh, hl;
+#pragma unroll
+        for (int e = 0; e < 4; ++e) {
+          hh[e] = (f16)o[u][4 * g + e];
+          hl[e] = (f16)(o[u][4 * g + e] - (float)hh[e]);
+        }
+        *reinterpret_cast<half4*>(ctx16 + oi) = hh;
+        *reinterpret_cast<half4*>(ctx16 + lo + oi) = hl;
+      } else {
+        *reinterpret_cast<float4*>(ctx + oi) =
+            make_float4(o[u][4 * g + 0], o[u][4 * g + 1], o[u][4 * g + 2], o[u][4 * g + 3]);
+      }
+    }
 }
 
 int TextModel::forward_f32(const int32_t* ids, const int32_t* mask, int B, int L, float* cls, float* logits,
@@ -150,7 +167,7 @@ int TextModel::forward_f32(const int32_t* ids, const int32_t* mask, int B, int L
     g.A = h32; g.B32 = wqkv; g.bias = bqkv; g.C32 = big32; g.M = M; g.N = 2304; g.K = H;
     MEC_TRY(launch_gemm_f32(g, s, &prof, TAG_BERT_QKV));
     MEC_TRY(prof.begin(TAG_BERT_ATTN, s));
-    hipLaunchKernelGGL(bert_attention_f32_kernel, dim3(B * NH), dim3(256), 0, s, big32, mask, ctx32);
+    hipLaunchKernelGGL(bert_attention_f32_kernel<0>, dim3(B * NH), dim3(256), 0, s, big32, mask, ctx32, nullptr, 0LL);
     MEC_LAUNCH_CHECK();
     MEC_TRY(prof.end(TAG_BERT_ATTN, s));
     g = GemmParams();
@@ -167,6 +184,80 @@ int TextModel::forward_f32(const int32_t* ids, const int32_t* mask, int B, int L
     MEC_TRY(launch_gemm_f32(g, s, &prof, TAG_BERT_FFN2));
     MEC_TRY(prof.begin(TAG_BERT_LN, s));
     MEC_TRY(launch_bert_layernorm(t32, M, g2, b2, h32, nullptr, nullptr, s));
+    MEC_TRY(prof.end(TAG_BERT_LN, s));
+  }
+  const float* head = P + PRM_LAYER * NL;
+  const float *WpT = head, *bp = WpT + (size_t)H * H, *WcT = bp + H, *bc = WcT + (size_t)H * 7;
+  MEC_TRY(launch_linear_mfma<BACT_TANH>(h32, (size_t)L * H, B, H, WpT, bp, H, pooled, H, cls, H, s));
+  MEC_TRY(launch_head7(pooled, B, H, WcT, bc, logits, probs, s));
+  return 0;
+}
+
+// fp32x3 path: the fp32 path's structure with every GEMM on split-f16 operands (gemm_glds.hip
+// split mode, three f16 MFMA passes into one fp32 accumulator). Per layer (M = B*L rows):
+//   qkv32       = [h_hi|h_lo] . [Wqkv_hi|Wqkv_lo]^T 2^-e + b        split GEMM, f32 out
+//   ctx hi/lo   = softmax(QK^T/8 + mask_bias) V                     bert_attention_f32_kernel<1>
+//   t32         = ctx . Wo^T 2^-e + bo + h32                        split GEMM, f32 residual
+//   h32, h hi/lo = LN(t32)                                          bert_layernorm_kernel (lo plane)
+//   i hi/lo     = GELU(h . Wi^T 2^-e + bi)                          split GEMM, exact erf, split out
+//   t32         = i . Wo2^T 2^-e + bo2 + h32                        split GEMM
+//   h32, h hi/lo = LN(t32)
+int TextModel::forward_x3(const int32_t* ids, const int32_t* mask, int B, int L, float* cls, float* logits,
+                          float* probs, hipStream_t s) {
+  MEC_REQUIRE(wts.p && x3_lo && x3_scale.size() == 4 * NL, "text: fp32x3 weights missing");
+  const int M = B * L;
+  const long long MH = (long long)M * H, MF = (long long)M * FF;
+  // workspace: h32 | t32 (f32 [M,768]) ; h hi|lo, ctx hi|lo (f16 2x[M,768]) ; big: qkv32 f32 [M,2304]
+  // aliased with the FFN intermediate hi|lo (f16 2x[M,3072]) ; pooled [B,768]
+  const size_t need = (size_t)MH * 4 * 2 + (size_t)MH * 2 * 4 + (size_t)MF * 4 + (size_t)B * H * 4;
+  if (ws.bytes < need) MEC_TRY(ws.ensure(need));
+  char* p = ws.as<char>();
+  float* h32 = reinterpret_cast<float*>(p); p += (size_t)MH * 4;
+  float* t32 = reinterpret_cast<float*>(p); p += (size_t)MH * 4;
+  f16* hs = reinterpret_cast<f16*>(p); p += (size_t)MH * 2 * 2;
+  f16* cs = reinterpret_cast<f16*>(p); p += (size_t)MH * 2 * 2;
+  float* big32 = reinterpret_cast<float*>(p);
+  f16* bigs = reinterpret_cast<f16*>(p); p += (size_t)MF * 4;
+  float* pooled = reinterpret_cast<float*>(p);
+
+  MEC_TRY(launch_bert_embed_ln(ids, M, L, emb.as<float>(), h32, hs, s, MH));
+  const f16* W = wts.as<f16>();
+  const float* P = prm.as<float>();
+  const long long wlo = (long long)x3_lo;
+  for (int l = 0; l < NL; ++l) {
+    const f16* wqkv = W + WT_LAYER * l;
+    const f16* wo = wqkv + (size_t)2304 * H;
+    const f16* wi = wo + (size_t)H * H;
+    const f16* wo2 = wi + (size_t)FF * H;
+    const float* sc = x3_scale.data() + 4 * l;
+    const float* pl = P + PRM_LAYER * l;
+    const float *bqkv = pl, *bo = pl + 2304, *g1 = pl + 3072, *b1 = pl + 3840, *bi = pl + 4608, *bo2 = pl + 7680,
+                *g2 = pl + 8448, *b2 = pl + 9216;
+    GemmParams g;
+    g.split = 1; g.A = hs; g.a_lo = MH; g.B = wqkv; g.b_lo = wlo; g.oscale = sc[0];
+    g.bias = bqkv; g.C32 = big32; g.M = M; g.N = 2304; g.K = H;
+    MEC_TRY(launch_gemm(g, s, &prof, TAG_BERT_QKV));
+    MEC_TRY(prof.begin(TAG_BERT_ATTN, s));
+    hipLaunchKernelGGL(bert_attention_f32_kernel<1>, dim3(B * NH), dim3(256), 0, s, big32, mask, nullptr, cs, MH);
+    MEC_LAUNCH_CHECK();
+    MEC_TRY(prof.end(TAG_BERT_ATTN, s));
+    g = GemmParams();
+    g.split = 1; g.A = cs; g.a_lo = MH; g.B = wo; g.b_lo = wlo; g.oscale = sc[1];
+    g.bias = bo; g.R = h32; g.r_f32 = 1; g.C32 = t32; g.M = M; g.N = H; g.K = H;
+    MEC_TRY(launch_gemm(g, s, &prof, TAG_BERT_OPROJ));
+    MEC_TRY(prof.begin(TAG_BERT_LN, s));
+    MEC_TRY(launch_bert_layernorm(t32, M, g1, b1, h32, hs, nullptr, s, MH));
+    MEC_TRY(prof.end(TAG_BERT_LN, s));
+    g = GemmParams();
+    g.split = 1; g.A = hs; g.a_lo = MH; g.B = wi; g.b_lo = wlo; g.oscale = sc[2];
+    g.bias = bi; g.act = ACT_GELU_EXACT; g.C16 = bigs; g.c_lo = MF; g.M = M; g.N = FF; g.K = H;
+    MEC_TRY(launch_gemm(g, s, &prof, TAG_BERT_FFN1));
+    g = GemmParams();
+    g.split = 1; g.A = bigs; g.a_lo = MF; g.B = wo2; g.b_lo = wlo; g.oscale = sc[3];
+    g.bias = bo2; g.R = h32; g.r_f32 = 1; g.C32 = t32; g.M = M; g.N = H; g.K = FF;
+    MEC_TRY(launch_gemm(g, s, &prof, TAG_BERT_FFN2));
+    MEC_TRY(prof.begin(TAG_BERT_LN, s));
+    MEC_TRY(launch_bert_layernorm(t32, M, g2, b2, h32, hs, nullptr, s, MH));
     MEC_TRY(prof.end(TAG_BERT_LN, s));
   }
   const float* head = P + PRM_LAYER * NL;

@@ -170,9 +170,15 @@ __device__ __forceinline__ void gemm_epilogue(const GemmParams& p, accv (&acc)[T
             for (int q = 0; q < 8; ++q) rv[ps][q] = __builtin_fmaf((rv[ps][q] - st.x) * st.y, lng[q], lnb[q]);
           }
         } else {
-          const half8 r8 = *reinterpret_cast<const half8*>(reinterpret_cast<const f16*>(p.R) + base);
+          const f16* R16 = reinterpret_cast<const f16*>(p.R) + base;
+          const half8 r8 = *reinterpret_cast<const half8*>(R16);
 #pragma unroll
           for (int q = 0; q < 8; ++q) rv[ps][q] = (float)r8[q];
+          if (p.r_lo) {  // split residual: hi + lo (exact in f32)
+            const half8 l8 = *reinterpret_cast<const half8*>(R16 + p.r_lo);
+#pragma unroll
+            for (int q = 0; q < 8; ++q) rv[ps][q] += (float)l8[q];
+          }
         }
       }
     } else {
@@ -188,8 +194,12 @@ __device__ __forceinline__ void gemm_epilogue(const GemmParams& p, accv (&acc)[T
       float v[8];
       const float4 x0 = *reinterpret_cast<const float4*>(stg + sr * EPI_LD + ech * 8);
       const float4 x1 = *reinterpret_cast<const float4*>(stg + sr * EPI_LD + ech * 8 + 4);
-      v[0] = x0.x + bias[0]; v[1] = x0.y + bias[1]; v[2] = x0.z + bias[2]; v[3] = x0.w + bias[3];
-      v[4] = x1.x + bias[4]; v[5] = x1.y + bias[5]; v[6] = x1.z + bias[6]; v[7] = x1.w + bias[7];
+      // acc * oscale + bias (oscale = 1 except on split operands: then fma(acc, 1, b) == acc + b)
+      const float os = p.oscale;
+      v[0] = __builtin_fmaf(x0.x, os, bias[0]); v[1] = __builtin_fmaf(x0.y, os, bias[1]);
+      v[2] = __builtin_fmaf(x0.z, os, bias[2]); v[3] = __builtin_fmaf(x0.w, os, bias[3]);
+      v[4] = __builtin_fmaf(x1.x, os, bias[4]); v[5] = __builtin_fmaf(x1.y, os, bias[5]);
+      v[6] = __builtin_fmaf(x1.z, os, bias[6]); v[7] = __builtin_fmaf(x1.w, os, bias[7]);
 #pragma unroll
       for (int q = 0; q < 8; ++q) v[q] += rv[ps][q];
       const int act = ACT >= 0 ? ACT : p.act;
@@ -217,6 +227,12 @@ __device__ __forceinline__ void gemm_epilogue(const GemmParams& p, accv (&acc)[T
 #pragma unroll
           for (int q = 0; q < 8; ++q) h[q] = (f16)v[q];
           *reinterpret_cast<half8*>(p.C16 + base) = h;
+          if (p.c_lo) {  // split output: the lo plane carries v - hi
+            half8 l;
+#pragma unroll
+            for (int q = 0; q < 8; ++q) l[q] = (f16)(v[q] - (float)h[q]);
+            *reinterpret_cast<half8*>(p.C16 + p.c_lo + base) = l;
+          }
         }
         if (p.C32) {
           *reinterpret_cast<float4*>(p.C32 + base) = make_float4(v[0], v[1], v[2], v[3]);

@@ -30,14 +30,17 @@ namespace mec {
 __device__ __attribute__((aligned(64))) uint4 g_zero_page[16];
 
 template <int BM, int BN, int WM, int WN, int NS, int AM, int DBG = 0, int MF = 32, int BK = 64, int PRE = 0,
-          int ACT = -1>
+          int ACT = -1, int SP = 0>
 __global__ __launch_bounds__(64 * WM * WN, (WM * WN == 4) ? 2 : 1) void gemm_glds_kernel(const GemmParams p) {
   // MF: 32 = v_mfma_f32_32x32x16_f16 tiles, 16 = v_mfma_f32_16x16x32_f16 tiles
   // DBG (probe builds only): 1 = no operand loads inside the K loop, 2 = no epilogue
   // PRE: the residual tile (1 = f16, 2 = f32) is loaded into registers before the main loop,
   // so its HBM read hides under the operand loads and MFMAs instead of following them
   // (ResNet's short-K conv3 GEMMs, BERT's O-projection)
+  // SP: split-f16 operands (GemmParams::split): the K loop runs over 3 K passes, pass 0 reading
+  // the A lo plane, pass 1 the B lo plane, pass 2 both hi planes
   static_assert(BK == 64 || BK == 32, "BK");
+  static_assert(SP == 0 || (AM != A_DUAL && PRE == 0), "split operands: plain or conv A, no prefetch");
   constexpr int CH = BK / 8;                   // 16-B chunks per LDS row
   constexpr int RPI = 64 / CH;                 // rows per glds wave-instruction (1 KB)
   constexpr int NW = WM * WN;
@@ -115,14 +118,22 @@ __global__ __launch_bounds__(64 * WM * WN, (WM * WN == 4) ? 2 : 1) void gemm_gld
   }
   const f16* zero = reinterpret_cast<const f16*>(g_zero_page);
 
+  const int nk0 = K / BK;  // K tiles per pass
   auto issue = [&](int stage, int kt) {
+    long long aoff = 0, boff = 0;
+    if constexpr (SP) {  // pass 0: A_lo . B_hi, pass 1: A_hi . B_lo, pass 2: A_hi . B_hi
+      const int pl = (kt >= nk0) + (kt >= 2 * nk0);
+      kt -= pl * nk0;
+      aoff = pl == 0 ? p.a_lo : 0;
+      boff = pl == 1 ? p.b_lo : 0;
+    }
     const int k0 = kt * BK;
     f16* sA = smem + stage * STAGE;
     f16* sB = sA + BM * BK;
     if constexpr (AM == A_PLAIN) {
 #pragma unroll
       for (int i = 0; i < AI; ++i) {
-        const f16* src = a_ok[i] ? a_src[i] + k0 : zero;
+        const f16* src = a_ok[i] ? a_src[i] + aoff + k0 : zero;
         __builtin_amdgcn_global_load_lds((const void*)src, (lds_vptr)(sA + (wave * AI + i) * RPI * BK), 16, 0, 0);
       }
     } else if constexpr (AM == A_DUAL) {
@@ -141,14 +152,14 @@ __global__ __launch_bounds__(64 * WM * WN, (WM * WN == 4) ? 2 : 1) void gemm_gld
       for (int i = 0; i < AI; ++i) {
         const int ih = a_ih0[i] + kh, iw = a_iw0[i] + kw;
         const bool ok = a_ok[i] && ih >= 0 && ih < p.H && iw >= 0 && iw < p.W;
-        const f16* src = ok ? a_src[i] + ((size_t)ih * p.W + iw) * p.C + c0 : zero;
+        const f16* src = ok ? a_src[i] + aoff + ((size_t)ih * p.W + iw) * p.C + c0 : zero;
         __builtin_amdgcn_global_load_lds((const void*)src, (lds_vptr)(sA + (wave * AI + i) * RPI * BK), 16, 0, 0);
       }
     }
 #pragma unroll
     for (int j = 0; j < BI; ++j)
-      __builtin_amdgcn_global_load_lds((const void*)(b_src[j] + k0), (lds_vptr)(sB + (wave * BI + j) * RPI * BK), 16,
-                                       0, 0);
+      __builtin_amdgcn_global_load_lds((const void*)(b_src[j] + boff + k0), (lds_vptr)(sB + (wave * BI + j) * RPI * BK),
+                                       16, 0, 0);
   };
 
   using EG = EpiGeom<BM, BN, WM, WN>;
@@ -180,7 +191,7 @@ __global__ __launch_bounds__(64 * WM * WN, (WM * WN == 4) ? 2 : 1) void gemm_gld
 #pragma unroll
       for (int e = 0; e < NACC; ++e) acc[i][j][e] = 0.f;
 
-  const int nk = K / BK;
+  const int nk = SP ? 3 * nk0 : nk0;
 #pragma unroll
   for (int s = 0; s < NS - 1; ++s)
     if (s < nk) issue(s, s);
@@ -331,13 +342,14 @@ __device__ __forceinline__ void pp_epilogue(const GemmParams& p, floatx4 (&acc)[
       for (int e = 0; e < 4; ++e) v[e] = (v[e] * 0.5f) * (1.0f + erff(v[e] * 0.70710678118654752f));
     }
   };
-  if (!p.R && p.C16 && !p.C32) {
+  const float os = p.oscale;  // 1 except on split operands: fma(acc, 1, b) == acc + b
+  if (!p.R && p.C16 && !p.C32 && !p.c_lo) {
 #pragma unroll
     for (int ia = 0; ia < NIA; ++ia)
 #pragma unroll
       for (int jb = 0; jb < 4; ++jb) {
-        float v[4] = {acc[ia][jb][0] + bb[jb].x, acc[ia][jb][1] + bb[jb].y, acc[ia][jb][2] + bb[jb].z,
-                      acc[ia][jb][3] + bb[jb].w};
+        float v[4] = {__builtin_fmaf(acc[ia][jb][0], os, bb[jb].x), __builtin_fmaf(acc[ia][jb][1], os, bb[jb].y),
+                      __builtin_fmaf(acc[ia][jb][2], os, bb[jb].z), __builtin_fmaf(acc[ia][jb][3], os, bb[jb].w)};
 #pragma unroll
         for (int e = 0; e < 4; ++e) v[e] += 0.f;  // gemm_epilogue's "+ residual" with none: -0 -> +0
         act4(v);
@@ -371,8 +383,10 @@ __device__ __forceinline__ void pp_epilogue(const GemmParams& p, floatx4 (&acc)[
 #pragma unroll
       for (int jb = 0; jb < 4; ++jb) {
         const int ia = sl * 2 + a;
-        const float4 v = make_float4(acc[ia][jb][0] + bb[jb].x, acc[ia][jb][1] + bb[jb].y,
-                                     acc[ia][jb][2] + bb[jb].z, acc[ia][jb][3] + bb[jb].w);
+        const float4 v = make_float4(__builtin_fmaf(acc[ia][jb][0], os, bb[jb].x),
+                                     __builtin_fmaf(acc[ia][jb][1], os, bb[jb].y),
+                                     __builtin_fmaf(acc[ia][jb][2], os, bb[jb].z),
+                                     __builtin_fmaf(acc[ia][jb][3], os, bb[jb].w));
         const int r = a * 16 + l16, x = jb * 4 + q;
         *reinterpret_cast<float4*>(reg + r * 256 + ((x ^ (r & 15)) << 4)) = v;
       }
@@ -395,9 +409,15 @@ __device__ __forceinline__ void pp_epilogue(const GemmParams& p, floatx4 (&acc)[
             rv[it][3] = __builtin_fmaf((rv[it][3] - st.x) * st.y, g4.w, b4.w);
           }
         } else {
-          const half4 r4 = *reinterpret_cast<const half4*>(reinterpret_cast<const f16*>(p.R) + base);
+          const f16* R16 = reinterpret_cast<const f16*>(p.R) + base;
+          const half4 r4 = *reinterpret_cast<const half4*>(R16);
 #pragma unroll
           for (int e = 0; e < 4; ++e) rv[it][e] = (float)r4[e];
+          if (p.r_lo) {  // split residual: hi + lo (exact in f32)
+            const half4 l4 = *reinterpret_cast<const half4*>(R16 + p.r_lo);
+#pragma unroll
+            for (int e = 0; e < 4; ++e) rv[it][e] += (float)l4[e];
+          }
         }
       }
     }
@@ -415,6 +435,12 @@ __device__ __forceinline__ void pp_epilogue(const GemmParams& p, floatx4 (&acc)[
 #pragma unroll
           for (int e = 0; e < 4; ++e) h[e] = (f16)v[e];
           *reinterpret_cast<half4*>(p.C16 + base) = h;
+          if (p.c_lo) {  // split output: the lo plane carries v - hi
+            half4 l;
+#pragma unroll
+            for (int e = 0; e < 4; ++e) l[e] = (f16)(v[e] - (float)h[e]);
+            *reinterpret_cast<half4*>(p.C16 + p.c_lo + base) = l;
+          }
         }
         if (p.C32) *reinterpret_cast<float4*>(p.C32 + base) = make_float4(v[0], v[1], v[2], v[3]);
       }
@@ -439,7 +465,7 @@ __device__ __forceinline__ void pp_epilogue(const GemmParams& p, floatx4 (&acc)[
 // DBG = 4 (probe build, tools/pp_trace.py): s_memtime at four points of every phase of the
 // first 12 K tiles, per wave, kept in spare LDS and dumped by one block into C32. DBG = 5
 // (probe): the epilogue computes everything but stores nothing.
-template <int AM, int DBG = 0, int BM = 256, int ACT = -1>
+template <int AM, int DBG = 0, int BM = 256, int ACT = -1, int SP = 0>
 __global__ __launch_bounds__(512) void gemm_pp_kernel(const GemmParams p) {
   static_assert(AM == A_PLAIN, "ping-pong tile: plain A only");
   static_assert(BM == 256 || BM == 128, "BM");
@@ -501,22 +527,31 @@ __global__ __launch_bounds__(512) void gemm_pp_kernel(const GemmParams p) {
     }
   }
   const f16* zero = reinterpret_cast<const f16*>(g_zero_page);
+  const int nk0 = K / BK;  // K tiles per pass (SP: three passes, as gemm_glds_kernel)
   // piece: 0 = A0, 1 = A1, 2 = B0, 3 = B1
   auto issue = [&](const int piece, const int kt) {
     f16* base = smem + (kt & 1) * BUF;
-    const int k0 = kt * BK;
+    int kk = kt;
+    long long aoff = 0, boff = 0;
+    if constexpr (SP) {
+      const int pl = (kt >= nk0) + (kt >= 2 * nk0);
+      kk = kt - pl * nk0;
+      aoff = pl == 0 ? p.a_lo : 0;
+      boff = pl == 1 ? p.b_lo : 0;
+    }
+    const int k0 = kk * BK;
     if (piece < 2) {
       f16* dst = base + piece * OFF_A1;
 #pragma unroll
       for (int i = 0; i < GA; ++i) {
-        const f16* src = a_ok[piece][i] ? a_src[piece][i] + k0 : zero;
+        const f16* src = a_ok[piece][i] ? a_src[piece][i] + aoff + k0 : zero;
         __builtin_amdgcn_global_load_lds((const void*)src, (lds_vptr)(dst + (wave * GA + i) * 8 * BK), 16, 0, 0);
       }
     } else {
       f16* dst = base + (piece == 2 ? OFF_B0 : OFF_B1);
 #pragma unroll
       for (int i = 0; i < GB; ++i)
-        __builtin_amdgcn_global_load_lds((const void*)(b_src[piece - 2][i] + k0),
+        __builtin_amdgcn_global_load_lds((const void*)(b_src[piece - 2][i] + boff + k0),
                                          (lds_vptr)(dst + (wave * GB + i) * 8 * BK), 16, 0, 0);
     }
   };
@@ -572,7 +607,7 @@ __global__ __launch_bounds__(512) void gemm_pp_kernel(const GemmParams p) {
     __builtin_amdgcn_sched_barrier(0);
   };
 
-  const int nk = K / BK;
+  const int nk = SP ? 3 * nk0 : nk0;
   issue(0, 0);
   issue(3, 0);
   issue(1, 0);
@@ -644,7 +679,16 @@ __global__ __launch_bounds__(512) void gemm_pp_kernel(const GemmParams p) {
 
 template <int BM, int BN, int WM, int WN, int NS, int MF, int BK, int ACT>
 static int launch_cfg_act(const GemmParams& p, hipStream_t s, int nwg, dim3 blk) {
-  if (BM * BN <= 128 * 128 && opt().gemm_prefetch_r && p.amode == A_PLAIN && p.R && !p.r_f32 && p.K <= 512) {
+  if (p.split) {  // split-f16 operands (fp32x3 path): three K passes, runtime activation
+    if (p.amode == A_PLAIN)
+      hipLaunchKernelGGL((gemm_glds_kernel<BM, BN, WM, WN, NS, A_PLAIN, 0, MF, BK, 0, -1, 1>), dim3(nwg), blk, 0, s, p);
+    else if (p.amode == A_CONV)
+      hipLaunchKernelGGL((gemm_glds_kernel<BM, BN, WM, WN, NS, A_CONV, 0, MF, BK, 0, -1, 1>), dim3(nwg), blk, 0, s, p);
+    else {
+      set_error("gemm_glds: split operands take a plain or conv A");
+      return -1;
+    }
+  } else if (BM * BN <= 128 * 128 && opt().gemm_prefetch_r && p.amode == A_PLAIN && p.R && !p.r_f32 && p.K <= 512) {
     // f16 residual prefetch for ResNet's short-K conv3 GEMMs (small tiles only: no spills);
     // 225 -> 170 us on layer1's conv3. The f32 form (PRE = 2, BERT's O-projection, K = 768)
     // measured 10-15% slower than no prefetch, so it is not dispatched.
@@ -675,6 +719,7 @@ static int launch_cfg(const GemmParams& p, hipStream_t s) {
   }
 #endif
   // the activation is a template argument for ReLU (ResNet) and none (BERT O-proj); others runtime
+  if (p.split) return launch_cfg_act<BM, BN, WM, WN, NS, MF, BK, -1>(p, s, nwg, blk);
   if (p.act == ACT_RELU) return launch_cfg_act<BM, BN, WM, WN, NS, MF, BK, ACT_RELU>(p, s, nwg, blk);
   if (p.act == ACT_NONE) return launch_cfg_act<BM, BN, WM, WN, NS, MF, BK, ACT_NONE>(p, s, nwg, blk);
   return launch_cfg_act<BM, BN, WM, WN, NS, MF, BK, -1>(p, s, nwg, blk);
@@ -686,8 +731,8 @@ static int launch_cfg(const GemmParams& p, hipStream_t s) {
 // being captured into a graph) and caches the fastest; `gemm_bn` forces a width.
 // Cache key: engine 0 (this engine) + the shape; the cache is the calling handle's
 // (tune_cache(), mec_common.h).
-static std::array<int, 11> gemm_key(const GemmParams& p) {
-  return {0, p.amode, p.M, p.N, p.K, p.H, p.W, p.C, p.ks, p.stride, p.pad};
+static std::array<int, 11> gemm_key(const GemmParams& p) {  // engine slot: 0, or 2 for split operands
+  return {p.split ? 2 : 0, p.amode, p.M, p.N, p.K, p.H, p.W, p.C, p.ks, p.stride, p.pad};
 }
 
 // Tile configs (id): 256 / 128 / 64 = 256 x BN with 8 waves; 1128 / 1064 = 128 x BN with
@@ -748,7 +793,12 @@ static int launch_bn(const GemmParams& p, hipStream_t s, int id) {
       else
 #endif
       // the activation is a template argument for the common cases: one epilogue path per kernel
-      if (id == 40256) {
+      if (p.split) {
+        if (id == 40256)
+          hipLaunchKernelGGL((gemm_pp_kernel<A_PLAIN, 0, 256, -1, 1>), grd, blk, 0, s, p);
+        else
+          hipLaunchKernelGGL((gemm_pp_kernel<A_PLAIN, 0, 128, -1, 1>), grd, blk, 0, s, p);
+      } else if (id == 40256) {
         if (p.act == ACT_GELU)
           hipLaunchKernelGGL((gemm_pp_kernel<A_PLAIN, 0, 256, ACT_GELU>), grd, blk, 0, s, p);
         else if (p.act == ACT_RELU)
@@ -808,7 +858,10 @@ static int tune_bn(const GemmParams& p, hipStream_t s, int* out_bn) {
   return 0;
 }
 
-int gemm_tuned_bn(int amode, int M, int N, int K) { return tune_cache().find_shape(0, amode, M, N, K); }
+int gemm_tuned_bn(int amode, int M, int N, int K) {
+  const int t = tune_cache().find_shape(0, amode, M, N, K);
+  return t ? t : tune_cache().find_shape(2, amode, M, N, K);  // else the split-operand engine's
+}
 
 int launch_gemm_glds(const GemmParams& p, hipStream_t s, int force_bn) {
   if (force_bn) {
@@ -826,8 +879,8 @@ int launch_gemm_glds(const GemmParams& p, hipStream_t s, int force_bn) {
     }
     tune_cache().put(key, bn);
     if (getenv("MEC_GEMM_TRACE"))  // one line per distinct shape, at its first launch
-      fprintf(stderr, "MEC_GEMM amode=%d M=%d N=%d K=%d H=%d C=%d ks=%d stride=%d act=%d R=%d r_f32=%d tile=%d\n",
-              p.amode, p.M, p.N, p.K, p.H, p.C, p.ks, p.stride, p.act, p.R != nullptr, p.r_f32, bn);
+      fprintf(stderr, "MEC_GEMM amode=%d M=%d N=%d K=%d H=%d C=%d ks=%d stride=%d act=%d R=%d r_f32=%d split=%d tile=%d\n",
+              p.amode, p.M, p.N, p.K, p.H, p.C, p.ks, p.stride, p.act, p.R != nullptr, p.r_f32, p.split, bn);
   }
   return launch_bn(p, s, bn);
 }

@@ -215,6 +215,17 @@ struct GemmParams {
   // conv geometry (NHWC input)
   int H = 1, W = 1, C = 0, OH = 1, OW = 1, ks = 1, stride = 1, pad = 0;
   int group_m = 0;  // ping-pong tile order inside an XCD's range: 0 row-major, G = G-row groups
+  // Split-f16 operands (the MEC_PREC_FP32X3 path, f16 engine only): A and B are each an f16
+  // hi plane and an f16 lo plane (x = hi + lo exactly, |lo| <= 2^-11 |hi|), the lo planes at
+  // element offsets a_lo / b_lo from A / B. The K loop makes three passes over K, A_lo.B_hi,
+  // A_hi.B_lo, A_hi.B_hi, into one fp32 accumulator (the dropped A_lo.B_lo term is below
+  // 2^-22 |A B|). oscale (a power of two: undoes the weights' pre-scale, exact) multiplies the
+  // accumulator before the bias; it is 1 (an exact no-op) everywhere else.
+  int split = 0;
+  long long a_lo = 0, b_lo = 0;
+  float oscale = 1.f;
+  long long c_lo = 0;  // != 0: C16 is written as a hi plane and a lo plane (C16 + c_lo): f16(v), f16(v - hi)
+  long long r_lo = 0;  // != 0: the f16 residual R is a hi plane + a lo plane at R + r_lo (R = hi + lo)
 };
 
 int launch_gemm(const GemmParams& p, hipStream_t s, Prof* prof, int tag);

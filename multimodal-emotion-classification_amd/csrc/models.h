@@ -13,7 +13,12 @@ size_t blob_floats(int kind);
 // Arithmetic of a handle (mec_create_ex): PREC_F16 = f16 MFMA operands with fp32
 // accumulation / LayerNorm / softmax / residual stream (the fast path); PREC_FP32 = every
 // operand and product in fp32 (v_mfma_f32_32x32x2_f32), the reference's own precision.
-enum Precision : int { PREC_F16 = 0, PREC_FP32 = 1 };
+// PREC_FP32X3 = fp32 arithmetic on the f16 MFMA: every fp32 GEMM operand x is carried as an
+// exact pair of f16 planes x = hi + lo, and each product as hi.hi + hi.lo + lo.hi in one fp32
+// accumulator (gemm_glds.hip split mode; 22 significant bits per operand against fp32's 24,
+// the dropped lo.lo term below 2^-22 of the product); LayerNorm, softmax, attention, GELU, the
+// residual stream and the heads are fp32 exactly as on the fp32 path.
+enum Precision : int { PREC_F16 = 0, PREC_FP32 = 1, PREC_FP32X3 = 2 };
 
 struct Model {
   int kind = -1;
@@ -85,10 +90,24 @@ struct TextModel : Model {
               float* probs, hipStream_t s);
   int forward_f32(const int32_t* ids, const int32_t* mask, int B, int L, float* cls, float* logits,
                   float* probs, hipStream_t s);  // bert_f32.hip
+  // fp32x3 path: wts holds the hi planes, then the lo planes (at x3_lo halfs); per GEMM B matrix
+  // (4 per layer) the epilogue scale 2^-e of its planes
+  size_t x3_lo = 0;
+  std::vector<float> x3_scale;
+  int forward_x3(const int32_t* ids, const int32_t* mask, int B, int L, float* cls, float* logits,
+                 float* probs, hipStream_t s);  // bert_f32.hip
 };
-int launch_bert_embed_ln(const int32_t* ids, int M, int L, const float* emb, float* h32, f16* h16, hipStream_t s);
+// lo != 0 (fp32x3 path): h16 is written as a hi plane and h16 + lo as the lo plane f16(y - hi)
+int launch_bert_embed_ln(const int32_t* ids, int M, int L, const float* emb, float* h32, f16* h16, hipStream_t s,
+                         long long lo = 0);
 int launch_bert_layernorm(const float* x, int M, const float* g, const float* b, float* h32, f16* h16, float2* stats,
-                          hipStream_t s);
+                          hipStream_t s, long long lo = 0);
+
+// Split n fp32 weights into f16 planes for the fp32x3 path: hi = f16(w 2^e), lo = f16(w 2^e - hi)
+// with e the largest power of two keeping max |w| 2^e <= 2^14 (so hi never overflows and lo
+// stays out of the f16 subnormals for all but the smallest weights); returns 2^-e, the GEMM
+// epilogue's oscale. Host code (runtime.hip).
+float split_planes(const float* w, size_t n, f16* hi, f16* lo);
 
 // ---------------------------------------------------------------- image encoders
 // Both backbones take the same u8 inputs and produce the same (512-d feature, logits, probs).
@@ -106,6 +125,7 @@ struct ConvLayer {
   size_t w_off = 0;   // f16 [Cout][kh][kw][Cin] (BN scale folded)
   size_t b_off = 0;   // f32 [Cout] (BN shift)
   int cin = 0, cout = 0, ks = 1, stride = 1, pad = 0;
+  float x3_scale = 1.f;  // fp32x3 path: the epilogue scale 2^-e of this conv's weight planes
 };
 struct Bottleneck {
   ConvLayer c1, c2, c3, ds;
@@ -132,6 +152,11 @@ struct ImageModel : ImageNet {
                  hipStream_t s) override;
   int forward_f32(const uint8_t* img, int B, int H, int W, int C, float* feat, float* logits, float* probs,
                   hipStream_t s);
+  // fp32x3 path (resnet_f32.hip): wts holds every bottleneck conv's f16 hi planes, then the lo
+  // planes at x3_lo halfs (w_off indexes both); the stem, pooling and head run as on the fp32 path
+  size_t x3_lo = 0;
+  int forward_x3(const uint8_t* img, int B, int H, int W, int C, float* feat, float* logits, float* probs,
+                 hipStream_t s);
 };
 
 // ---------------------------------------------------------------- MobileNetV2 + head
@@ -159,6 +184,11 @@ struct MobileNetModel : ImageNet {
                  hipStream_t s) override;
   int forward_f32(const uint8_t* img, int B, int H, int W, int C, float* feat, float* logits, float* probs,
                   hipStream_t s);
+  // fp32x3 path (resnet_f32.hip): wts holds every bottleneck conv's f16 hi planes, then the lo
+  // planes at x3_lo halfs (w_off indexes both); the stem, pooling and head run as on the fp32 path
+  size_t x3_lo = 0;
+  int forward_x3(const uint8_t* img, int B, int H, int W, int C, float* feat, float* logits, float* probs,
+                 hipStream_t s);
 };
 
 int resize_u8(const uint8_t* in, int B, int H, int W, uint8_t* out, int OH, int OW, hipStream_t s);

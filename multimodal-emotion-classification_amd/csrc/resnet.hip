@@ -361,7 +361,7 @@ __global__ __launch_bounds__(256, 2) void stem_pool_kernel(const uint8_t* __rest
 static const int kLayers[4][3] = {{64, 3, 1}, {128, 4, 2}, {256, 6, 2}, {512, 3, 2}};
 
 int ImageModel::create(const float* blob, size_t n) {
-  if (prec == PREC_FP32) {  // resnet_f32.hip
+  if (prec == PREC_FP32 || prec == PREC_FP32X3) {  // resnet_f32.hip
     MEC_TRY(create_f32(blob, n));
     return ensure_taps();
   }
@@ -506,6 +506,7 @@ int ImageModel::forward_u8(const uint8_t* img, int B, int H, int W, int C, float
   MEC_REQUIRE(fer || (H == 224 && W == 224 && (C == 1 || C == 3)),
               "image: input must be u8 [B,48,48,1] (GPU resize) or [B,224,224,{1,3}] (already resized)");
   if (prec == PREC_FP32) return forward_f32(img, B, H, W, C, feat, logits, probs, s);
+  if (prec == PREC_FP32X3) return forward_x3(img, B, H, W, C, feat, logits, probs, s);
   const size_t per_img_big = (size_t)56 * 56 * 256;  // largest NHWC activation (elements)
   const size_t per_t1 = (size_t)56 * 56 * 128, per_t2 = (size_t)56 * 56 * 64;
   const size_t per_img = 224 * 224 + (2 * per_img_big + per_t1 + per_t2) * sizeof(f16) + 256 + 2048 * sizeof(float);

@@ -306,7 +306,49 @@ int ImageModel::create_f32(const float* blob, size_t n) {
   pr.insert(pr.end(), f2b, f2b + 7);
   MEC_TRY(upload(wts32, w.data(), w.size() * sizeof(float)));
   MEC_TRY(upload(prm, pr.data(), pr.size() * sizeof(float)));
+  if (prec == PREC_FP32X3) {
+    // every bottleneck conv's weights scaled by 2^e and split into f16 hi / lo planes, at the
+    // same offsets as in wts32 (the stem keeps its f32 weights: it runs the fp32 kernels)
+    std::vector<f16> hl(2 * w.size(), (f16)0.f);
+    x3_lo = w.size();
+    auto split = [&](ConvLayer& L) {
+      const size_t cnt = (size_t)L.cout * L.cin * L.ks * L.ks;
+      L.x3_scale = split_planes(w.data() + L.w_off, cnt, hl.data() + L.w_off, hl.data() + x3_lo + L.w_off);
+    };
+    for (Bottleneck& bk : blocks) {
+      split(bk.c1);
+      split(bk.c2);
+      split(bk.c3);
+      if (bk.has_ds) split(bk.ds);
+    }
+    MEC_TRY(upload(wts, hl.data(), hl.size() * sizeof(f16)));
+  }
   return 0;
+}
+
+// fp32 tensor -> f16 hi / lo planes (the fp32x3 path's stem output): hi = f16(x), lo = f16(x - hi)
+__global__ __launch_bounds__(256) void split_f32_kernel(const float* __restrict__ x, size_t n4, f16* __restrict__ hi,
+                                                        long long lo) {
+  const size_t i = (size_t)blockIdx.x * 256 + threadIdx.x;
+  if (i >= n4) return;
+  const float4 v = reinterpret_cast<const float4*>(x)[i];
+  const half4 h = {(f16)v.x, (f16)v.y, (f16)v.z, (f16)v.w};
+  const half4 l = {(f16)(v.x - (float)h[0]), (f16)(v.y - (float)h[1]), (f16)(v.z - (float)h[2]),
+                   (f16)(v.w - (float)h[3])};
+  reinterpret_cast<half4*>(hi)[i] = h;
+  reinterpret_cast<half4*>(hi + lo)[i] = l;
+}
+
+// global average pool of an NHWC tensor held as f16 hi / lo planes (x = hi + lo exactly), the
+// same summation order as avgpool_f32_kernel
+__global__ __launch_bounds__(256) void avgpool_split_kernel(const f16* __restrict__ x, long long lo, int HW, int C,
+                                                            float* __restrict__ y) {
+  const int b = blockIdx.x, c = blockIdx.y * 256 + threadIdx.x;
+  if (c >= C) return;
+  const f16* p = x + (size_t)b * HW * C + c;
+  float s = 0.f;
+  for (int q = 0; q < HW; ++q) s += (float)p[(size_t)q * C] + (float)p[(size_t)q * C + lo];
+  y[(size_t)b * C + c] = s / (float)HW;
 }
 
 int ImageModel::forward_f32(const uint8_t* img, int B, int H, int W, int C, float* feat, float* logits, float* probs,
@@ -401,6 +443,123 @@ int ImageModel::forward_f32(const uint8_t* img, int B, int H, int W, int C, floa
     Hc = OH;
   }
   hipLaunchKernelGGL(avgpool_f32_kernel, dim3(B, 2048 / 256), dim3(256), 0, s, cur, Hc * Hc, 2048, pooled);
+  MEC_LAUNCH_CHECK();
+  MEC_TRY(launch_linear_mfma<BACT_RELU>(pooled, 2048, B, 2048, P + fc1_off, P + fc1b_off, 512, feat, 512, nullptr, 0, s));
+  MEC_TRY(launch_head7(feat, B, 512, P + fc2_off, P + fc2b_off, logits, probs, s));
+  return 0;
+}
+
+// fp32x3 path: the fp32 path with every bottleneck conv on split-f16 operands (gemm_glds.hip
+// split mode: A_PLAIN 1x1 convs and A_CONV 3x3 / strided 1x1 convs, three f16 MFMA passes into
+// one fp32 accumulator, weights pre-scaled by 2^e and undone in the epilogue). Activations
+// between convs are f16 hi / lo planes (the same bytes as f32); the downsample branch is written
+// in f32 and added as an f32 residual; an identity residual is added as hi + lo (exact). The
+// stem (conv + BN + ReLU + max-pool), the average pool and the head are the fp32 path's kernels.
+int ImageModel::forward_x3(const uint8_t* img, int B, int H, int W, int C, float* feat, float* logits, float* probs,
+                           hipStream_t s) {
+  MEC_REQUIRE(wts.p && wts32.p && x3_lo, "image: fp32x3 weights missing");
+  const bool fer = (H == 48 && W == 48 && C == 1);
+  // per image (floats): im2col 12544 x 160 (RGB stem); S32 112*112*64 (stem f32 out, then the
+  // f32 downsample DS); X, Y as hi|lo planes of 56*56*256; T1 (56*56*128), T2 (56*56*64) planes
+  const size_t big = (size_t)56 * 56 * 256, t1n = (size_t)56 * 56 * 128, t2n = (size_t)56 * 56 * 64;
+  const size_t per_img = 224 * 224 + ((size_t)12544 * STEM_K + (size_t)112 * 112 * 64 + 2 * big + t1n + t2n + 2048) * 4;
+  const size_t need = per_img * (size_t)B + 8192;
+  if (ws.bytes < need) MEC_TRY(ws.ensure(need));
+  char* p = ws.as<char>();
+  uint8_t* resized = reinterpret_cast<uint8_t*>(p);
+  p += ((size_t)B * 224 * 224 + 255) / 256 * 256;
+  float* A0 = reinterpret_cast<float*>(p); p += (size_t)B * 12544 * STEM_K * 4;
+  float* S32 = reinterpret_cast<float*>(p); p += (size_t)B * 112 * 112 * 64 * 4;
+  f16* X = reinterpret_cast<f16*>(p); p += (size_t)B * big * 4;
+  f16* Y = reinterpret_cast<f16*>(p); p += (size_t)B * big * 4;
+  f16* T1 = reinterpret_cast<f16*>(p); p += (size_t)B * t1n * 4;
+  f16* T2 = reinterpret_cast<f16*>(p); p += (size_t)B * t2n * 4;
+  float* pooled = reinterpret_cast<float*>(p);
+  const long long lo_big = (long long)B * big, lo_t1 = (long long)B * t1n, lo_t2 = (long long)B * t2n;
+
+  const float* Wt32 = wts32.as<float>();
+  const f16* Wt = wts.as<f16>();
+  const long long wlo = (long long)x3_lo;
+  const float* P = prm.as<float>();
+  const uint8_t* stem_in = img;
+  int Cin = C;
+  if (fer) {
+    MEC_TRY(resize_u8(img, B, 48, 48, resized, 224, 224, s));
+    stem_in = resized;
+    Cin = 1;
+  }
+  // stem -> S32 f32 [B,56,56,64] (the fp32 path's kernels), then split into X's planes
+  MEC_TRY(prof.begin(TAG_RESNET_STEM, s));
+  if (Cin == 1 && opt().stem_gray_f32) {
+    static int ncu = 0;
+    if (!ncu) {
+      int dev = 0;
+      MEC_HIP(hipGetDevice(&dev));
+      MEC_HIP(hipDeviceGetAttribute(&ncu, hipDeviceAttributeMultiprocessorCount, dev));
+    }
+    const int ntiles = B * 49;
+    hipLaunchKernelGGL(stem_pool_gray_f32_kernel, dim3(std::min(ntiles, ncu)), dim3(512), 0, s, stem_in, ntiles,
+                       Wt32 + stem_gray32_off, P + stem.b_off, S32);
+    MEC_LAUNCH_CHECK();
+  } else {
+    const size_t total = (size_t)B * 112 * 112 * (STEM_K / 4);
+    hipLaunchKernelGGL(stem_im2col_f32_kernel, dim3((unsigned)((total + 255) / 256)), dim3(256), 0, s, stem_in, B,
+                       Cin, A0);
+    MEC_LAUNCH_CHECK();
+    GemmParams g;  // the stem output (112 x 112) goes to the f32 scratch in the ping buffer's bytes
+    float* Y32 = reinterpret_cast<float*>(Y);
+    g.A = A0; g.B32 = Wt32 + stem.w_off; g.bias = P + stem.b_off; g.act = ACT_RELU; g.C32 = Y32;
+    g.M = B * 112 * 112; g.N = 64; g.K = STEM_K;
+    MEC_TRY(launch_gemm_f32(g, s, nullptr, 0));
+    const size_t tp = (size_t)B * 56 * 56 * 16;
+    hipLaunchKernelGGL(maxpool_f32_kernel, dim3((unsigned)((tp + 255) / 256)), dim3(256), 0, s, Y32, B, 112, 64, 56, S32);
+    MEC_LAUNCH_CHECK();
+  }
+  {
+    const size_t n4 = (size_t)B * 56 * 56 * 64 / 4;
+    hipLaunchKernelGGL(split_f32_kernel, dim3((unsigned)((n4 + 255) / 256)), dim3(256), 0, s, S32, n4, X, lo_big);
+    MEC_LAUNCH_CHECK();
+  }
+  MEC_TRY(prof.end(TAG_RESNET_STEM, s));
+  float* DS = S32;  // the stem's f32 scratch, reused for the downsample branch
+  GemmParams g;
+  f16* cur = X;
+  f16* other = Y;
+  int Hc = 56;
+  for (const Bottleneck& bk : blocks) {
+    const int wd = bk.c1.cout, cin = bk.c1.cin, st = bk.c2.stride;
+    const int OH = (Hc + 2 - 3) / st + 1;
+    g = GemmParams();
+    g.split = 1; g.A = cur; g.a_lo = lo_big; g.B = Wt + bk.c1.w_off; g.b_lo = wlo; g.oscale = bk.c1.x3_scale;
+    g.bias = P + bk.c1.b_off; g.act = ACT_RELU; g.C16 = T1; g.c_lo = lo_t1;
+    g.M = B * Hc * Hc; g.N = wd; g.K = cin;
+    MEC_TRY(launch_gemm(g, s, &prof, TAG_RESNET_CONV1X1));
+    g = GemmParams();
+    g.split = 1; g.amode = A_CONV; g.A = T1; g.a_lo = lo_t1; g.B = Wt + bk.c2.w_off; g.b_lo = wlo;
+    g.oscale = bk.c2.x3_scale; g.bias = P + bk.c2.b_off; g.act = ACT_RELU; g.C16 = T2; g.c_lo = lo_t2;
+    g.M = B * OH * OH; g.N = wd; g.K = 9 * wd;
+    g.H = Hc; g.W = Hc; g.C = wd; g.OH = OH; g.OW = OH; g.ks = 3; g.stride = st; g.pad = 1;
+    MEC_TRY(launch_gemm(g, s, &prof, TAG_RESNET_CONV3X3));
+    g = GemmParams();  // relu(bn3(conv3(t2)) + identity)
+    if (bk.has_ds) {  // downsample = BN(conv1x1/s(x)) in f32, added as an f32 residual
+      GemmParams d;
+      d.split = 1; d.amode = A_CONV; d.A = cur; d.a_lo = lo_big; d.B = Wt + bk.ds.w_off; d.b_lo = wlo;
+      d.oscale = bk.ds.x3_scale; d.bias = P + bk.ds.b_off; d.C32 = DS;
+      d.M = B * OH * OH; d.N = 4 * wd; d.K = cin;
+      d.H = Hc; d.W = Hc; d.C = cin; d.OH = OH; d.OW = OH; d.ks = 1; d.stride = st; d.pad = 0;
+      MEC_TRY(launch_gemm(d, s, &prof, TAG_RESNET_CONV1X1));
+      g.R = DS; g.r_f32 = 1;
+    } else {
+      g.R = cur; g.r_lo = lo_big;
+    }
+    g.split = 1; g.A = T2; g.a_lo = lo_t2; g.B = Wt + bk.c3.w_off; g.b_lo = wlo; g.oscale = bk.c3.x3_scale;
+    g.bias = P + bk.c3.b_off; g.act = ACT_RELU; g.C16 = other; g.c_lo = lo_big;
+    g.M = B * OH * OH; g.N = 4 * wd; g.K = wd;
+    MEC_TRY(launch_gemm(g, s, &prof, TAG_RESNET_CONV1X1));
+    std::swap(cur, other);
+    Hc = OH;
+  }
+  hipLaunchKernelGGL(avgpool_split_kernel, dim3(B, 2048 / 256), dim3(256), 0, s, cur, lo_big, Hc * Hc, 2048, pooled);
   MEC_LAUNCH_CHECK();
   MEC_TRY(launch_linear_mfma<BACT_RELU>(pooled, 2048, B, 2048, P + fc1_off, P + fc1b_off, 512, feat, 512, nullptr, 0, s));
   MEC_TRY(launch_head7(feat, B, 512, P + fc2_off, P + fc2b_off, logits, probs, s));

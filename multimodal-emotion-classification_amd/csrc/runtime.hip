@@ -1,4 +1,7 @@
 // Runtime plumbing: thread-local error string, device buffers, hipEvent timing hook.
+#include <algorithm>
+#include <cmath>
+
 #include "mec_common.h"
 
 namespace mec {
@@ -84,6 +87,23 @@ int Prof::read(double* total_ms, int* count) {
 
 Prof::~Prof() {
   for (auto e : ev) (void)hipEventDestroy(e);
+}
+
+float split_planes(const float* w, size_t n, f16* hi, f16* lo) {
+  float mx = 0.f;
+  for (size_t i = 0; i < n; ++i) mx = std::max(mx, std::fabs(w[i]));
+  int e = 0;
+  if (mx > 0.f && std::isfinite(mx)) {
+    e = (int)std::floor(std::log2(16384.0 / (double)mx));
+    while (std::ldexp((double)mx, e) > 16384.0) --e;  // guard the log2 rounding
+  }
+  for (size_t i = 0; i < n; ++i) {
+    const float x = std::ldexp(w[i], e);  // exact (power of two), unless it leaves the f32 range
+    const f16 h = (f16)x;
+    hi[i] = h;
+    lo[i] = (f16)(x - (float)h);  // x - hi is exact in f32
+  }
+  return std::ldexp(1.0f, -e);
 }
 
 }  // namespace mec

@@ -60,8 +60,9 @@ TAGS = {'bert_qkv': 1, 'bert_attn': 2, 'bert_oproj': 3, 'bert_ffn1': 4, 'bert_ff
 
 
 # Handle precision (include/mec.h MEC_PREC_*): 'f16' = f16 MFMA operands with fp32
-# accumulation / LayerNorm / softmax / residual (the fast path), 'fp32' = fp32 throughout.
-PRECISIONS = {'f16': 0, 'fp32': 1}
+# accumulation / LayerNorm / softmax / residual (the fast path), 'fp32' = fp32 throughout,
+# 'fp32x3' = the fp32 path with its GEMM operands as exact f16 hi/lo pairs on the f16 MFMA.
+PRECISIONS = {'f16': 0, 'fp32': 1, 'fp32x3': 2}
 
 
 class MecError(RuntimeError):

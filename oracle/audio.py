@@ -180,9 +180,10 @@ def piptrack(S, sr=SR, n_fft=N_FFT, fmin=150.0, fmax=4000.0, threshold=0.1):
     return pitches, mags
 
 
-def estimate_tuning_index(S):
-    """librosa.estimate_tuning(S=S, sr, bins_per_octave=12) -> index into TUNING_EDGES."""
-    pitch, mag = piptrack(S)
+def estimate_tuning_index(S, sr=SR):
+    """librosa.estimate_tuning(S=S, sr=sr, bins_per_octave=12) -> index into TUNING_EDGES
+    (estimate_tuning passes sr on to piptrack: the pitch of a bin is (bin + shift) * sr / n_fft)."""
+    pitch, mag = piptrack(S, sr=sr)
     mask = pitch > 0
     thr = np.median(mag[mask]) if mask.any() else 0.0
     freqs = pitch[(mag >= thr) & mask]
@@ -206,7 +207,7 @@ def features(y, sr=SR, tuning_index=None):
     mel = np.einsum('ft,mf->mt', P, mel_filters(sr), optimize=True)
     mfcc = scipy.fftpack.dct(power_to_db(mel), axis=0, type=2, norm='ortho')[:N_MFCC]
     f_mfcc = np.mean(mfcc.T, axis=0)
-    tidx = estimate_tuning_index(P) if tuning_index is None else tuning_index
+    tidx = estimate_tuning_index(P, sr) if tuning_index is None else tuning_index
     fb = chroma_filters(float(TUNING_EDGES[tidx]), sr)
     chroma = normalize(np.einsum('cf,ft->ct', fb, P, optimize=True), norm=np.inf, axis=0)
     f_chroma = np.mean(chroma.T, axis=0)

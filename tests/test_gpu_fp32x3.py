@@ -1,0 +1,114 @@
+"""GPU: the fp32x3 path (MEC_PREC_FP32X3) -- the fp32 path's arithmetic with every GEMM / conv
+operand carried as an exact f16 hi/lo pair on the f16 MFMA (three products per fp32 product,
+one fp32 accumulator) -- held to the fp32 path's own bars against the oracle: probs within
+1e-5, features within 1e-4 relative, argmax exact on every row; and compared with the exact
+fp32 path on the same inputs (the two differ by reassociation-scale amounts only)."""
+import numpy as np
+import pytest
+import torch
+
+from mec import engine, synthetic as syn
+from oracle import image as o_i, text as o_t
+
+pytestmark = pytest.mark.gpu
+
+PROB_TOL, FEAT_RTOL = 1e-5, 1e-4
+
+
+def _np(ts):
+    torch.cuda.synchronize()
+    return [t.cpu().numpy() for t in ts]
+
+
+def _report(name, got, ref, got32):
+    err = float(np.abs(got - ref).max())
+    e32 = float(np.abs(got32 - ref).max())
+    agree = int((got.argmax(1) == ref.argmax(1)).sum())
+    s = np.sort(ref, axis=1)
+    print(f'{name}: probs max|d| vs oracle {err:.3g} (exact fp32 path {e32:.3g}), argmax {agree}/{len(got)}, '
+          f'min top-2 margin {(s[:, -1] - s[:, -2]).min():.3g}')
+    return err, agree
+
+
+@pytest.mark.parametrize('B,ragged', [(3, True), (64, True), (128, False)])
+def test_text_fp32x3_vs_oracle(dev, B, ragged):
+    ids, mask = syn.text_inputs(B, 128, seed=500 + B, ragged=ragged)
+    args = (engine.to_device(ids, dev), engine.to_device(mask, dev))
+    cls, logits, probs = _np(engine.TextEncoder(device=dev, precision='fp32x3').forward(*args))
+    cls32, _, probs32 = _np(engine.TextEncoder(device=dev, precision='fp32').forward(*args))
+    sub = np.unique(np.r_[0, np.arange(0, B, max(1, B // 24)), B - 1])
+    rc, rl, rp = o_t.forward(syn.weights('text'), ids[sub], mask[sub])
+    err, agree = _report(f'text fp32x3 B={B}', probs[sub], rp, probs32[sub])
+    ferr = float(np.abs(cls[sub] - rc).max() / np.abs(rc).max())
+    print(f'  cls rel err {ferr:.3g} (fp32 path {float(np.abs(cls32[sub] - rc).max() / np.abs(rc).max()):.3g}), '
+          f'logits max|d| {np.abs(logits[sub] - rl).max():.3g}; fp32x3 vs fp32 probs {np.abs(probs - probs32).max():.3g}')
+    assert agree == len(sub) and err <= PROB_TOL and ferr <= FEAT_RTOL
+
+
+def test_text_fp32x3_batch_invariance(dev):
+    """Rows of a B=128 batch equal the same rows run as B=16, bit for bit (every split tile sums
+    each output in the same k order: pass 0, 1, 2, each in k order)."""
+    m = engine.TextEncoder(device=dev, precision='fp32x3')
+    ids, mask = syn.text_inputs(128, 128, seed=41, ragged=True)
+    args = (engine.to_device(ids, dev), engine.to_device(mask, dev))
+    big = [t[:16].cpu() for t in m.forward(*args)]
+    small = [t.cpu() for t in m.forward(*(a[:16] for a in args))]
+    for i, (a, b) in enumerate(zip(big, small)):
+        assert torch.equal(a, b), f'output {i}'
+
+
+@pytest.mark.parametrize('B', [5, 64])
+def test_resnet_fp32x3_vs_oracle(dev, B):
+    gray = syn.image_inputs(B, seed=600 + B)
+    g = engine.to_device(gray, dev)
+    feat, logits, probs = _np(engine.ImageEncoder(device=dev, precision='fp32x3').forward(g))
+    feat32, _, probs32 = _np(engine.ImageEncoder(device=dev, precision='fp32').forward(g))
+    sub = np.unique(np.r_[0, np.arange(0, B, max(1, B // 16)), B - 1])
+    rf, rl, rp = o_i.forward(syn.weights('image'), gray[sub])
+    err, agree = _report(f'resnet50 fp32x3 B={B}', probs[sub], rp, probs32[sub])
+    ferr = float(np.abs(feat[sub] - rf).max() / np.abs(rf).max())
+    print(f'  feat rel err {ferr:.3g} (fp32 path {float(np.abs(feat32[sub] - rf).max() / np.abs(rf).max()):.3g}), '
+          f'logits max|d| {np.abs(logits[sub] - rl).max():.3g}')
+    assert agree == len(sub) and err <= PROB_TOL and ferr <= FEAT_RTOL
+
+
+def test_resnet_fp32x3_rgb_and_224_gray_inputs(dev):
+    """The other u8 entry shapes (already-resized 224 gray, RGB) through the fp32x3 stem."""
+    from oracle import image as oi
+    enc = engine.ImageEncoder(device=dev, precision='fp32x3')
+    rgb = np.stack([syn.image_inputs(2, seed=70 + c).repeat(4, axis=1).repeat(4, axis=2)[:, :224, :224]
+                    for c in range(3)], -1)
+    rgb = np.ascontiguousarray(np.pad(rgb, ((0, 0), (0, 32), (0, 32), (0, 0)))[:, :224, :224])
+    _, _, probs = _np(enc.forward_u8(engine.to_device(rgb, dev)))
+    _, _, rp = oi.forward_resized(syn.weights('image'), rgb)
+    assert np.abs(probs - rp).max() <= PROB_TOL and (probs.argmax(1) == rp.argmax(1)).all()
+    g224 = np.ascontiguousarray(rgb[..., 0])
+    _, _, probs = _np(enc.forward_u8(engine.to_device(g224[..., None], dev)))
+    _, _, rp = oi.forward_resized(syn.weights('image'), g224)
+    assert np.abs(probs - rp).max() <= PROB_TOL
+
+
+def test_fused_fp32x3_b256_vs_oracle(dev):
+    """The whole fused step at the headline config (B=256) on the fp32x3 path against the oracle
+    chain o_f(o_s, o_t, o_i) on 32 rows spread over the batch (every row: bench.py's parity)."""
+    from oracle import fusion as o_f, speech as o_s
+    B = 256
+    x = syn.speech_inputs(B, seed=71)
+    ids, mask = syn.text_inputs(B, 128, seed=71, ragged=True)
+    gray = syn.image_inputs(B, seed=71)
+    pipe = engine.FusedPipeline(device=dev, precision='fp32x3')
+    args = [engine.to_device(a, dev) for a in (x, ids, mask, gray)]
+    pipe.forward(*args)
+    out = pipe.forward(*args)
+    pipe.check()
+    got = {k: _np(v) for k, v in out.items()}
+    sub = np.unique(np.r_[np.arange(0, B, 8), B - 1])
+    rs = o_s.forward(syn.weights('speech'), x[sub])
+    rt = o_t.forward(syn.weights('text'), ids[sub], mask[sub])
+    ri = o_i.forward(syn.weights('image'), gray[sub])
+    rf = o_f.forward(syn.weights('fusion'), rs[0], rt[0], ri[0], rs[2], rt[2], ri[2])
+    for name, g, r in (('text', got['text'][2][sub], rt[2]), ('image', got['image'][2][sub], ri[2]),
+                       ('fused', got['fusion'][1][sub], rf[1])):
+        err = float(np.abs(g - r).max())
+        print(f'fp32x3 fused step {name}: probs max|d| {err:.3g}')
+        assert err <= PROB_TOL and (g.argmax(1) == r.argmax(1)).all(), name
