@@ -120,6 +120,13 @@ int mec_fuse_weighted_f64(const double* s_probs, const double* t_probs, const do
 int mec_resize_u8(const uint8_t* in, int B, int H, int W, uint8_t* out, int OH, int OW, void* stream);
 /* C[M,N] = act(A[M,K] . B[N,K]^T + bias (+ R)); f16 operands, fp32 accumulate.
  * act: 0 none, 1 relu, 2 gelu(erf). Any of bias/R/C16/C32 may be NULL (not both outputs). */
+/* Split-f16 GEMM (the MEC_PREC_FP32X3 engine): A and B each an f16 hi plane with its lo plane
+ * a_lo / b_lo elements further on (x = hi + lo); C = act((A_lo.B_hi + A_hi.B_lo + A_hi.B_hi) *
+ * oscale + bias (+ R f32)); C16 (hi plane, lo plane at C16 + c_lo when c_lo != 0) and/or C32.
+ * act: 0 none, 1 relu, 4 exact-erf GELU. */
+int mec_gemm_f16x3(const void* A, long long a_lo, const void* B, long long b_lo, float oscale, const float* bias,
+                   const float* R, void* C16, long long c_lo, float* C32, int M, int N, int K, int act,
+                   void* stream);
 int mec_gemm_f16(const void* A, const void* B, const float* bias, const void* R, int r_is_f32, void* C16,
                  float* C32, int M, int N, int K, int act, void* stream);
 /* Implicit-GEMM conv on NHWC f16: x[n,H,W,C], w[Cout][ks][ks][C], y[n,OH,OW,Cout]. */

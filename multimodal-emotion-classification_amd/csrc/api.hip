@@ -246,6 +246,19 @@ int mec_gemm_f16(const void* A, const void* B, const float* bias, const void* R,
   })
 }
 
+int mec_gemm_f16x3(const void* A, long long a_lo, const void* B, long long b_lo, float oscale, const float* bias,
+                   const float* R, void* C16, long long c_lo, float* C32, int M, int N, int K, int act,
+                   void* stream) {
+  API_GUARD({
+    MEC_REQUIRE(a_lo != 0 && b_lo != 0, "mec_gemm_f16x3: a_lo / b_lo must locate the lo planes");
+    GemmParams g;
+    g.split = 1; g.A = A; g.a_lo = a_lo; g.B = reinterpret_cast<const f16*>(B); g.b_lo = b_lo; g.oscale = oscale;
+    g.bias = bias; g.R = R; g.r_f32 = R != nullptr; g.C16 = reinterpret_cast<f16*>(C16); g.c_lo = C16 ? c_lo : 0;
+    g.C32 = C32; g.M = M; g.N = N; g.K = K; g.act = act;
+    return launch_gemm(g, S(stream), nullptr, TAG_NONE);
+  })
+}
+
 int mec_conv_f16(const void* x, const void* w, const float* bias, const void* R, void* y, int n, int H, int W,
                  int C, int Cout, int ks, int stride, int pad, int act, void* stream) {
   API_GUARD({

@@ -37,6 +37,8 @@ SIGNATURES = {
     'mec_fuse_weighted_f64': (c_int, [c_vp, c_vp, c_vp, c_int, c_vp, c_vp]),
     'mec_resize_u8': (c_int, [c_vp, c_int, c_int, c_int, c_vp, c_int, c_int, c_vp]),
     'mec_gemm_f16': (c_int, [c_vp, c_vp, c_vp, c_vp, c_int, c_vp, c_vp, c_int, c_int, c_int, c_int, c_vp]),
+    'mec_gemm_f16x3': (c_int, [c_vp, ctypes.c_longlong, c_vp, ctypes.c_longlong, ctypes.c_float, c_vp, c_vp, c_vp,
+                               ctypes.c_longlong, c_vp, c_int, c_int, c_int, c_int, c_vp]),
     'mec_conv_f16': (c_int, [c_vp, c_vp, c_vp, c_vp, c_vp, c_int, c_int, c_int, c_int, c_int, c_int, c_int,
                              c_int, c_int, c_vp]),
     'mec_gemm_f32': (c_int, [c_vp, c_vp, c_vp, c_vp, c_vp, c_int, c_int, c_int, c_int, c_vp]),

@@ -112,3 +112,64 @@ def test_fused_fp32x3_b256_vs_oracle(dev):
         err = float(np.abs(g - r).max())
         print(f'fp32x3 fused step {name}: probs max|d| {err:.3g}')
         assert err <= PROB_TOL and (g.argmax(1) == r.argmax(1)).all(), name
+
+
+def _split(a, scale=1.0):
+    x = (np.asarray(a, np.float32) * np.float32(scale)).astype(np.float32)
+    hi = x.astype(np.float16)
+    lo = (x - hi.astype(np.float32)).astype(np.float16)
+    return np.concatenate([hi.ravel(), lo.ravel()]).reshape((2,) + x.shape)
+
+
+SPLIT_TILES = [64, 128, 256, 1128, 1064, 10064, 10128, 10256, 11128, 11064, 20256, 30256, 20128, 50128, 60128, 50256,
+               40256, 41256]
+
+
+@pytest.mark.parametrize('M,N,K,act', [(512, 256, 768, 0), (1000, 768, 3072, 4), (300, 512, 128, 1)])
+def test_split_gemm_vs_fp64_and_every_tile_bit_identical(dev, M, N, K, act):
+    """mec_gemm_f16x3 (the fp32x3 engine) against float64 A . B^T of the fp32 operands: within the
+    fp32 GEMM engine's bar (2e-6 x sum |a b|, tests/test_gpu_fp32.py), with the weights pre-scaled
+    by 2^8 and undone by oscale; and every tile computes the same bits (each output's passes and
+    k chain are tile-independent)."""
+    import ctypes
+    from mec import _lib
+    lib = _lib.load()
+    rng = np.random.default_rng(M + N + K)
+    A = rng.standard_normal((M, K)).astype(np.float32)
+    Bw = (rng.standard_normal((N, K)) * 0.03).astype(np.float32)
+    bias = rng.standard_normal(N).astype(np.float32)
+    R = rng.standard_normal((M, N)).astype(np.float32) if act == 0 else None
+    Ad = torch.from_numpy(_split(A)).to(dev)
+    Bd = torch.from_numpy(_split(Bw, 256.0)).to(dev)
+    bd = torch.from_numpy(bias).to(dev)
+    Rd = torch.from_numpy(R).to(dev) if R is not None else None
+    p = lambda t: ctypes.c_void_p(t.data_ptr()) if t is not None else ctypes.c_void_p(0)  # noqa: E731
+    ref = A.astype(np.float64) @ Bw.astype(np.float64).T + bias
+    if R is not None:
+        ref = ref + R
+    if act == 1:
+        ref = np.maximum(ref, 0)
+    elif act == 4:
+        from scipy.special import erf
+        ref = 0.5 * ref * (1 + erf(ref / np.sqrt(2)))
+    bound = 2e-6 * (np.abs(A).astype(np.float64) @ np.abs(Bw).astype(np.float64).T + np.abs(bias) + 1)
+    outs = {}
+    for tile in [0] + SPLIT_TILES:
+        if N % (256 if tile >= 40000 else (tile % 10000 if tile % 10000 < 1000 else tile % 10000 - 1000)):
+            continue
+        _lib.check(lib.mec_set_option(b'gemm_bn', tile), 'gemm_bn')
+        C = torch.empty((M, N), device=dev)
+        try:
+            _lib.check(lib.mec_gemm_f16x3(p(Ad), M * K, p(Bd), N * K, ctypes.c_float(1 / 256), p(bd), p(Rd), None, 0,
+                                          p(C), M, N, K, act, ctypes.c_void_p(torch.cuda.current_stream(dev).cuda_stream)),
+                       f'split gemm tile {tile}')
+        finally:
+            lib.mec_set_option(b'gemm_bn', 0)
+        outs[tile] = C.cpu().numpy()
+    got = outs[0]
+    err = np.abs(got - ref)
+    print(f'split GEMM {M}x{N}x{K} act {act}: max err {err.max():.3g}, max err / bound {(err / bound).max():.3g}, '
+          f'tiles {len(outs) - 1}')
+    assert (err <= bound).all()
+    for tile, o in outs.items():
+        assert np.array_equal(o, got), f'tile {tile} differs from the autotuned tile'

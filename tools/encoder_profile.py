@@ -26,7 +26,7 @@ def main():
     ap.add_argument('--iters', type=int, default=5)
     ap.add_argument('--batch', type=int, default=256)
     ap.add_argument('--opt', action='append', default=[], help='library option NAME=VALUE (mec_set_option)')
-    ap.add_argument('--precision', default='f16', choices=['f16', 'fp32'])
+    ap.add_argument('--precision', default='f16', choices=['f16', 'fp32', 'fp32x3'])
     a = ap.parse_args()
     dev = torch.device('cuda', 0)
     B = a.batch
