@@ -343,7 +343,9 @@ __device__ __forceinline__ void pp_epilogue(const GemmParams& p, floatx4 (&acc)[
     }
   };
   const float os = p.oscale;  // 1 except on split operands: fma(acc, 1, b) == acc + b
-  if (!p.R && p.C16 && !p.C32 && !p.c_lo) {
+  if (!p.R && p.C16 && !p.C32) {
+    // bias + act in registers, written back into acc; then one staged pass per f16 plane (the lo
+    // plane f16(v - hi) only on split outputs, c_lo != 0), through the wave's own LDS region
 #pragma unroll
     for (int ia = 0; ia < NIA; ++ia)
 #pragma unroll
@@ -353,19 +355,34 @@ __device__ __forceinline__ void pp_epilogue(const GemmParams& p, floatx4 (&acc)[
 #pragma unroll
         for (int e = 0; e < 4; ++e) v[e] += 0.f;  // gemm_epilogue's "+ residual" with none: -0 -> +0
         act4(v);
-        half4 h;
 #pragma unroll
-        for (int e = 0; e < 4; ++e) h[e] = (f16)v[e];
-        const int r = ia * 16 + l16, x = jb * 2 + (q >> 1);
-        *reinterpret_cast<half4*>(reg + r * 128 + ((x ^ ((r >> 1) & 7)) << 4) + (q & 1) * 8) = h;
+        for (int e = 0; e < 4; ++e) acc[ia][jb][e] = v[e];
       }
-    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+    const int planes = p.c_lo ? 2 : 1;
+    for (int pl = 0; pl < planes; ++pl) {
+      if (pl) asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");  // plane 0's staging reads are done
 #pragma unroll
-    for (int it = 0; it < HB / 8; ++it) {
-      const int r = it * 8 + (lane >> 3), x = lane & 7;
-      const uint4 v = *reinterpret_cast<const uint4*>(reg + r * 128 + ((x ^ ((r >> 1) & 7)) << 4));
-      if (rw0 + r < M && (!NOSTORE || v.x == 0x12345678u))
-        *reinterpret_cast<uint4*>(p.C16 + (size_t)(rw0 + r) * N + cw0 + x * 8) = v;
+      for (int ia = 0; ia < NIA; ++ia)
+#pragma unroll
+        for (int jb = 0; jb < 4; ++jb) {
+          half4 h;
+#pragma unroll
+          for (int e = 0; e < 4; ++e) {
+            const f16 hi = (f16)acc[ia][jb][e];
+            h[e] = pl ? (f16)(acc[ia][jb][e] - (float)hi) : hi;
+          }
+          const int r = ia * 16 + l16, x = jb * 2 + (q >> 1);
+          *reinterpret_cast<half4*>(reg + r * 128 + ((x ^ ((r >> 1) & 7)) << 4) + (q & 1) * 8) = h;
+        }
+      asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+      f16* C = p.C16 + (pl ? p.c_lo : 0);
+#pragma unroll
+      for (int it = 0; it < HB / 8; ++it) {
+        const int r = it * 8 + (lane >> 3), x = lane & 7;
+        const uint4 v = *reinterpret_cast<const uint4*>(reg + r * 128 + ((x ^ ((r >> 1) & 7)) << 4));
+        if (rw0 + r < M && (!NOSTORE || v.x == 0x12345678u))
+          *reinterpret_cast<uint4*>(C + (size_t)(rw0 + r) * N + cw0 + x * 8) = v;
+      }
     }
     return;
   }

@@ -155,7 +155,8 @@ def test_split_gemm_vs_fp64_and_every_tile_bit_identical(dev, M, N, K, act):
     bound = 2e-6 * (np.abs(A).astype(np.float64) @ np.abs(Bw).astype(np.float64).T + np.abs(bias) + 1)
     outs = {}
     for tile in [0] + SPLIT_TILES:
-        if N % (256 if tile >= 40000 else (tile % 10000 if tile % 10000 < 1000 else tile % 10000 - 1000)):
+        width = 256 if tile >= 40000 else (tile % 10000 if tile % 10000 < 1000 else tile % 10000 - 1000)
+        if tile and N % width:
             continue
         _lib.check(lib.mec_set_option(b'gemm_bn', tile), 'gemm_bn')
         C = torch.empty((M, N), device=dev)
@@ -173,3 +174,67 @@ def test_split_gemm_vs_fp64_and_every_tile_bit_identical(dev, M, N, K, act):
     assert (err <= bound).all()
     for tile, o in outs.items():
         assert np.array_equal(o, got), f'tile {tile} differs from the autotuned tile'
+
+
+@pytest.mark.parametrize('M,N,K', [(4096, 768, 768), (4096, 768, 3072), (2048, 512, 4608)])
+def test_split_gemm_error_vs_exact_fp32_gemm(dev, M, N, K):
+    """Against float64 on the same fp32 operands (BERT-like scales: activations O(1), weights
+    ~0.02-0.05), the split-f16 engine's error is of the exact-fp32 MFMA engine's size (the
+    split's 2^-22 operand rounding sits below the fp32 accumulation error): max and RMS error of
+    both printed; the split's max error may exceed the exact engine's by at most 50%."""
+    import ctypes
+    from mec import _lib
+    lib = _lib.load()
+    rng = np.random.default_rng(K)
+    A = rng.standard_normal((M, K)).astype(np.float32)
+    W = (rng.standard_normal((N, K)) * (0.02 if K < 4000 else 0.05)).astype(np.float32)
+    ref = A.astype(np.float64) @ W.astype(np.float64).T
+    st = ctypes.c_void_p(torch.cuda.current_stream(dev).cuda_stream)
+    p = lambda t: ctypes.c_void_p(t.data_ptr())  # noqa: E731
+    C32 = torch.empty((M, N), device=dev)
+    _lib.check(lib.mec_gemm_f32(p(torch.from_numpy(A).to(dev)), p(torch.from_numpy(W).to(dev)), None, None, p(C32),
+                                M, N, K, 0, st), 'mec_gemm_f32')
+    e = float(np.ceil(np.log2(16384 / np.abs(W).max())) - 1)
+    Cx = torch.empty((M, N), device=dev)
+    _lib.check(lib.mec_gemm_f16x3(p(torch.from_numpy(_split(A)).to(dev)), M * K,
+                                  p(torch.from_numpy(_split(W, 2.0 ** e)).to(dev)), N * K, ctypes.c_float(2.0 ** -e),
+                                  None, None, None, 0, p(Cx), M, N, K, 0, st), 'mec_gemm_f16x3')
+    e32 = np.abs(C32.cpu().numpy() - ref)
+    ex3 = np.abs(Cx.cpu().numpy() - ref)
+    print(f'{M}x{N}x{K}: exact-fp32 engine max {e32.max():.3g} rms {np.sqrt((e32 ** 2).mean()):.3g}; '
+          f'split-f16 engine max {ex3.max():.3g} rms {np.sqrt((ex3 ** 2).mean()):.3g}')
+    assert ex3.max() <= 1.5 * e32.max()
+
+
+@pytest.mark.parametrize('tile', [0, 40256, 10256, 11128])
+def test_split_gemm_plane_output(dev, tile):
+    """C16 written as hi / lo planes (c_lo): hi = f16(v), lo = f16(v - hi), for v the fp32 result
+    the same launch writes to C32 on another call; on the ping-pong tile this is its staged
+    f16 fast-path epilogue run once per plane."""
+    import ctypes
+    from mec import _lib
+    lib = _lib.load()
+    M, N, K = 700, 512, 768
+    rng = np.random.default_rng(7)
+    A = rng.standard_normal((M, K)).astype(np.float32)
+    Bw = (rng.standard_normal((N, K)) * 0.03).astype(np.float32)
+    bias = rng.standard_normal(N).astype(np.float32)
+    Ad = torch.from_numpy(_split(A)).to(dev)
+    Bd = torch.from_numpy(_split(Bw, 256.0)).to(dev)
+    bd = torch.from_numpy(bias).to(dev)
+    st = ctypes.c_void_p(torch.cuda.current_stream(dev).cuda_stream)
+    p = lambda t: ctypes.c_void_p(t.data_ptr())  # noqa: E731
+    C32 = torch.empty((M, N), device=dev)
+    C16 = torch.empty((2, M, N), device=dev, dtype=torch.float16)
+    _lib.check(lib.mec_set_option(b'gemm_bn', tile), 'gemm_bn')
+    try:
+        _lib.check(lib.mec_gemm_f16x3(p(Ad), M * K, p(Bd), N * K, ctypes.c_float(1 / 256), p(bd), None, None, 0, p(C32),
+                                      M, N, K, 4, st), 'f32 out')
+        _lib.check(lib.mec_gemm_f16x3(p(Ad), M * K, p(Bd), N * K, ctypes.c_float(1 / 256), p(bd), None, p(C16), M * N,
+                                      None, M, N, K, 4, st), 'plane out')
+    finally:
+        lib.mec_set_option(b'gemm_bn', 0)
+    v = C32.cpu().numpy()
+    hi, lo = C16[0].cpu().numpy(), C16[1].cpu().numpy()
+    assert np.array_equal(hi, v.astype(np.float16))
+    assert np.array_equal(lo, (v - hi.astype(np.float32)).astype(np.float16))
