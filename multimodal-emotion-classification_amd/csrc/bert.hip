@@ -321,6 +321,158 @@ __global__ __launch_bounds__(256) void bert_attention_kernel(const f16* __restri
   attn_head(sQ, sK, sV, sBias, wave, lane, ctx + (size_t)b * ATT_L * BH + h * BDH);
 }
 
+// ----------------------------------------------------------------------------- fp32x3 attention
+// The fp32 attention of one (sequence, head) on split-f16 operands (the MEC_PREC_FP32X3 path):
+// Q, K, V arrive as f16 hi / lo planes (qkv, qkv + lo; the split QKV GEMM's output) and every
+// product is hi.hi + hi.lo + lo.hi into an fp32 accumulator, as in the split GEMM:
+//   S^T = K Q^T      3 v_mfma_f32_32x32x16_f16 per 16-deep k step (K_lo Q_hi, K_hi Q_lo, K_hi Q_hi)
+//   P   = softmax(S / 8 + mask_bias) in fp32 with libm expf (the fp32 path's arithmetic)
+//   O^T = V^T P^T    P (x 2^12, exact, so its small entries stay out of the f16 subnormals) split
+//                    into hi / lo in registers, 3 MFMAs per step; O scaled back by 2^-12
+// Layout and lane roles are attn_head's (keys in registers, one cross-half shuffle per row,
+// transposed V reads); the output is staged per wave and written as hi / lo planes
+// (ctx, ctx + clo) for the split O-projection. 96 KB of LDS: one workgroup per CU.
+__global__ __launch_bounds__(256) void bert_attention_x3_kernel(const f16* __restrict__ qkv, long long lo,
+                                                                const int32_t* __restrict__ mask,
+                                                                f16* __restrict__ ctx, long long clo) {
+  __shared__ __attribute__((aligned(16))) f16 sQ[2][ATT_L * BDH];
+  __shared__ __attribute__((aligned(16))) f16 sK[2][ATT_L * BDH];
+  __shared__ __attribute__((aligned(16))) f16 sV[2][ATT_L * BDH];
+  __shared__ float sBias[ATT_L];
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int b = blockIdx.x / BHEADS, h = blockIdx.x - (blockIdx.x / BHEADS) * BHEADS;
+#pragma unroll
+  for (int pl = 0; pl < 2; ++pl) {
+    const f16* base = qkv + (pl ? lo : 0) + (size_t)b * ATT_L * (3 * BH) + h * BDH;
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+      const int c = tid + 256 * i;
+      const int row = c >> 3, kc = c & 7;
+      const f16* src = base + (size_t)row * (3 * BH) + kc * 8;
+      const uint4 q = *reinterpret_cast<const uint4*>(src);
+      const uint4 k = *reinterpret_cast<const uint4*>(src + BH);
+      const uint4 v = *reinterpret_cast<const uint4*>(src + 2 * BH);
+      *reinterpret_cast<uint4*>(sQ[pl] + row * BDH + aswz(row, kc) * 8) = q;
+      *reinterpret_cast<uint4*>(sK[pl] + row * BDH + aswz(row, kc) * 8) = k;
+      *reinterpret_cast<uint4*>(sV[pl] + row * BDH + vswz(row, kc) * 8) = v;
+    }
+  }
+  if (tid < ATT_L) sBias[tid] = mask[(size_t)b * ATT_L + tid] ? 0.f : -3.4028234663852886e38f;  // finfo(f32).min
+  __syncthreads();
+  const int lr = lane & 31, lh = lane >> 5;
+  floatx16 s[4];
+#pragma unroll
+  for (int t = 0; t < 4; ++t) {
+#pragma unroll
+    for (int e = 0; e < 16; ++e) s[t][e] = 0.f;
+#pragma unroll
+    for (int kk = 0; kk < 4; ++kk) {
+      const int kc = 2 * kk + lh;
+      const int rk = 32 * t + lr, rq = 32 * wave + lr;
+      const half8 ah = *reinterpret_cast<const half8*>(sK[0] + rk * BDH + aswz(rk, kc) * 8);
+      const half8 al = *reinterpret_cast<const half8*>(sK[1] + rk * BDH + aswz(rk, kc) * 8);
+      const half8 bh = *reinterpret_cast<const half8*>(sQ[0] + rq * BDH + aswz(rq, kc) * 8);
+      const half8 bl = *reinterpret_cast<const half8*>(sQ[1] + rq * BDH + aswz(rq, kc) * 8);
+      s[t] = __builtin_amdgcn_mfma_f32_32x32x16_f16(al, bh, s[t], 0, 0, 0);
+      s[t] = __builtin_amdgcn_mfma_f32_32x32x16_f16(ah, bl, s[t], 0, 0, 0);
+      s[t] = __builtin_amdgcn_mfma_f32_32x32x16_f16(ah, bh, s[t], 0, 0, 0);
+    }
+  }
+  float mx = -INFINITY;
+#pragma unroll
+  for (int t = 0; t < 4; ++t)
+#pragma unroll
+    for (int e = 0; e < 16; ++e) {
+      const int key = 32 * t + (e & 3) + 8 * (e >> 2) + 4 * lh;
+      const float v = s[t][e] * 0.125f + sBias[key];
+      s[t][e] = v;
+      mx = fmaxf(mx, v);
+    }
+  mx = fmaxf(mx, __shfl_xor(mx, 32, 64));
+  float sum = 0.f;
+#pragma unroll
+  for (int t = 0; t < 4; ++t)
+#pragma unroll
+    for (int e = 0; e < 16; ++e) {
+      const float p = expf(s[t][e] - mx);
+      s[t][e] = p;
+      sum += p;
+    }
+  sum += __shfl_xor(sum, 32, 64);
+  const float inv = 1.0f / sum;
+
+  floatx16 o[2];
+#pragma unroll
+  for (int u = 0; u < 2; ++u)
+#pragma unroll
+    for (int e = 0; e < 16; ++e) o[u][e] = 0.f;
+  const int tq = (lane >> 2) & 3, tp = lane & 3, tg = (lane >> 4) & 1;
+#pragma unroll
+  for (int st = 0; st < 8; ++st) {
+    const int t = st >> 1, sp = st & 1;
+    half8 ph, pl8;
+#pragma unroll
+    for (int j = 0; j < 8; ++j) {
+      const float pv = (s[t][8 * sp + j] * inv) * 4096.f;
+      ph[j] = (f16)pv;
+      pl8[j] = (f16)(pv - (float)ph[j]);
+    }
+    const int kq = 32 * t + 16 * sp + 4 * lh + tq;
+#pragma unroll
+    for (int u = 0; u < 2; ++u) {
+      const int dc = 32 * u + 16 * tg + 4 * tp;
+      half8 vh, vl;
+      {
+        const half4 a = lds_tr16(sV[0] + kq * BDH + vswz(kq, dc >> 3) * 8 + (dc & 7));
+        const half4 c = lds_tr16(sV[0] + (kq + 8) * BDH + vswz(kq + 8, dc >> 3) * 8 + (dc & 7));
+        vh = half8{a[0], a[1], a[2], a[3], c[0], c[1], c[2], c[3]};
+      }
+      {
+        const half4 a = lds_tr16(sV[1] + kq * BDH + vswz(kq, dc >> 3) * 8 + (dc & 7));
+        const half4 c = lds_tr16(sV[1] + (kq + 8) * BDH + vswz(kq + 8, dc >> 3) * 8 + (dc & 7));
+        vl = half8{a[0], a[1], a[2], a[3], c[0], c[1], c[2], c[3]};
+      }
+      o[u] = __builtin_amdgcn_mfma_f32_32x32x16_f16(vl, ph, o[u], 0, 0, 0);
+      o[u] = __builtin_amdgcn_mfma_f32_32x32x16_f16(vh, pl8, o[u], 0, 0, 0);
+      o[u] = __builtin_amdgcn_mfma_f32_32x32x16_f16(vh, ph, o[u], 0, 0, 0);
+    }
+  }
+  // O = o 2^-12 -> hi / lo planes, staged through this wave's own rows of sQ[0] / sQ[1]
+  const int rq = 32 * wave + lr;
+#pragma unroll
+  for (int u = 0; u < 2; ++u)
+#pragma unroll
+    for (int gq = 0; gq < 4; ++gq) {
+      half4 hv, lv;
+#pragma unroll
+      for (int e = 0; e < 4; ++e) {
+        const float x = o[u][4 * gq + e] * (1.0f / 4096.f);
+        hv[e] = (f16)x;
+        lv[e] = (f16)(x - (float)hv[e]);
+      }
+      const int d = 32 * u + 8 * gq + 4 * lh;
+      *reinterpret_cast<half4*>(sQ[0] + rq * BDH + aswz(rq, d >> 3) * 8 + (d & 7)) = hv;
+      *reinterpret_cast<half4*>(sQ[1] + rq * BDH + aswz(rq, d >> 3) * 8 + (d & 7)) = lv;
+    }
+  asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");  // wave-local rows: no barrier needed
+  f16* out = ctx + (size_t)b * ATT_L * BH + h * BDH;
+#pragma unroll
+  for (int pl = 0; pl < 2; ++pl)
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+      const int c = 64 * i + lane, r = 32 * wave + (c >> 3), kc = c & 7;
+      const uint4 v = *reinterpret_cast<const uint4*>(sQ[pl] + r * BDH + aswz(r, kc) * 8);
+      *reinterpret_cast<uint4*>(out + (pl ? clo : 0) + (size_t)r * BH + kc * 8) = v;
+    }
+}
+
+int launch_bert_attention_x3(const f16* qkv, long long lo, const int32_t* mask, f16* ctx, long long clo, int B,
+                             hipStream_t s) {
+  hipLaunchKernelGGL(bert_attention_x3_kernel, dim3(B * BHEADS), dim3(256), 0, s, qkv, lo, mask, ctx, clo);
+  MEC_LAUNCH_CHECK();
+  return 0;
+}
+
 // ----------------------------------------------------------------------------- QKV + attention
 // The QKV projection and the attention of one (sequence, head pair) in one workgroup, so Q,
 // K and V never go through HBM (unfused: a 151-MB write by the QKV GEMM and the same read by

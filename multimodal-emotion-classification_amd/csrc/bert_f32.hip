@@ -195,8 +195,9 @@ int TextModel::forward_f32(const int32_t* ids, const int32_t* mask, int B, int L
 
 // fp32x3 path: the fp32 path's structure with every GEMM on split-f16 operands (gemm_glds.hip
 // split mode, three f16 MFMA passes into one fp32 accumulator). Per layer (M = B*L rows):
-//   qkv32       = [h_hi|h_lo] . [Wqkv_hi|Wqkv_lo]^T 2^-e + b        split GEMM, f32 out
-//   ctx hi/lo   = softmax(QK^T/8 + mask_bias) V                     bert_attention_f32_kernel<1>
+//   qkv hi/lo   = [h_hi|h_lo] . [Wqkv_hi|Wqkv_lo]^T 2^-e + b        split GEMM, split out
+//   ctx hi/lo   = softmax(QK^T/8 + mask_bias) V                     bert_attention_x3_kernel (split
+//                                                                    MFMA products, fp32 softmax)
 //   t32         = ctx . Wo^T 2^-e + bo + h32                        split GEMM, f32 residual
 //   h32, h hi/lo = LN(t32)                                          bert_layernorm_kernel (lo plane)
 //   i hi/lo     = GELU(h . Wi^T 2^-e + bi)                          split GEMM, exact erf, split out
@@ -207,8 +208,8 @@ int TextModel::forward_x3(const int32_t* ids, const int32_t* mask, int B, int L,
   MEC_REQUIRE(wts.p && x3_lo && x3_scale.size() == 4 * NL, "text: fp32x3 weights missing");
   const int M = B * L;
   const long long MH = (long long)M * H, MF = (long long)M * FF;
-  // workspace: h32 | t32 (f32 [M,768]) ; h hi|lo, ctx hi|lo (f16 2x[M,768]) ; big: qkv32 f32 [M,2304]
-  // aliased with the FFN intermediate hi|lo (f16 2x[M,3072]) ; pooled [B,768]
+  // workspace: h32 | t32 (f32 [M,768]) ; h hi|lo, ctx hi|lo (f16 2x[M,768]) ; big: qkv hi|lo
+  // (f16 2x[M,2304]), then the FFN intermediate hi|lo (f16 2x[M,3072]) ; pooled [B,768]
   const size_t need = (size_t)MH * 4 * 2 + (size_t)MH * 2 * 4 + (size_t)MF * 4 + (size_t)B * H * 4;
   if (ws.bytes < need) MEC_TRY(ws.ensure(need));
   char* p = ws.as<char>();
@@ -235,11 +236,10 @@ int TextModel::forward_x3(const int32_t* ids, const int32_t* mask, int B, int L,
                 *g2 = pl + 8448, *b2 = pl + 9216;
     GemmParams g;
     g.split = 1; g.A = hs; g.a_lo = MH; g.B = wqkv; g.b_lo = wlo; g.oscale = sc[0];
-    g.bias = bqkv; g.C32 = big32; g.M = M; g.N = 2304; g.K = H;
+    g.bias = bqkv; g.C16 = bigs; g.c_lo = (long long)M * 2304; g.M = M; g.N = 2304; g.K = H;
     MEC_TRY(launch_gemm(g, s, &prof, TAG_BERT_QKV));
     MEC_TRY(prof.begin(TAG_BERT_ATTN, s));
-    hipLaunchKernelGGL(bert_attention_f32_kernel<1>, dim3(B * NH), dim3(256), 0, s, big32, mask, nullptr, cs, MH);
-    MEC_LAUNCH_CHECK();
+    MEC_TRY(launch_bert_attention_x3(bigs, (long long)M * 2304, mask, cs, MH, B, s));
     MEC_TRY(prof.end(TAG_BERT_ATTN, s));
     g = GemmParams();
     g.split = 1; g.A = cs; g.a_lo = MH; g.B = wo; g.b_lo = wlo; g.oscale = sc[1];

@@ -36,7 +36,6 @@ int launch_gemm(const GemmParams& p, hipStream_t s, Prof* prof, int tag) {
   }
   if (prof) MEC_TRY(prof->begin(tag, s));
   int rc;
-  MEC_REQUIRE(!p.split || p.amode == A_PLAIN || p.amode == A_CONV, "gemm: split operands take a plain or conv A");
   if (p.split)  // split-f16 operands: the glds engine only (the halo conv kernels read one plane), autotuned
     rc = launch_gemm_glds(p, s, opt().gemm_bn);
   else if (opt().conv3x3_direct && !opt().gemm_bn && p.amode == A_CONV && p.ks == 3 && p.stride == 1 && p.pad == 1 && p.H == 56 &&

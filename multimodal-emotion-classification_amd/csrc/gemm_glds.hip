@@ -40,7 +40,7 @@ __global__ __launch_bounds__(64 * WM * WN, (WM * WN == 4) ? 2 : 1) void gemm_gld
   // SP: split-f16 operands (GemmParams::split): the K loop runs over 3 K passes, pass 0 reading
   // the A lo plane, pass 1 the B lo plane, pass 2 both hi planes
   static_assert(BK == 64 || BK == 32, "BK");
-  static_assert(SP == 0 || (AM != A_DUAL && PRE == 0), "split operands: plain or conv A, no prefetch");
+  static_assert(SP == 0 || PRE == 0, "split operands: no residual prefetch");
   constexpr int CH = BK / 8;                   // 16-B chunks per LDS row
   constexpr int RPI = 64 / CH;                 // rows per glds wave-instruction (1 KB)
   constexpr int NW = WM * WN;
@@ -139,8 +139,8 @@ __global__ __launch_bounds__(64 * WM * WN, (WM * WN == 4) ? 2 : 1) void gemm_gld
     } else if constexpr (AM == A_DUAL) {
       const bool first = k0 < p.K1;
 #pragma unroll
-      for (int i = 0; i < AI; ++i) {
-        const f16* src = !a_ok[i] ? zero : (first ? a_src[i] + k0 : a2_src[i] + (k0 - p.K1));
+      for (int i = 0; i < AI; ++i) {  // split: both sources' lo planes at the same offset a_lo
+        const f16* src = !a_ok[i] ? zero : (first ? a_src[i] + aoff + k0 : a2_src[i] + aoff + (k0 - p.K1));
         __builtin_amdgcn_global_load_lds((const void*)src, (lds_vptr)(sA + (wave * AI + i) * RPI * BK), 16, 0, 0);
       }
     } else {
@@ -343,9 +343,7 @@ __device__ __forceinline__ void pp_epilogue(const GemmParams& p, floatx4 (&acc)[
     }
   };
   const float os = p.oscale;  // 1 except on split operands: fma(acc, 1, b) == acc + b
-  if (!p.R && p.C16 && !p.C32) {
-    // bias + act in registers, written back into acc; then one staged pass per f16 plane (the lo
-    // plane f16(v - hi) only on split outputs, c_lo != 0), through the wave's own LDS region
+  if (!p.R && p.C16 && !p.C32 && !p.c_lo) {
 #pragma unroll
     for (int ia = 0; ia < NIA; ++ia)
 #pragma unroll
@@ -355,34 +353,19 @@ __device__ __forceinline__ void pp_epilogue(const GemmParams& p, floatx4 (&acc)[
 #pragma unroll
         for (int e = 0; e < 4; ++e) v[e] += 0.f;  // gemm_epilogue's "+ residual" with none: -0 -> +0
         act4(v);
+        half4 h;
 #pragma unroll
-        for (int e = 0; e < 4; ++e) acc[ia][jb][e] = v[e];
+        for (int e = 0; e < 4; ++e) h[e] = (f16)v[e];
+        const int r = ia * 16 + l16, x = jb * 2 + (q >> 1);
+        *reinterpret_cast<half4*>(reg + r * 128 + ((x ^ ((r >> 1) & 7)) << 4) + (q & 1) * 8) = h;
       }
-    const int planes = p.c_lo ? 2 : 1;
-    for (int pl = 0; pl < planes; ++pl) {
-      if (pl) asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");  // plane 0's staging reads are done
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
 #pragma unroll
-      for (int ia = 0; ia < NIA; ++ia)
-#pragma unroll
-        for (int jb = 0; jb < 4; ++jb) {
-          half4 h;
-#pragma unroll
-          for (int e = 0; e < 4; ++e) {
-            const f16 hi = (f16)acc[ia][jb][e];
-            h[e] = pl ? (f16)(acc[ia][jb][e] - (float)hi) : hi;
-          }
-          const int r = ia * 16 + l16, x = jb * 2 + (q >> 1);
-          *reinterpret_cast<half4*>(reg + r * 128 + ((x ^ ((r >> 1) & 7)) << 4) + (q & 1) * 8) = h;
-        }
-      asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
-      f16* C = p.C16 + (pl ? p.c_lo : 0);
-#pragma unroll
-      for (int it = 0; it < HB / 8; ++it) {
-        const int r = it * 8 + (lane >> 3), x = lane & 7;
-        const uint4 v = *reinterpret_cast<const uint4*>(reg + r * 128 + ((x ^ ((r >> 1) & 7)) << 4));
-        if (rw0 + r < M && (!NOSTORE || v.x == 0x12345678u))
-          *reinterpret_cast<uint4*>(C + (size_t)(rw0 + r) * N + cw0 + x * 8) = v;
-      }
+    for (int it = 0; it < HB / 8; ++it) {
+      const int r = it * 8 + (lane >> 3), x = lane & 7;
+      const uint4 v = *reinterpret_cast<const uint4*>(reg + r * 128 + ((x ^ ((r >> 1) & 7)) << 4));
+      if (rw0 + r < M && (!NOSTORE || v.x == 0x12345678u))
+        *reinterpret_cast<uint4*>(p.C16 + (size_t)(rw0 + r) * N + cw0 + x * 8) = v;
     }
     return;
   }
@@ -701,10 +684,8 @@ static int launch_cfg_act(const GemmParams& p, hipStream_t s, int nwg, dim3 blk)
       hipLaunchKernelGGL((gemm_glds_kernel<BM, BN, WM, WN, NS, A_PLAIN, 0, MF, BK, 0, -1, 1>), dim3(nwg), blk, 0, s, p);
     else if (p.amode == A_CONV)
       hipLaunchKernelGGL((gemm_glds_kernel<BM, BN, WM, WN, NS, A_CONV, 0, MF, BK, 0, -1, 1>), dim3(nwg), blk, 0, s, p);
-    else {
-      set_error("gemm_glds: split operands take a plain or conv A");
-      return -1;
-    }
+    else
+      hipLaunchKernelGGL((gemm_glds_kernel<BM, BN, WM, WN, NS, A_DUAL, 0, MF, BK, 0, -1, 1>), dim3(nwg), blk, 0, s, p);
   } else if (BM * BN <= 128 * 128 && opt().gemm_prefetch_r && p.amode == A_PLAIN && p.R && !p.r_f32 && p.K <= 512) {
     // f16 residual prefetch for ResNet's short-K conv3 GEMMs (small tiles only: no spills);
     // 225 -> 170 us on layer1's conv3. The f32 form (PRE = 2, BERT's O-projection, K = 768)

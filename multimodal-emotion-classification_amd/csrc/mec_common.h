@@ -217,7 +217,7 @@ struct GemmParams {
   int group_m = 0;  // ping-pong tile order inside an XCD's range: 0 row-major, G = G-row groups
   // Split-f16 operands (the MEC_PREC_FP32X3 path, f16 engine only): A and B are each an f16
   // hi plane and an f16 lo plane (x = hi + lo exactly, |lo| <= 2^-11 |hi|), the lo planes at
-  // element offsets a_lo / b_lo from A / B. The K loop makes three passes over K, A_lo.B_hi,
+  // element offsets a_lo / b_lo from A / B (A_DUAL: from A and from A2 alike). The K loop makes three passes over K, A_lo.B_hi,
   // A_hi.B_lo, A_hi.B_hi, into one fp32 accumulator (the dropped A_lo.B_lo term is below
   // 2^-22 |A B|). oscale (a power of two: undoes the weights' pre-scale, exact) multiplies the
   // accumulator before the bias; it is 1 (an exact no-op) everywhere else.

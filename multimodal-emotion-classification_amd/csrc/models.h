@@ -102,6 +102,10 @@ int launch_bert_embed_ln(const int32_t* ids, int M, int L, const float* emb, flo
                          long long lo = 0);
 int launch_bert_layernorm(const float* x, int M, const float* g, const float* b, float* h32, f16* h16, float2* stats,
                           hipStream_t s, long long lo = 0);
+// fp32x3 attention (bert.hip): Q|K|V as f16 hi / lo planes [B*128, 2304] (lo at qkv + lo), ctx
+// written as hi / lo planes [B*128, 768] (lo at ctx + clo)
+int launch_bert_attention_x3(const f16* qkv, long long lo, const int32_t* mask, f16* ctx, long long clo, int B,
+                             hipStream_t s);
 
 // Split n fp32 weights into f16 planes for the fp32x3 path: hi = f16(w 2^e), lo = f16(w 2^e - hi)
 // with e the largest power of two keeping max |w| 2^e <= 2^14 (so hi never overflows and lo
@@ -131,6 +135,8 @@ struct Bottleneck {
   ConvLayer c1, c2, c3, ds;
   bool has_ds = false;
   size_t c3ds_w_off = 0, c3ds_b_off = 0;  // block 0: [conv3 | downsample] weights [4w][w+cin], summed bias
+  float c3ds_x3_scale = 1.f;              // fp32x3 path: its planes' scale (in wts_dual) and lo offset
+  size_t c3ds_x3_lo = 0;
 };
 struct ImageModel : ImageNet {
   DevBuf wts;   // f16 conv weights
@@ -155,6 +161,8 @@ struct ImageModel : ImageNet {
   // fp32x3 path (resnet_f32.hip): wts holds every bottleneck conv's f16 hi planes, then the lo
   // planes at x3_lo halfs (w_off indexes both); the stem, pooling and head run as on the fp32 path
   size_t x3_lo = 0;
+  float stem_x3_up = 1.f;  // 2^e: the gray stem's weight pre-scale (stem.x3_scale = 2^-e)
+  DevBuf wts_dual;  // fp32x3: block 0's [conv3 | downsample] hi / lo planes (c3ds_w_off, c3ds_x3_lo)
   int forward_x3(const uint8_t* img, int B, int H, int W, int C, float* feat, float* logits, float* probs,
                  hipStream_t s);
 };
@@ -187,6 +195,8 @@ struct MobileNetModel : ImageNet {
   // fp32x3 path (resnet_f32.hip): wts holds every bottleneck conv's f16 hi planes, then the lo
   // planes at x3_lo halfs (w_off indexes both); the stem, pooling and head run as on the fp32 path
   size_t x3_lo = 0;
+  float stem_x3_up = 1.f;  // 2^e: the gray stem's weight pre-scale (stem.x3_scale = 2^-e)
+  DevBuf wts_dual;  // fp32x3: block 0's [conv3 | downsample] hi / lo planes (c3ds_w_off, c3ds_x3_lo)
   int forward_x3(const uint8_t* img, int B, int H, int W, int C, float* feat, float* logits, float* probs,
                  hipStream_t s);
 };

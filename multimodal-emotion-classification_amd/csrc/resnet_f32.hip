@@ -207,6 +207,148 @@ __global__ __launch_bounds__(512, 1) void stem_pool_gray_f32_kernel(const uint8_
   }
 }
 
+// fp32x3 form of the gray stem: the same (pixel, inside) 2-channel conv + BN + ReLU + max-pool,
+// on v_mfma_f32_32x32x8_f16. The A operand (pixel value 0..255, inside 0 / 1) is exact in f16,
+// so only the folded weights are split (w 2^e = hi + lo, wscale = 2^-e): two f16 products per
+// fp32 product (A.lo, then A.hi), 49 taps padded to 52 = 13 k-steps of 8 (4 taps x 2 channels;
+// lane half kk supplies taps 4s + 2kk, 4s + 2kk + 1). Writes the pooled map as hi / lo planes
+// (y, y + lo): the first bottleneck's split operand, no f32 intermediate.
+typedef _Float16 hpair __attribute__((ext_vector_type(2)));
+
+__global__ __launch_bounds__(512, 1) void stem_pool_gray_x3_kernel(const uint8_t* __restrict__ img, int ntiles,
+                                                                  const float* __restrict__ wg, float wsc_up,
+                                                                  float wscale, const float* __restrict__ bias,
+                                                                  f16* __restrict__ y, long long lo) {
+  __shared__ __attribute__((aligned(16))) f16 swh[52 * 2 * 64];  // [tap][channel][co], taps 49..51 zero
+  __shared__ __attribute__((aligned(16))) f16 swl[52 * 2 * 64];
+  __shared__ __attribute__((aligned(16))) hpair patch[SGF_P * SGF_P];  // (pixel, inside)
+  __shared__ __attribute__((aligned(16))) float stg[SGF_NPIX * 64];
+  const int tid = threadIdx.x, lane = tid & 63;
+  const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int li = lane & 31, kk = lane >> 5;
+  for (int i = tid; i < 52 * 2 * 64; i += 512) {
+    const float x = i < 49 * 2 * 64 ? wg[i] * wsc_up : 0.f;  // w 2^e (exact)
+    const f16 h = (f16)x;
+    swh[i] = h;
+    swl[i] = (f16)(x - (float)h);
+  }
+  int base[3], nt[3];
+  float bv[3];
+#pragma unroll
+  for (int q = 0; q < 3; ++q) {
+    const int pr = wave + 8 * q;
+    const int i = min((pr >> 1) * 32 + li, SGF_NPIX - 1);
+    const int sr = i / SGF_S, sc = i - (i / SGF_S) * SGF_S;
+    base[q] = 2 * sr * SGF_P + 2 * sc;
+    nt[q] = pr & 1;
+    bv[q] = bias[nt[q] * 32 + li];
+  }
+  const int npair = wave < 4 ? 3 : 2;
+  auto patch_load = [&](int t, int (&v)[SGF_PL]) {
+    const int b = t / 49, tt = t - (t / 49) * 49;
+    const int r0 = 4 * (tt / 7) * 8 - 5, c0 = 4 * (tt - (tt / 7) * 7) * 8 - 5;
+#pragma unroll
+    for (int j = 0; j < SGF_PL; ++j) {
+      const int i = tid + 512 * j;
+      const int pr = i / SGF_P, pc = i - (i / SGF_P) * SGF_P;
+      const int ih = r0 + pr, iw = c0 + pc;
+      v[j] = (i < SGF_P * SGF_P && ih >= 0 && ih < 224 && iw >= 0 && iw < 224) ? (int)img[((size_t)b * 224 + ih) * 224 + iw]
+                                                                                : -1;
+    }
+  };
+  auto patch_store = [&](const int (&v)[SGF_PL]) {
+#pragma unroll
+    for (int j = 0; j < SGF_PL; ++j) {
+      const int i = tid + 512 * j;
+      if (i < SGF_P * SGF_P) {
+        hpair h;
+        h.x = v[j] >= 0 ? (f16)(float)v[j] : (f16)0.f;
+        h.y = v[j] >= 0 ? (f16)1.f : (f16)0.f;
+        patch[i] = h;
+      }
+    }
+  };
+  // per k-step s, this lane half's two taps t0 = 4s + 2kk, t1 = t0 + 1: patch offsets (kh * P + kw)
+  int toff[13][2];
+  bool tin[13][2];
+#pragma unroll
+  for (int st = 0; st < 13; ++st)
+#pragma unroll
+    for (int u = 0; u < 2; ++u) {
+      const int t = 4 * st + 2 * kk + u;
+      tin[st][u] = t < 49;
+      toff[st][u] = t < 49 ? (t / 7) * SGF_P + (t - (t / 7) * 7) : 0;
+    }
+  int pv[SGF_PL];
+  if (blockIdx.x < ntiles) {
+    patch_load(blockIdx.x, pv);
+    patch_store(pv);
+  }
+  for (int t = blockIdx.x; t < ntiles; t += gridDim.x) {
+    const int b = t / 49, tt = t - (t / 49) * 49;
+    const int py0 = (tt / 7) * 8, px0 = (tt - (tt / 7) * 7) * 8;
+    __syncthreads();
+    const int tn = t + gridDim.x;
+    if (tn < ntiles) patch_load(tn, pv);
+    floatx16 acc[3];
+#pragma unroll
+    for (int q = 0; q < 3; ++q)
+#pragma unroll
+      for (int e = 0; e < 16; ++e) acc[q][e] = 0.f;
+#pragma unroll
+    for (int st = 0; st < 13; ++st) {
+#pragma unroll
+      for (int q = 0; q < 3; ++q) {
+        if (q < npair) {
+          const hpair p0 = tin[st][0] ? patch[base[q] + toff[st][0]] : hpair{(f16)0.f, (f16)0.f};
+          const hpair p1 = tin[st][1] ? patch[base[q] + toff[st][1]] : hpair{(f16)0.f, (f16)0.f};
+          const half4 av = {p0.x, p0.y, p1.x, p1.y};
+          const int w0 = ((4 * st + 2 * kk) * 2) * 64 + nt[q] * 32 + li;  // [tap t0][ch 0][co]
+          const half4 bl = {swl[w0], swl[w0 + 64], swl[w0 + 128], swl[w0 + 192]};
+          const half4 bh = {swh[w0], swh[w0 + 64], swh[w0 + 128], swh[w0 + 192]};
+          acc[q] = __builtin_amdgcn_mfma_f32_32x32x8f16(av, bl, acc[q], 0, 0, 0);
+          acc[q] = __builtin_amdgcn_mfma_f32_32x32x8f16(av, bh, acc[q], 0, 0, 0);
+        }
+      }
+    }
+#pragma unroll
+    for (int q = 0; q < 3; ++q)
+      if (q < npair)
+#pragma unroll
+        for (int e = 0; e < 16; ++e) {
+          const int pix = ((wave + 8 * q) >> 1) * 32 + (e & 3) + 8 * (e >> 2) + 4 * kk;
+          if (pix < SGF_NPIX) stg[pix * 64 + nt[q] * 32 + li] = fmaxf(__builtin_fmaf(acc[q][e], wscale, bv[q]), 0.f);
+        }
+    __syncthreads();
+    if (tn < ntiles) patch_store(pv);
+    const float4* stg4 = reinterpret_cast<const float4*>(stg);
+#pragma unroll
+    for (int it = 0; it < 2; ++it) {
+      const int idx = it * 512 + tid, pp = idx >> 4, cq = idx & 15;
+      const int py = pp >> 3, px = pp & 7;
+      float4 m = make_float4(-INFINITY, -INFINITY, -INFINITY, -INFINITY);
+#pragma unroll
+      for (int dy = 0; dy < 3; ++dy) {
+        const int sr = 2 * py + dy, R = 2 * py0 - 1 + sr;
+        if (R < 0 || R >= 112) continue;
+#pragma unroll
+        for (int dx = 0; dx < 3; ++dx) {
+          const int sc = 2 * px + dx, Cc = 2 * px0 - 1 + sc;
+          if (Cc < 0 || Cc >= 112) continue;
+          const float4 v = stg4[(sr * SGF_S + sc) * 16 + cq];
+          m.x = fmaxf(m.x, v.x); m.y = fmaxf(m.y, v.y); m.z = fmaxf(m.z, v.z); m.w = fmaxf(m.w, v.w);
+        }
+      }
+      const size_t o = (((size_t)b * 56 + py0 + py) * 56 + px0 + px) * 64 + cq * 4;
+      const half4 h = {(f16)m.x, (f16)m.y, (f16)m.z, (f16)m.w};
+      const half4 l = {(f16)(m.x - (float)h[0]), (f16)(m.y - (float)h[1]), (f16)(m.z - (float)h[2]),
+                       (f16)(m.w - (float)h[3])};
+      *reinterpret_cast<half4*>(y + o) = h;
+      *reinterpret_cast<half4*>(y + lo + o) = l;
+    }
+  }
+}
+
 int ImageModel::create_f32(const float* blob, size_t n) {
   BlobReader rd(blob, n);
   std::vector<float> w;
@@ -311,6 +453,17 @@ int ImageModel::create_f32(const float* blob, size_t n) {
     // same offsets as in wts32 (the stem keeps its f32 weights: it runs the fp32 kernels)
     std::vector<f16> hl(2 * w.size(), (f16)0.f);
     x3_lo = w.size();
+    {  // the gray stem's folded weights: split on the device (stem_pool_gray_x3_kernel) at scale 2^e
+      float mx = 0.f;
+      for (int i = 0; i < 49 * 2 * 64; ++i) mx = std::max(mx, std::fabs(w[stem_gray32_off + i]));
+      int e = 0;
+      if (mx > 0.f) {
+        e = (int)std::floor(std::log2(16384.0 / (double)mx));
+        while (std::ldexp((double)mx, e) > 16384.0) --e;
+      }
+      stem_x3_up = std::ldexp(1.0f, e);
+      stem.x3_scale = std::ldexp(1.0f, -e);
+    }
     auto split = [&](ConvLayer& L) {
       const size_t cnt = (size_t)L.cout * L.cin * L.ks * L.ks;
       L.x3_scale = split_planes(w.data() + L.w_off, cnt, hl.data() + L.w_off, hl.data() + x3_lo + L.w_off);
@@ -321,7 +474,29 @@ int ImageModel::create_f32(const float* blob, size_t n) {
       split(bk.c3);
       if (bk.has_ds) split(bk.ds);
     }
+    // block 0 of each stage: conv3 and the downsample as ONE dual-source GEMM over K = [w | cin]
+    // (the f16 path's A_DUAL), weights [W3 | Wds] split with one scale, bias b3 + bds
+    std::vector<float> cat;
+    std::vector<f16> hl2;
+    for (Bottleneck& bk : blocks) {
+      if (!bk.has_ds) continue;
+      const int wd = bk.c3.cin, cin = bk.ds.cin, Kt = wd + cin, No = bk.c3.cout;
+      cat.assign((size_t)No * Kt, 0.f);
+      for (int o = 0; o < No; ++o) {
+        for (int k = 0; k < wd; ++k) cat[(size_t)o * Kt + k] = w[bk.c3.w_off + (size_t)o * wd + k];
+        for (int k = 0; k < cin; ++k) cat[(size_t)o * Kt + wd + k] = w[bk.ds.w_off + (size_t)o * cin + k];
+      }
+      bk.c3ds_w_off = hl2.size();
+      hl2.resize(hl2.size() + 2 * cat.size());
+      bk.c3ds_x3_scale = split_planes(cat.data(), cat.size(), hl2.data() + bk.c3ds_w_off,
+                                      hl2.data() + bk.c3ds_w_off + cat.size());
+      bk.c3ds_x3_lo = cat.size();
+      bk.c3ds_b_off = pr.size();
+      for (int o = 0; o < No; ++o) pr.push_back(pr[bk.c3.b_off + o] + pr[bk.ds.b_off + o]);
+    }
     MEC_TRY(upload(wts, hl.data(), hl.size() * sizeof(f16)));
+    MEC_TRY(upload(wts_dual, hl2.data(), hl2.size() * sizeof(f16)));
+    MEC_TRY(upload(prm, pr.data(), pr.size() * sizeof(float)));  // + the dual biases
   }
   return 0;
 }
@@ -450,35 +625,41 @@ int ImageModel::forward_f32(const uint8_t* img, int B, int H, int W, int C, floa
 }
 
 // fp32x3 path: the fp32 path with every bottleneck conv on split-f16 operands (gemm_glds.hip
-// split mode: A_PLAIN 1x1 convs and A_CONV 3x3 / strided 1x1 convs, three f16 MFMA passes into
-// one fp32 accumulator, weights pre-scaled by 2^e and undone in the epilogue). Activations
-// between convs are f16 hi / lo planes (the same bytes as f32); the downsample branch is written
-// in f32 and added as an f32 residual; an identity residual is added as hi + lo (exact). The
-// stem (conv + BN + ReLU + max-pool), the average pool and the head are the fp32 path's kernels.
+// split mode: A_PLAIN 1x1 convs, A_CONV 3x3 convs, and each stage's first block's conv3 +
+// downsample as one A_DUAL GEMM over K = [w | cin]; three f16 MFMA passes into one fp32
+// accumulator, weights pre-scaled by 2^e and undone in the epilogue). Activations between convs
+// are f16 hi / lo planes (the same bytes as f32) in one arena whose lo half sits a fixed L
+// elements after the hi half, so every operand -- both sources of a dual GEMM included -- finds
+// its lo plane at the same offset; an identity residual is added as hi + lo (exact). The stem
+// (conv + BN + ReLU + max-pool), the average pool and the head are the fp32 path's kernels.
 int ImageModel::forward_x3(const uint8_t* img, int B, int H, int W, int C, float* feat, float* logits, float* probs,
                            hipStream_t s) {
-  MEC_REQUIRE(wts.p && wts32.p && x3_lo, "image: fp32x3 weights missing");
+  MEC_REQUIRE(wts.p && wts32.p && wts_dual.p && x3_lo, "image: fp32x3 weights missing");
   const bool fer = (H == 48 && W == 48 && C == 1);
-  // per image (floats): im2col 12544 x 160 (RGB stem); S32 112*112*64 (stem f32 out, then the
-  // f32 downsample DS); X, Y as hi|lo planes of 56*56*256; T1 (56*56*128), T2 (56*56*64) planes
+  // per image: im2col 12544 x 160 f32 (RGB stem); S32 f32 56*56*64 (stem out; the RGB stem's
+  // 112*112*64 pre-pool map goes to the arena's bytes); arena hi half: X, Y (56*56*256), T1
+  // (56*56*128), T2 (56*56*64) halfs, then the lo half (same layout)
   const size_t big = (size_t)56 * 56 * 256, t1n = (size_t)56 * 56 * 128, t2n = (size_t)56 * 56 * 64;
-  const size_t per_img = 224 * 224 + ((size_t)12544 * STEM_K + (size_t)112 * 112 * 64 + 2 * big + t1n + t2n + 2048) * 4;
+  const size_t arena_img = 2 * big + t1n + t2n;  // halfs per image per half-arena
+  const size_t per_img = 224 * 224 + ((size_t)12544 * STEM_K + (size_t)56 * 56 * 64 + 2048) * 4 + arena_img * 2 * 2;
   const size_t need = per_img * (size_t)B + 8192;
   if (ws.bytes < need) MEC_TRY(ws.ensure(need));
   char* p = ws.as<char>();
   uint8_t* resized = reinterpret_cast<uint8_t*>(p);
   p += ((size_t)B * 224 * 224 + 255) / 256 * 256;
   float* A0 = reinterpret_cast<float*>(p); p += (size_t)B * 12544 * STEM_K * 4;
-  float* S32 = reinterpret_cast<float*>(p); p += (size_t)B * 112 * 112 * 64 * 4;
-  f16* X = reinterpret_cast<f16*>(p); p += (size_t)B * big * 4;
-  f16* Y = reinterpret_cast<f16*>(p); p += (size_t)B * big * 4;
-  f16* T1 = reinterpret_cast<f16*>(p); p += (size_t)B * t1n * 4;
-  f16* T2 = reinterpret_cast<f16*>(p); p += (size_t)B * t2n * 4;
-  float* pooled = reinterpret_cast<float*>(p);
-  const long long lo_big = (long long)B * big, lo_t1 = (long long)B * t1n, lo_t2 = (long long)B * t2n;
+  float* S32 = reinterpret_cast<float*>(p); p += (size_t)B * 56 * 56 * 64 * 4;
+  float* pooled = reinterpret_cast<float*>(p); p += (size_t)B * 2048 * 4;
+  f16* arena = reinterpret_cast<f16*>(p);
+  const long long L = (long long)B * arena_img;  // lo plane = hi plane + L, for every activation
+  f16* X = arena;
+  f16* Y = X + (size_t)B * big;
+  f16* T1 = Y + (size_t)B * big;
+  f16* T2 = T1 + (size_t)B * t1n;
 
   const float* Wt32 = wts32.as<float>();
   const f16* Wt = wts.as<f16>();
+  const f16* Wd = wts_dual.as<f16>();
   const long long wlo = (long long)x3_lo;
   const float* P = prm.as<float>();
   const uint8_t* stem_in = img;
@@ -490,7 +671,7 @@ int ImageModel::forward_x3(const uint8_t* img, int B, int H, int W, int C, float
   }
   // stem -> S32 f32 [B,56,56,64] (the fp32 path's kernels), then split into X's planes
   MEC_TRY(prof.begin(TAG_RESNET_STEM, s));
-  if (Cin == 1 && opt().stem_gray_f32) {
+  if (Cin == 1 && opt().stem_gray_f32) {  // conv + BN + ReLU + pool on split weights -> X's planes
     static int ncu = 0;
     if (!ncu) {
       int dev = 0;
@@ -498,30 +679,27 @@ int ImageModel::forward_x3(const uint8_t* img, int B, int H, int W, int C, float
       MEC_HIP(hipDeviceGetAttribute(&ncu, hipDeviceAttributeMultiprocessorCount, dev));
     }
     const int ntiles = B * 49;
-    hipLaunchKernelGGL(stem_pool_gray_f32_kernel, dim3(std::min(ntiles, ncu)), dim3(512), 0, s, stem_in, ntiles,
-                       Wt32 + stem_gray32_off, P + stem.b_off, S32);
+    hipLaunchKernelGGL(stem_pool_gray_x3_kernel, dim3(std::min(ntiles, ncu)), dim3(512), 0, s, stem_in, ntiles,
+                       Wt32 + stem_gray32_off, stem_x3_up, stem.x3_scale, P + stem.b_off, X, L);
     MEC_LAUNCH_CHECK();
   } else {
     const size_t total = (size_t)B * 112 * 112 * (STEM_K / 4);
     hipLaunchKernelGGL(stem_im2col_f32_kernel, dim3((unsigned)((total + 255) / 256)), dim3(256), 0, s, stem_in, B,
                        Cin, A0);
     MEC_LAUNCH_CHECK();
-    GemmParams g;  // the stem output (112 x 112) goes to the f32 scratch in the ping buffer's bytes
-    float* Y32 = reinterpret_cast<float*>(Y);
+    GemmParams g;  // the 112 x 112 pre-pool map (B * 802816 floats) fits in the arena's bytes
+    float* Y32 = reinterpret_cast<float*>(arena);
     g.A = A0; g.B32 = Wt32 + stem.w_off; g.bias = P + stem.b_off; g.act = ACT_RELU; g.C32 = Y32;
     g.M = B * 112 * 112; g.N = 64; g.K = STEM_K;
     MEC_TRY(launch_gemm_f32(g, s, nullptr, 0));
     const size_t tp = (size_t)B * 56 * 56 * 16;
     hipLaunchKernelGGL(maxpool_f32_kernel, dim3((unsigned)((tp + 255) / 256)), dim3(256), 0, s, Y32, B, 112, 64, 56, S32);
     MEC_LAUNCH_CHECK();
-  }
-  {
     const size_t n4 = (size_t)B * 56 * 56 * 64 / 4;
-    hipLaunchKernelGGL(split_f32_kernel, dim3((unsigned)((n4 + 255) / 256)), dim3(256), 0, s, S32, n4, X, lo_big);
+    hipLaunchKernelGGL(split_f32_kernel, dim3((unsigned)((n4 + 255) / 256)), dim3(256), 0, s, S32, n4, X, L);
     MEC_LAUNCH_CHECK();
   }
   MEC_TRY(prof.end(TAG_RESNET_STEM, s));
-  float* DS = S32;  // the stem's f32 scratch, reused for the downsample branch
   GemmParams g;
   f16* cur = X;
   f16* other = Y;
@@ -530,36 +708,31 @@ int ImageModel::forward_x3(const uint8_t* img, int B, int H, int W, int C, float
     const int wd = bk.c1.cout, cin = bk.c1.cin, st = bk.c2.stride;
     const int OH = (Hc + 2 - 3) / st + 1;
     g = GemmParams();
-    g.split = 1; g.A = cur; g.a_lo = lo_big; g.B = Wt + bk.c1.w_off; g.b_lo = wlo; g.oscale = bk.c1.x3_scale;
-    g.bias = P + bk.c1.b_off; g.act = ACT_RELU; g.C16 = T1; g.c_lo = lo_t1;
+    g.split = 1; g.A = cur; g.a_lo = L; g.B = Wt + bk.c1.w_off; g.b_lo = wlo; g.oscale = bk.c1.x3_scale;
+    g.bias = P + bk.c1.b_off; g.act = ACT_RELU; g.C16 = T1; g.c_lo = L;
     g.M = B * Hc * Hc; g.N = wd; g.K = cin;
     MEC_TRY(launch_gemm(g, s, &prof, TAG_RESNET_CONV1X1));
     g = GemmParams();
-    g.split = 1; g.amode = A_CONV; g.A = T1; g.a_lo = lo_t1; g.B = Wt + bk.c2.w_off; g.b_lo = wlo;
-    g.oscale = bk.c2.x3_scale; g.bias = P + bk.c2.b_off; g.act = ACT_RELU; g.C16 = T2; g.c_lo = lo_t2;
+    g.split = 1; g.amode = A_CONV; g.A = T1; g.a_lo = L; g.B = Wt + bk.c2.w_off; g.b_lo = wlo;
+    g.oscale = bk.c2.x3_scale; g.bias = P + bk.c2.b_off; g.act = ACT_RELU; g.C16 = T2; g.c_lo = L;
     g.M = B * OH * OH; g.N = wd; g.K = 9 * wd;
     g.H = Hc; g.W = Hc; g.C = wd; g.OH = OH; g.OW = OH; g.ks = 3; g.stride = st; g.pad = 1;
     MEC_TRY(launch_gemm(g, s, &prof, TAG_RESNET_CONV3X3));
-    g = GemmParams();  // relu(bn3(conv3(t2)) + identity)
-    if (bk.has_ds) {  // downsample = BN(conv1x1/s(x)) in f32, added as an f32 residual
-      GemmParams d;
-      d.split = 1; d.amode = A_CONV; d.A = cur; d.a_lo = lo_big; d.B = Wt + bk.ds.w_off; d.b_lo = wlo;
-      d.oscale = bk.ds.x3_scale; d.bias = P + bk.ds.b_off; d.C32 = DS;
-      d.M = B * OH * OH; d.N = 4 * wd; d.K = cin;
-      d.H = Hc; d.W = Hc; d.C = cin; d.OH = OH; d.OW = OH; d.ks = 1; d.stride = st; d.pad = 0;
-      MEC_TRY(launch_gemm(d, s, &prof, TAG_RESNET_CONV1X1));
-      g.R = DS; g.r_f32 = 1;
-    } else {
-      g.R = cur; g.r_lo = lo_big;
+    g = GemmParams();
+    g.split = 1; g.a_lo = L; g.act = ACT_RELU; g.C16 = other; g.c_lo = L; g.M = B * OH * OH; g.N = 4 * wd;
+    if (bk.has_ds) {  // relu(bn3(conv3(t2)) + bn_ds(conv_ds/s(x))) as one GEMM over K = [w | cin]
+      g.amode = A_DUAL; g.A = T2; g.K1 = wd; g.A2 = cur; g.B = Wd + bk.c3ds_w_off; g.b_lo = (long long)bk.c3ds_x3_lo;
+      g.oscale = bk.c3ds_x3_scale; g.bias = P + bk.c3ds_b_off; g.K = wd + cin;
+      g.H = Hc; g.W = Hc; g.C = cin; g.OH = OH; g.OW = OH; g.ks = 1; g.stride = st; g.pad = 0;
+    } else {  // relu(bn3(conv3(t2)) + x)
+      g.A = T2; g.B = Wt + bk.c3.w_off; g.b_lo = wlo; g.oscale = bk.c3.x3_scale; g.bias = P + bk.c3.b_off;
+      g.R = cur; g.r_lo = L; g.K = wd;
     }
-    g.split = 1; g.A = T2; g.a_lo = lo_t2; g.B = Wt + bk.c3.w_off; g.b_lo = wlo; g.oscale = bk.c3.x3_scale;
-    g.bias = P + bk.c3.b_off; g.act = ACT_RELU; g.C16 = other; g.c_lo = lo_big;
-    g.M = B * OH * OH; g.N = 4 * wd; g.K = wd;
     MEC_TRY(launch_gemm(g, s, &prof, TAG_RESNET_CONV1X1));
     std::swap(cur, other);
     Hc = OH;
   }
-  hipLaunchKernelGGL(avgpool_split_kernel, dim3(B, 2048 / 256), dim3(256), 0, s, cur, lo_big, Hc * Hc, 2048, pooled);
+  hipLaunchKernelGGL(avgpool_split_kernel, dim3(B, 2048 / 256), dim3(256), 0, s, cur, L, Hc * Hc, 2048, pooled);
   MEC_LAUNCH_CHECK();
   MEC_TRY(launch_linear_mfma<BACT_RELU>(pooled, 2048, B, 2048, P + fc1_off, P + fc1b_off, 512, feat, 512, nullptr, 0, s));
   MEC_TRY(launch_head7(feat, B, 512, P + fc2_off, P + fc2b_off, logits, probs, s));
