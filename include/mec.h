@@ -152,9 +152,10 @@ int mec_conv_f32(const float* x, const float* w, const float* bias, const float*
  *   "gemm_f32_tag" tag*100000+id  pin an fp32 tile for one launch class (default: BERT FFN1 -> 8)
  *   "gemm_f32_family" 0|[16]|32  fp32 tiles of one MFMA shape only (16x16x4 / 32x32x2): one k order
  *                          for every shape, so rows do not depend on the batch size
- *   "gemm_prefetch_r" 0|[1]  f16 residual prefetch in short-K GEMMs
+ *   "gemm_prefetch_r" 0|[1]  f16 (and split hi / lo) residual prefetch in short-K GEMMs
  *   "gemm_group_m" 0|2|4|[8]|16  ping-pong GEMM tile order inside each XCD's tile range (0: row-major,
  *                          G: G-panel groups of M walked M-fastest, fewer weight re-fetches)
+ *   "gemm_glds_group_m" 0|2|4|[8]|16  the same tile order for the multi-stage GEMM engine
  *   "conv3x3_direct" 0|[1] layer1 3x3 conv on the halo-tile kernel (mec_conv_f16 too)
  *   "conv3x3_halo" 0|[1]   layers 2-3 stride-1 3x3 convs on the halo kernel (mec_conv_f16 too;
  *                          fp32 accumulation in another order: not bit-identical to 0)

@@ -292,6 +292,10 @@ int set_option(Options& o, const std::string& k, int value) {
     o.gemm_group_m = value;
     return 0;
   }
+  if (k == "gemm_glds_group_m" && (value == 0 || value == 2 || value == 4 || value == 8 || value == 16)) {
+    o.gemm_glds_group_m = value;
+    return 0;
+  }
   if (k == "fusion_split" && (value == 0 || value == 1)) { o.fusion_split = value; return 0; }
   if (k == "speech_spin_limit" && (value == -1 || (probe && value >= 0))) { o.speech_spin_limit = value; return 0; }
   if (k == "gemm_debug" && (value == 0 || (probe && value >= 1 && value <= 5))) { o.gemm_debug = value; return 0; }

@@ -330,17 +330,28 @@ __global__ __launch_bounds__(256) void bert_attention_kernel(const f16* __restri
 //   O^T = V^T P^T    P (x 2^12, exact, so its small entries stay out of the f16 subnormals) split
 //                    into hi / lo in registers, 3 MFMAs per step; O scaled back by 2^-12
 // Layout and lane roles are attn_head's (keys in registers, one cross-half shuffle per row,
-// transposed V reads); the output is staged per wave and written as hi / lo planes
-// (ctx, ctx + clo) for the split O-projection. 96 KB of LDS: one workgroup per CU.
-__global__ __launch_bounds__(256) void bert_attention_x3_kernel(const f16* __restrict__ qkv, long long lo,
-                                                                const int32_t* __restrict__ mask,
-                                                                f16* __restrict__ ctx, long long clo) {
-  __shared__ __attribute__((aligned(16))) f16 sQ[2][ATT_L * BDH];
+// transposed V reads); Q goes straight to registers (each wave reads only its own 32 query
+// rows), so 64 KB of LDS (K, V planes) lets two workgroups share a CU and one's loads overlap
+// the other's MFMAs. The output is staged per wave in K's rows (free after the score loop) and
+// written as hi / lo planes (ctx, ctx + clo) for the split O-projection.
+__global__ __launch_bounds__(256, 2) void bert_attention_x3_kernel(const f16* __restrict__ qkv, long long lo,
+                                                                   const int32_t* __restrict__ mask,
+                                                                   f16* __restrict__ ctx, long long clo) {
   __shared__ __attribute__((aligned(16))) f16 sK[2][ATT_L * BDH];
   __shared__ __attribute__((aligned(16))) f16 sV[2][ATT_L * BDH];
   __shared__ float sBias[ATT_L];
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   const int b = blockIdx.x / BHEADS, h = blockIdx.x - (blockIdx.x / BHEADS) * BHEADS;
+  const int lr = lane & 31, lh = lane >> 5;
+  half8 qh[4], ql[4];  // this lane's Q row 32 wave + lr, k chunks 2 kk + lh (the MFMA B operand)
+  {
+    const f16* qrow = qkv + (size_t)b * ATT_L * (3 * BH) + h * BDH + (size_t)(32 * wave + lr) * (3 * BH);
+#pragma unroll
+    for (int kk = 0; kk < 4; ++kk) {
+      qh[kk] = *reinterpret_cast<const half8*>(qrow + (2 * kk + lh) * 8);
+      ql[kk] = *reinterpret_cast<const half8*>(qrow + lo + (2 * kk + lh) * 8);
+    }
+  }
 #pragma unroll
   for (int pl = 0; pl < 2; ++pl) {
     const f16* base = qkv + (pl ? lo : 0) + (size_t)b * ATT_L * (3 * BH) + h * BDH;
@@ -349,17 +360,14 @@ __global__ __launch_bounds__(256) void bert_attention_x3_kernel(const f16* __res
       const int c = tid + 256 * i;
       const int row = c >> 3, kc = c & 7;
       const f16* src = base + (size_t)row * (3 * BH) + kc * 8;
-      const uint4 q = *reinterpret_cast<const uint4*>(src);
       const uint4 k = *reinterpret_cast<const uint4*>(src + BH);
       const uint4 v = *reinterpret_cast<const uint4*>(src + 2 * BH);
-      *reinterpret_cast<uint4*>(sQ[pl] + row * BDH + aswz(row, kc) * 8) = q;
       *reinterpret_cast<uint4*>(sK[pl] + row * BDH + aswz(row, kc) * 8) = k;
       *reinterpret_cast<uint4*>(sV[pl] + row * BDH + vswz(row, kc) * 8) = v;
     }
   }
   if (tid < ATT_L) sBias[tid] = mask[(size_t)b * ATT_L + tid] ? 0.f : -3.4028234663852886e38f;  // finfo(f32).min
   __syncthreads();
-  const int lr = lane & 31, lh = lane >> 5;
   floatx16 s[4];
 #pragma unroll
   for (int t = 0; t < 4; ++t) {
@@ -368,16 +376,15 @@ __global__ __launch_bounds__(256) void bert_attention_x3_kernel(const f16* __res
 #pragma unroll
     for (int kk = 0; kk < 4; ++kk) {
       const int kc = 2 * kk + lh;
-      const int rk = 32 * t + lr, rq = 32 * wave + lr;
+      const int rk = 32 * t + lr;
       const half8 ah = *reinterpret_cast<const half8*>(sK[0] + rk * BDH + aswz(rk, kc) * 8);
       const half8 al = *reinterpret_cast<const half8*>(sK[1] + rk * BDH + aswz(rk, kc) * 8);
-      const half8 bh = *reinterpret_cast<const half8*>(sQ[0] + rq * BDH + aswz(rq, kc) * 8);
-      const half8 bl = *reinterpret_cast<const half8*>(sQ[1] + rq * BDH + aswz(rq, kc) * 8);
-      s[t] = __builtin_amdgcn_mfma_f32_32x32x16_f16(al, bh, s[t], 0, 0, 0);
-      s[t] = __builtin_amdgcn_mfma_f32_32x32x16_f16(ah, bl, s[t], 0, 0, 0);
-      s[t] = __builtin_amdgcn_mfma_f32_32x32x16_f16(ah, bh, s[t], 0, 0, 0);
+      s[t] = __builtin_amdgcn_mfma_f32_32x32x16_f16(al, qh[kk], s[t], 0, 0, 0);
+      s[t] = __builtin_amdgcn_mfma_f32_32x32x16_f16(ah, ql[kk], s[t], 0, 0, 0);
+      s[t] = __builtin_amdgcn_mfma_f32_32x32x16_f16(ah, qh[kk], s[t], 0, 0, 0);
     }
   }
+  __syncthreads();  // every wave is done with sK: its rows stage the output below
   float mx = -INFINITY;
 #pragma unroll
   for (int t = 0; t < 4; ++t)
@@ -437,7 +444,7 @@ __global__ __launch_bounds__(256) void bert_attention_x3_kernel(const f16* __res
       o[u] = __builtin_amdgcn_mfma_f32_32x32x16_f16(vh, ph, o[u], 0, 0, 0);
     }
   }
-  // O = o 2^-12 -> hi / lo planes, staged through this wave's own rows of sQ[0] / sQ[1]
+  // O = o 2^-12 -> hi / lo planes, staged through this wave's own rows of sK[0] / sK[1]
   const int rq = 32 * wave + lr;
 #pragma unroll
   for (int u = 0; u < 2; ++u)
@@ -451,8 +458,8 @@ __global__ __launch_bounds__(256) void bert_attention_x3_kernel(const f16* __res
         lv[e] = (f16)(x - (float)hv[e]);
       }
       const int d = 32 * u + 8 * gq + 4 * lh;
-      *reinterpret_cast<half4*>(sQ[0] + rq * BDH + aswz(rq, d >> 3) * 8 + (d & 7)) = hv;
-      *reinterpret_cast<half4*>(sQ[1] + rq * BDH + aswz(rq, d >> 3) * 8 + (d & 7)) = lv;
+      *reinterpret_cast<half4*>(sK[0] + rq * BDH + aswz(rq, d >> 3) * 8 + (d & 7)) = hv;
+      *reinterpret_cast<half4*>(sK[1] + rq * BDH + aswz(rq, d >> 3) * 8 + (d & 7)) = lv;
     }
   asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");  // wave-local rows: no barrier needed
   f16* out = ctx + (size_t)b * ATT_L * BH + h * BDH;
@@ -461,7 +468,7 @@ __global__ __launch_bounds__(256) void bert_attention_x3_kernel(const f16* __res
 #pragma unroll
     for (int i = 0; i < 4; ++i) {
       const int c = 64 * i + lane, r = 32 * wave + (c >> 3), kc = c & 7;
-      const uint4 v = *reinterpret_cast<const uint4*>(sQ[pl] + r * BDH + aswz(r, kc) * 8);
+      const uint4 v = *reinterpret_cast<const uint4*>(sK[pl] + r * BDH + aswz(r, kc) * 8);
       *reinterpret_cast<uint4*>(out + (pl ? clo : 0) + (size_t)r * BH + kc * 8) = v;
     }
 }

@@ -85,7 +85,8 @@ template <int BM, int BN, int WM, int WN, int MF, typename accv, int TI, int TJ,
 __device__ __forceinline__ void gemm_epilogue(const GemmParams& p, accv (&acc)[TI][TJ], f16* smem, int m0, int n0,
                                               int wm, int wn, int wave, int lane,
                                               const half8 (*rpre)[EpiGeom<BM, BN, WM, WN>::NPS] = nullptr,
-                                              const float4 (*rpre32)[EpiGeom<BM, BN, WM, WN>::NPS][2] = nullptr) {
+                                              const float4 (*rpre32)[EpiGeom<BM, BN, WM, WN>::NPS][2] = nullptr,
+                                              const half8 (*rplo)[EpiGeom<BM, BN, WM, WN>::NPS] = nullptr) {
   constexpr int TM = BM / WM, TN = BN / WN;
   constexpr int EPI_LD = TN + 4;
   const int M = p.M, N = p.N;
@@ -140,6 +141,11 @@ __device__ __forceinline__ void gemm_epilogue(const GemmParams& p, accv (&acc)[T
       for (int ps = 0; ps < NPS; ++ps)
 #pragma unroll
         for (int q = 0; q < 8; ++q) rv[ps][q] = (float)rpre[i][ps][q];
+    } else if (PRE == 3) {  // split residual in registers: hi + lo (exact in f32), as the load path below
+#pragma unroll
+      for (int ps = 0; ps < NPS; ++ps)
+#pragma unroll
+        for (int q = 0; q < 8; ++q) rv[ps][q] = (float)rpre[i][ps][q] + (float)rplo[i][ps][q];
     } else if (PRE == 2) {  // f32 residual already in registers; deferred LayerNorm applied here
 #pragma unroll
       for (int ps = 0; ps < NPS; ++ps) {

@@ -34,13 +34,14 @@ template <int BM, int BN, int WM, int WN, int NS, int AM, int DBG = 0, int MF = 
 __global__ __launch_bounds__(64 * WM * WN, (WM * WN == 4) ? 2 : 1) void gemm_glds_kernel(const GemmParams p) {
   // MF: 32 = v_mfma_f32_32x32x16_f16 tiles, 16 = v_mfma_f32_16x16x32_f16 tiles
   // DBG (probe builds only): 1 = no operand loads inside the K loop, 2 = no epilogue
-  // PRE: the residual tile (1 = f16, 2 = f32) is loaded into registers before the main loop,
+  // PRE: the residual tile (1 = f16, 2 = f32, 3 = f16 hi / lo planes of a split residual) is
+  // loaded into registers before the main loop,
   // so its HBM read hides under the operand loads and MFMAs instead of following them
   // (ResNet's short-K conv3 GEMMs, BERT's O-projection)
   // SP: split-f16 operands (GemmParams::split): the K loop runs over 3 K passes, pass 0 reading
   // the A lo plane, pass 1 the B lo plane, pass 2 both hi planes
   static_assert(BK == 64 || BK == 32, "BK");
-  static_assert(SP == 0 || PRE == 0, "split operands: no residual prefetch");
+  static_assert(SP == 0 || PRE == 0 || PRE == 3, "split operands: split residual prefetch only");
   constexpr int CH = BK / 8;                   // 16-B chunks per LDS row
   constexpr int RPI = 64 / CH;                 // rows per glds wave-instruction (1 KB)
   constexpr int NW = WM * WN;
@@ -71,7 +72,8 @@ __global__ __launch_bounds__(64 * WM * WN, (WM * WN == 4) ? 2 : 1) void gemm_gld
     const int xcd = bid & 7, q = nwg >> 3, r = nwg & 7;
     bid = (xcd < r ? xcd * (q + 1) : r * (q + 1) + (xcd - r) * q) + (bid >> 3);
   }
-  const int bm = bid / nbn, bn = bid - (bid / nbn) * nbn;
+  int bm, bn;
+  tile_coords(bid, nbm, nbn, p.group_m, bm, bn);
   const int m0 = bm * BM, n0 = bn * BN;
 
   // ---- per-lane DMA sources: lane -> (row in its 8-row group, physical chunk)
@@ -163,7 +165,8 @@ __global__ __launch_bounds__(64 * WM * WN, (WM * WN == 4) ? 2 : 1) void gemm_gld
   };
 
   using EG = EpiGeom<BM, BN, WM, WN>;
-  half8 rpre[PRE == 1 ? EG::SLABS : 1][EG::NPS];
+  half8 rpre[(PRE == 1 || PRE == 3) ? EG::SLABS : 1][EG::NPS];
+  half8 rplo[PRE == 3 ? EG::SLABS : 1][EG::NPS];
   float4 rpre32[PRE == 2 ? EG::SLABS : 1][EG::NPS][2];
   if constexpr (PRE != 0) {
     const int ech = lane % EG::CPR, erow = lane / EG::CPR;
@@ -173,8 +176,9 @@ __global__ __launch_bounds__(64 * WM * WN, (WM * WN == 4) ? 2 : 1) void gemm_gld
 #pragma unroll
       for (int ps = 0; ps < EG::NPS; ++ps) {
         const size_t off = (size_t)min(m0 + wm * TM + i * 32 + ps * EG::RPP + erow, M - 1) * N + col0;
-        if constexpr (PRE == 1) {
+        if constexpr (PRE == 1 || PRE == 3) {
           rpre[i][ps] = *reinterpret_cast<const half8*>(reinterpret_cast<const f16*>(p.R) + off);
+          if constexpr (PRE == 3) rplo[i][ps] = *reinterpret_cast<const half8*>(reinterpret_cast<const f16*>(p.R) + off + p.r_lo);
         } else {
           const float* R = reinterpret_cast<const float*>(p.R) + off;
           rpre32[i][ps][0] = *reinterpret_cast<const float4*>(R);
@@ -289,7 +293,7 @@ __global__ __launch_bounds__(64 * WM * WN, (WM * WN == 4) ? 2 : 1) void gemm_gld
     return;
   }
   gemm_epilogue<BM, BN, WM, WN, MF, accv, TI, TJ, PRE, false, ACT>(p, acc, smem, m0, n0, wm, wn, wave, lane, rpre,
-                                                                   rpre32);
+                                                                   rpre32, rplo);
 }
 
 
@@ -680,7 +684,11 @@ __global__ __launch_bounds__(512) void gemm_pp_kernel(const GemmParams p) {
 template <int BM, int BN, int WM, int WN, int NS, int MF, int BK, int ACT>
 static int launch_cfg_act(const GemmParams& p, hipStream_t s, int nwg, dim3 blk) {
   if (p.split) {  // split-f16 operands (fp32x3 path): three K passes, runtime activation
-    if (p.amode == A_PLAIN)
+    if (BM * BN <= 128 * 128 && opt().gemm_prefetch_r && p.amode == A_PLAIN && p.R && p.r_lo && p.K <= 512) {
+      // split identity residual of ResNet's conv3 GEMMs, both planes prefetched (PRE = 3)
+      if constexpr (BM * BN <= 128 * 128)
+        hipLaunchKernelGGL((gemm_glds_kernel<BM, BN, WM, WN, NS, A_PLAIN, 0, MF, BK, 3, -1, 1>), dim3(nwg), blk, 0, s, p);
+    } else if (p.amode == A_PLAIN)
       hipLaunchKernelGGL((gemm_glds_kernel<BM, BN, WM, WN, NS, A_PLAIN, 0, MF, BK, 0, -1, 1>), dim3(nwg), blk, 0, s, p);
     else if (p.amode == A_CONV)
       hipLaunchKernelGGL((gemm_glds_kernel<BM, BN, WM, WN, NS, A_CONV, 0, MF, BK, 0, -1, 1>), dim3(nwg), blk, 0, s, p);
@@ -703,7 +711,9 @@ static int launch_cfg_act(const GemmParams& p, hipStream_t s, int nwg, dim3 blk)
 }
 
 template <int BM, int BN, int WM, int WN, int NS, int MF = 32, int BK = 64>
-static int launch_cfg(const GemmParams& p, hipStream_t s) {
+static int launch_cfg(const GemmParams& p0, hipStream_t s) {
+  GemmParams p = p0;
+  p.group_m = opt().gemm_glds_group_m;
   const int nwg = ((p.M + BM - 1) / BM) * (p.N / BN);
   const dim3 blk(64 * WM * WN);
 #ifdef MEC_PROBES

@@ -75,7 +75,7 @@ enum KernelTag : int {
 struct Options {
   int gemm_bn = 0;          // forced f16 GEMM tile id (0 = autotune)
   int gemm_autotune = 1;
-  int gemm_prefetch_r = 1;  // f16 residual prefetch in short-K GEMMs
+  int gemm_prefetch_r = 1;  // f16 (and split hi / lo) residual prefetch in short-K GEMMs
   int gemm_f32_tile = 0;    // forced fp32 GEMM tile id (0 = autotune)
   // fp32 autotune family: 0 both, 16 = 16x16x4 tiles only, 32 = 32x32x2 only. 16 (default): one k
   // order for every shape, so the fp32 path is batch-invariant bit for bit, at no measured cost
@@ -101,6 +101,10 @@ struct Options {
   // tiles an XCD runs at once share G A panels and 32/G weight panels
   // (8: FFN1 reads 290 -> 227 MB per launch at B = 256, time unchanged; profiles/ffn1_traffic_gm*.json)
   int gemm_group_m = 8;
+  // the same tile order for the multi-stage (glds) engine, every tile and A mode; 0 = row-major
+  // (8: the fp32x3 FFN1 reads 911 -> 663 MB per launch at B = 256, time unchanged;
+  // profiles/ffn1_x3_traffic*.json)
+  int gemm_glds_group_m = 8;
   int fusion_r = 4;         // samples per fusion workgroup
   int fusion_split = 1;     // fusion as 3 launches
   int gemm_debug = 0, conv3x3_debug = 0, stem_debug = 0, audio_debug = 0, speech_debug = 0;  // probe builds only

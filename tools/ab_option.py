@@ -30,7 +30,7 @@ def main():
     ap.add_argument('--iters', type=int, default=5)
     ap.add_argument('--rounds', type=int, default=5)
     ap.add_argument('--probes', action='store_true', help='load libmec_hip_probes.so (probe option values)')
-    ap.add_argument('--precision', default='f16', choices=['f16', 'fp32'])
+    ap.add_argument('--precision', default='f16', choices=['f16', 'fp32', 'fp32x3'])
     a = ap.parse_args()
     dev = torch.device('cuda', 0)
     lib = _lib.load()

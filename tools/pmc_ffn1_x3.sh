@@ -7,17 +7,18 @@ cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
 export TMPDIR=/tmp
 TILE=${TILE:-10256}
 OUT=gpurun_out/pmc_ffn1_x3
+EXTRA=${GM:+--opt gemm_glds_group_m=$GM}  # optional glds tile order
 rm -rf $OUT; mkdir -p $OUT
 i=0
 for SET in "FETCH_SIZE" "WRITE_SIZE" "SQ_VALU_MFMA_BUSY_CYCLES SQ_BUSY_CYCLES GRBM_GUI_ACTIVE"; do
   i=$((i+1))
   timeout -s KILL 120 rocprofv3 --pmc $SET --kernel-include-regex "gemm_glds_kernel|gemm_pp_kernel" -d $OUT/p$i -o p -f csv -- \
-    python3 tools/encoder_profile.py --enc text --precision fp32x3 --iters 3 --opt gemm_bn=$TILE > $OUT/p$i.log 2>&1
+    python3 tools/encoder_profile.py --enc text --precision fp32x3 --iters 3 --opt gemm_bn=$TILE $EXTRA > $OUT/p$i.log 2>&1
   rc=$?
   echo "pass $i ($SET) rc=$rc"
   if [ $rc -ne 0 ]; then tail -5 $OUT/p$i.log; exit $rc; fi
 done
-TILE=$TILE python3 - <<'PY'
+TILE=$TILE GM=$GM python3 - <<'PY'
 import csv, glob, json, os
 from collections import defaultdict
 root = 'gpurun_out/pmc_ffn1_x3'
@@ -42,6 +43,7 @@ out = {'tile': int(os.environ['TILE']), 'M': 32768, 'kernel': k[:100], 'bytes_pe
        'source': 'rocprofv3 --pmc, separate FETCH_SIZE / WRITE_SIZE / SQ passes (tools/pmc_ffn1_x3.sh) over the '
                  'fp32x3 text encoder at B=256; FETCH_SIZE doubled per MI355X_MICROARCH.md (gfx950); algorithmic '
                  'bytes = fp32-equivalent operands (each hi+lo pair is 4 B)'}
-json.dump(out, open('gpurun_out/ffn1_x3_traffic.json', 'w'), indent=1)
+out['gemm_glds_group_m'] = int(os.environ.get('GM') or 0)
+json.dump(out, open('gpurun_out/ffn1_x3_traffic%s.json' % ('_gm' + os.environ['GM'] if os.environ.get('GM') else ''), 'w'), indent=1)
 print(json.dumps(out, indent=1))
 PY
