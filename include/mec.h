@@ -163,6 +163,8 @@ int mec_conv_f32(const float* x, const float* w, const float* bias, const float*
  *   "pw_chain_form" [0]|1|2  seam weight placement (LDS / registers)
  *   "bert_qkv_attn" 0|[1]  fused BERT QKV projection + attention
  *   "bert_ln_rows" 1|[2]|4  BERT LayerNorm rows per wave (all loads of a wave's rows in flight first)
+ *   "bert_cls_last" 0|[1]  BERT's last layer on the [CLS] rows only (K / V still for every token):
+ *                          the pooler, logits and CLS feature read nothing else of it; same bits as 0
  *   "resnet_chunk" [0]|n   ResNet layers 1-2 over n-image chunks
  *   "mbv2_impl" [0]|1|2    MobileNetV2 block form: 0 = time both per block shape, 1 = workgroup, 2 = wave
  *   "fusion_r" 1|2|[4]     samples per fusion workgroup

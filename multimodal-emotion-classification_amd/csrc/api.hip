@@ -284,6 +284,7 @@ int set_option(Options& o, const std::string& k, int value) {
     o.gemm_f32_family = value;
     return 0;
   }
+  if (k == "bert_cls_last" && (value == 0 || value == 1)) { o.bert_cls_last = value; return 0; }
   if (k == "bert_ln_rows" && (value == 1 || value == 2 || value == 4)) {
     o.bert_ln_rows = value;
     return 0;

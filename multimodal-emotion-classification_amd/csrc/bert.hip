@@ -202,6 +202,8 @@ __device__ __forceinline__ half4 lds_tr16(const f16* p) {
 // One (sequence, head) on 4 waves (wave w: queries 32w .. 32w+31) from Q, K (aswz rows)
 // and V (vswz rows) in LDS; sQ's rows are reused to stage the output, which is written to
 // ctx_row0 (query row 0 of this sequence and head, row stride BH).
+// NOUT < 32: only the wave's first NOUT query rows are stored (the [CLS]-only last layer: 1).
+template <int NOUT = 32>
 __device__ __forceinline__ void attn_head(f16* sQ, const f16* sK, const f16* sV, const float* sBias, int wave,
                                           int lane, f16* ctx_row0) {
   const int lr = lane & 31, lh = lane >> 5;
@@ -290,7 +292,7 @@ __device__ __forceinline__ void attn_head(f16* sQ, const f16* sK, const f16* sV,
   for (int i = 0; i < 4; ++i) {
     const int c = 64 * i + lane, r = 32 * wave + (c >> 3), kc = c & 7;
     const uint4 v = *reinterpret_cast<const uint4*>(sQ + r * BDH + aswz(r, kc) * 8);
-    *reinterpret_cast<uint4*>(ctx_row0 + (size_t)r * BH + kc * 8) = v;
+    if (NOUT == 32 || (c >> 3) < NOUT) *reinterpret_cast<uint4*>(ctx_row0 + (size_t)r * BH + kc * 8) = v;
   }
 }
 
@@ -321,6 +323,42 @@ __global__ __launch_bounds__(256) void bert_attention_kernel(const f16* __restri
   attn_head(sQ, sK, sV, sBias, wave, lane, ctx + (size_t)b * ATT_L * BH + h * BDH);
 }
 
+// [CLS]-only attention of BERT's last layer (bert_cls_last): K | V of every token from the K / V
+// GEMM ([B*128, 1536], kv), the [CLS] query row from qc ([B, 768]), the context written compact
+// ([B, 768]). Wave 0 runs attn_head for queries 0..31 with Q rows 1..31 zero (an MFMA output column
+// depends only on its own B column): the [CLS] row has bert_attention_kernel's bits.
+__global__ __launch_bounds__(256) void bert_attention_cls_kernel(const f16* __restrict__ kv,
+                                                                 const int32_t* __restrict__ mask,
+                                                                 const f16* __restrict__ qc,
+                                                                 f16* __restrict__ ctx) {
+  __shared__ __attribute__((aligned(16))) f16 sQ[32 * BDH];
+  __shared__ __attribute__((aligned(16))) f16 sK[ATT_L * BDH];
+  __shared__ __attribute__((aligned(16))) f16 sV[ATT_L * BDH];
+  __shared__ float sBias[ATT_L];
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int b = blockIdx.x / BHEADS, h = blockIdx.x - (blockIdx.x / BHEADS) * BHEADS;
+  const f16* base = kv + (size_t)b * ATT_L * (2 * BH) + h * BDH;
+#pragma unroll
+  for (int i = 0; i < 4; ++i) {
+    const int c = tid + 256 * i;
+    const int row = c >> 3, kc = c & 7;
+    const f16* src = base + (size_t)row * (2 * BH) + kc * 8;
+    const uint4 k = *reinterpret_cast<const uint4*>(src);
+    const uint4 v = *reinterpret_cast<const uint4*>(src + BH);
+    *reinterpret_cast<uint4*>(sK + row * BDH + aswz(row, kc) * 8) = k;
+    *reinterpret_cast<uint4*>(sV + row * BDH + vswz(row, kc) * 8) = v;
+  }
+  {
+    const int row = tid >> 3, kc = tid & 7;  // 32 rows x 8 chunks
+    const uint4 z = make_uint4(0u, 0u, 0u, 0u);
+    const uint4 q = row == 0 ? *reinterpret_cast<const uint4*>(qc + (size_t)b * BH + h * BDH + kc * 8) : z;
+    *reinterpret_cast<uint4*>(sQ + row * BDH + aswz(row, kc) * 8) = q;
+  }
+  if (tid < ATT_L) sBias[tid] = mask[(size_t)b * ATT_L + tid] ? 0.f : -3.4028234663852886e38f;  // finfo(f32).min
+  __syncthreads();
+  if (wave == 0) attn_head<1>(sQ, sK, sV, sBias, 0, lane, ctx + (size_t)b * BH + h * BDH);
+}
+
 // ----------------------------------------------------------------------------- fp32x3 attention
 // The fp32 attention of one (sequence, head) on split-f16 operands (the MEC_PREC_FP32X3 path):
 // Q, K, V arrive as f16 hi / lo planes (qkv, qkv + lo; the split QKV GEMM's output) and every
@@ -334,9 +372,19 @@ __global__ __launch_bounds__(256) void bert_attention_kernel(const f16* __restri
 // rows), so 64 KB of LDS (K, V planes) lets two workgroups share a CU and one's loads overlap
 // the other's MFMAs. The output is staged per wave in K's rows (free after the score loop) and
 // written as hi / lo planes (ctx, ctx + clo) for the split O-projection.
+// CLS = 1 (BERT's last layer with bert_cls_last: only the [CLS] query's context is read): qkv holds
+// K | V only ([B*128, 1536] planes, the K / V GEMM's output), the [CLS] query comes from qc ([B, 768]
+// planes, lo at qc + qclo) and the context is written compact ([B, 768] planes). All four waves
+// stage K and V; wave 0 then runs the full kernel's instruction sequence for queries 0..31 with Q
+// zero for all but query 0 (an MFMA output column depends only on its own B column), so the [CLS]
+// context has the full kernel's bits; waves 1-3 leave after staging.
+template <int CLS = 0>
 __global__ __launch_bounds__(256, 2) void bert_attention_x3_kernel(const f16* __restrict__ qkv, long long lo,
                                                                    const int32_t* __restrict__ mask,
-                                                                   f16* __restrict__ ctx, long long clo) {
+                                                                   f16* __restrict__ ctx, long long clo,
+                                                                   const f16* __restrict__ qc, long long qclo) {
+  constexpr int LD = CLS ? 2 * BH : 3 * BH;  // row stride of qkv
+  constexpr int KO = CLS ? 0 : BH;           // K column offset (V at KO + BH)
   __shared__ __attribute__((aligned(16))) f16 sK[2][ATT_L * BDH];
   __shared__ __attribute__((aligned(16))) f16 sV[2][ATT_L * BDH];
   __shared__ float sBias[ATT_L];
@@ -344,8 +392,20 @@ __global__ __launch_bounds__(256, 2) void bert_attention_x3_kernel(const f16* __
   const int b = blockIdx.x / BHEADS, h = blockIdx.x - (blockIdx.x / BHEADS) * BHEADS;
   const int lr = lane & 31, lh = lane >> 5;
   half8 qh[4], ql[4];  // this lane's Q row 32 wave + lr, k chunks 2 kk + lh (the MFMA B operand)
-  {
-    const f16* qrow = qkv + (size_t)b * ATT_L * (3 * BH) + h * BDH + (size_t)(32 * wave + lr) * (3 * BH);
+  if constexpr (CLS) {
+    const bool own = wave == 0 && lr == 0;
+    const f16* qrow = qc + (size_t)b * BH + h * BDH;
+#pragma unroll
+    for (int kk = 0; kk < 4; ++kk) {
+#pragma unroll
+      for (int j = 0; j < 8; ++j) { qh[kk][j] = (f16)0.f; ql[kk][j] = (f16)0.f; }
+      if (own) {
+        qh[kk] = *reinterpret_cast<const half8*>(qrow + (2 * kk + lh) * 8);
+        ql[kk] = *reinterpret_cast<const half8*>(qrow + qclo + (2 * kk + lh) * 8);
+      }
+    }
+  } else {
+    const f16* qrow = qkv + (size_t)b * ATT_L * LD + h * BDH + (size_t)(32 * wave + lr) * LD;
 #pragma unroll
     for (int kk = 0; kk < 4; ++kk) {
       qh[kk] = *reinterpret_cast<const half8*>(qrow + (2 * kk + lh) * 8);
@@ -354,20 +414,21 @@ __global__ __launch_bounds__(256, 2) void bert_attention_x3_kernel(const f16* __
   }
 #pragma unroll
   for (int pl = 0; pl < 2; ++pl) {
-    const f16* base = qkv + (pl ? lo : 0) + (size_t)b * ATT_L * (3 * BH) + h * BDH;
+    const f16* base = qkv + (pl ? lo : 0) + (size_t)b * ATT_L * LD + h * BDH;
 #pragma unroll
     for (int i = 0; i < 4; ++i) {
       const int c = tid + 256 * i;
       const int row = c >> 3, kc = c & 7;
-      const f16* src = base + (size_t)row * (3 * BH) + kc * 8;
-      const uint4 k = *reinterpret_cast<const uint4*>(src + BH);
-      const uint4 v = *reinterpret_cast<const uint4*>(src + 2 * BH);
+      const f16* src = base + (size_t)row * LD + kc * 8;
+      const uint4 k = *reinterpret_cast<const uint4*>(src + KO);
+      const uint4 v = *reinterpret_cast<const uint4*>(src + KO + BH);
       *reinterpret_cast<uint4*>(sK[pl] + row * BDH + aswz(row, kc) * 8) = k;
       *reinterpret_cast<uint4*>(sV[pl] + row * BDH + vswz(row, kc) * 8) = v;
     }
   }
   if (tid < ATT_L) sBias[tid] = mask[(size_t)b * ATT_L + tid] ? 0.f : -3.4028234663852886e38f;  // finfo(f32).min
   __syncthreads();
+  if (CLS && wave != 0) return;
   floatx16 s[4];
 #pragma unroll
   for (int t = 0; t < 4; ++t) {
@@ -384,7 +445,7 @@ __global__ __launch_bounds__(256, 2) void bert_attention_x3_kernel(const f16* __
       s[t] = __builtin_amdgcn_mfma_f32_32x32x16_f16(ah, qh[kk], s[t], 0, 0, 0);
     }
   }
-  __syncthreads();  // every wave is done with sK: its rows stage the output below
+  if constexpr (!CLS) __syncthreads();  // every wave is done with sK: its rows stage the output below
   float mx = -INFINITY;
 #pragma unroll
   for (int t = 0; t < 4; ++t)
@@ -462,20 +523,29 @@ __global__ __launch_bounds__(256, 2) void bert_attention_x3_kernel(const f16* __
       *reinterpret_cast<half4*>(sK[1] + rq * BDH + aswz(rq, d >> 3) * 8 + (d & 7)) = lv;
     }
   asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");  // wave-local rows: no barrier needed
-  f16* out = ctx + (size_t)b * ATT_L * BH + h * BDH;
+  f16* out = ctx + (size_t)b * (CLS ? 1 : ATT_L) * BH + h * BDH;
 #pragma unroll
   for (int pl = 0; pl < 2; ++pl)
 #pragma unroll
-    for (int i = 0; i < 4; ++i) {
+    for (int i = 0; i < (CLS ? 1 : 4); ++i) {
       const int c = 64 * i + lane, r = 32 * wave + (c >> 3), kc = c & 7;
       const uint4 v = *reinterpret_cast<const uint4*>(sK[pl] + r * BDH + aswz(r, kc) * 8);
-      *reinterpret_cast<uint4*>(out + (pl ? clo : 0) + (size_t)r * BH + kc * 8) = v;
+      if (!CLS || r == 0) *reinterpret_cast<uint4*>(out + (pl ? clo : 0) + (size_t)r * BH + kc * 8) = v;
     }
 }
 
 int launch_bert_attention_x3(const f16* qkv, long long lo, const int32_t* mask, f16* ctx, long long clo, int B,
                              hipStream_t s) {
-  hipLaunchKernelGGL(bert_attention_x3_kernel, dim3(B * BHEADS), dim3(256), 0, s, qkv, lo, mask, ctx, clo);
+  hipLaunchKernelGGL(bert_attention_x3_kernel<0>, dim3(B * BHEADS), dim3(256), 0, s, qkv, lo, mask, ctx, clo,
+                     nullptr, 0LL);
+  MEC_LAUNCH_CHECK();
+  return 0;
+}
+
+int launch_bert_attention_x3_cls(const f16* kv, long long lo, const int32_t* mask, const f16* qc, long long qclo,
+                                 f16* ctx, long long clo, int B, hipStream_t s) {
+  hipLaunchKernelGGL(bert_attention_x3_kernel<1>, dim3(B * BHEADS), dim3(256), 0, s, kv, lo, mask, ctx, clo, qc,
+                     qclo);
   MEC_LAUNCH_CHECK();
   return 0;
 }
@@ -742,8 +812,11 @@ int TextModel::forward(const int32_t* ids, const int32_t* mask, int B, int L, fl
   if (prec == PREC_FP32X3) return forward_x3(ids, mask, B, L, cls, logits, probs, s);
   const int M = B * L;
   // workspace: h32 | t32 (f32 [M,768]) ; h16 | ctx16 (f16 [M,768]) ; qkv16 [M,2304] / i16 [M,3072]
+  // + the [CLS]-row buffers of the last layer (bert_cls_last): h32c | t32c (f32 [B,768]) ; h16c | qc |
+  // ctxc (f16 [B,768]) ; fc (f16 [B,3072]) ; st1c | st2c ([B] float2)
   const size_t need = (size_t)M * BH * 4 * 2 + (size_t)M * BH * 2 * 2 + (size_t)M * BI * 2 + (size_t)B * BH * 4 +
-                      (size_t)M * 8 * 2;
+                      (size_t)M * 8 * 2 + (size_t)B * BH * 4 * 2 + (size_t)B * BH * 2 * 3 + (size_t)B * BI * 2 +
+                      (size_t)B * 8 * 2;
   if (M > ws_tokens) {
     MEC_TRY(ws.ensure(need));
     ws_tokens = M;
@@ -759,6 +832,16 @@ int TextModel::forward(const int32_t* ids, const int32_t* mask, int B, int L, fl
   p += (size_t)B * BH * 4;
   float2* st1 = reinterpret_cast<float2*>(p);  // LN1 row stats [M]
   float2* st2 = st1 + M;                       // LN2 row stats [M]
+  p += (size_t)M * 8 * 2;
+  float* h32c = reinterpret_cast<float*>(p); p += (size_t)B * BH * 4;
+  float* t32c = reinterpret_cast<float*>(p); p += (size_t)B * BH * 4;
+  f16* h16c = reinterpret_cast<f16*>(p); p += (size_t)B * BH * 2;
+  f16* qc = reinterpret_cast<f16*>(p); p += (size_t)B * BH * 2;
+  f16* ctxc = reinterpret_cast<f16*>(p); p += (size_t)B * BH * 2;
+  f16* fc = reinterpret_cast<f16*>(p); p += (size_t)B * BI * 2;
+  float2* st1c = reinterpret_cast<float2*>(p);
+  float2* st2c = st1c + B;
+  const bool cls_last = opt().bert_cls_last != 0;
 
   const float* E = emb.as<float>();
   const float* word = E;
@@ -781,6 +864,44 @@ int TextModel::forward(const int32_t* ids, const int32_t* mask, int B, int L, fl
     const float *bqkv = pl, *bo = pl + 2304, *g1 = pl + 3072, *b1 = pl + 3840, *bi = pl + 4608,
                 *bo2 = pl + 7680, *g2 = pl + 8448, *b2 = pl + 9216;
     GemmParams g;
+    if (cls_last && l == BLAYERS - 1 && l > 0) {
+      // [CLS]-only last layer: K / V for every token, everything else on the B [CLS] rows (the
+      // pooler, logits and CLS feature read nothing else). Same kernels and expressions per row as
+      // the full layer below (its O-proj residual is the deferred LN2 of layer l-1), so same bits.
+      const float* pg2 = P + PRM_LAYER * (l - 1) + 8448;
+      RowGather rg{};
+      rg.n = 3;
+      rg.src[0] = reinterpret_cast<const char*>(h32); rg.dst[0] = reinterpret_cast<char*>(h32c);
+      rg.sstride[0] = (long long)L * BH * 4; rg.bytes[0] = BH * 4;
+      rg.src[1] = reinterpret_cast<const char*>(h16); rg.dst[1] = reinterpret_cast<char*>(h16c);
+      rg.sstride[1] = (long long)L * BH * 2; rg.bytes[1] = BH * 2;
+      rg.src[2] = reinterpret_cast<const char*>(st2); rg.dst[2] = reinterpret_cast<char*>(st2c);
+      rg.sstride[2] = (long long)L * 8; rg.bytes[2] = 8;
+      MEC_TRY(launch_gather_rows(rg, B, s));
+      g.A = h16; g.B = wqkv + (size_t)BH * BH; g.bias = bqkv + BH; g.C16 = big16; g.M = M; g.N = 2 * BH; g.K = BH;
+      MEC_TRY(launch_gemm(g, s, &prof, TAG_NONE));  // K | V [M, 1536]
+      g = GemmParams();
+      g.A = h16c; g.B = wqkv; g.bias = bqkv; g.C16 = qc; g.M = B; g.N = BH; g.K = BH;
+      MEC_TRY(launch_gemm(g, s, &prof, TAG_NONE));  // Q of the [CLS] rows
+      hipLaunchKernelGGL(bert_attention_cls_kernel, dim3(B * BHEADS), dim3(256), 0, s, big16, mask, qc, ctxc);
+      MEC_LAUNCH_CHECK();
+      g = GemmParams();
+      g.A = ctxc; g.B = wo; g.bias = bo; g.R = h32c; g.r_f32 = 1; g.r_stats = st2c; g.r_g = pg2; g.r_b = pg2 + BH;
+      g.C32 = t32c; g.M = B; g.N = BH; g.K = BH;
+      MEC_TRY(launch_gemm(g, s, &prof, TAG_NONE));
+      launch_ln_rows(t32c, B, g1, b1, nullptr, h16c, st1c, s);
+      MEC_LAUNCH_CHECK();
+      g = GemmParams();
+      g.A = h16c; g.B = wi; g.bias = bi; g.act = ACT_GELU; g.C16 = fc; g.M = B; g.N = BI; g.K = BH;
+      MEC_TRY(launch_gemm(g, s, &prof, TAG_NONE));
+      g = GemmParams();
+      g.A = fc; g.B = wo2; g.bias = bo2; g.R = t32c; g.r_f32 = 1; g.r_stats = st1c; g.r_g = g1; g.r_b = b1;
+      g.C32 = h32c; g.M = B; g.N = BH; g.K = BI;
+      MEC_TRY(launch_gemm(g, s, &prof, TAG_NONE));
+      launch_ln_rows(h32c, B, g2, b2, h32c, h16c, st2c, s);  // in place, written in full (the pooler's input)
+      MEC_LAUNCH_CHECK();
+      break;
+    }
     if (opt().bert_qkv_attn) {
       MEC_TRY(prof.begin(TAG_BERT_ATTN, s));
 #ifdef MEC_PROBES
@@ -833,7 +954,9 @@ int TextModel::forward(const int32_t* ids, const int32_t* mask, int B, int L, fl
   const float* head = P + PRM_LAYER * BLAYERS;
   const float *WpT = head, *bp = WpT + (size_t)BH * BH, *WcT = bp + BH, *bc = WcT + (size_t)BH * 7;
   // pooler: tanh(cls . Wp^T + bp) over the batch (also copies the CLS feature out)
-  MEC_TRY(launch_linear_mfma<BACT_TANH>(h32, (size_t)L * BH, B, BH, WpT, bp, BH, pooled, BH, cls, BH, s));
+  const bool compact = cls_last && BLAYERS > 1;
+  MEC_TRY(launch_linear_mfma<BACT_TANH>(compact ? h32c : h32, compact ? (size_t)BH : (size_t)L * BH, B, BH, WpT, bp,
+                                        BH, pooled, BH, cls, BH, s));
   MEC_TRY(launch_head7(pooled, B, BH, WcT, bc, logits, probs, s));
   return 0;
 }

@@ -34,24 +34,29 @@ __device__ __forceinline__ int kswz(int row, int c) { return c ^ (row & 15); }
 // score tile left them (two keys per MFMA: key f(e) + 4h of block t for lane half h).
 // SPLIT (fp32x3 path): ctx is written as f16 hi / lo planes (ctx16, ctx16 + lo) for the split
 // O-projection GEMM instead of f32.
-template <int SPLIT = 0>
+// CLS = 1 (the last layer with bert_cls_last): qkv holds K | V only ([B*128, 1536]), the [CLS] query
+// row comes from qc ([B, 768]) and the context is written compact ([B, 768]); wave 0 computes
+// queries 0..31 with Q zero for all but query 0 (an MFMA output column depends only on its own B
+// column: the [CLS] context has the full kernel's bits), waves 1-3 only stage K and V.
+template <int SPLIT = 0, int CLS = 0>
 __global__ __launch_bounds__(256, 2) void bert_attention_f32_kernel(const float* __restrict__ qkv,
                                                                     const int32_t* __restrict__ mask,
                                                                     float* __restrict__ ctx, f16* __restrict__ ctx16,
-                                                                    long long lo) {
+                                                                    long long lo, const float* __restrict__ qc) {
+  constexpr int LD = CLS ? 2 * H : 3 * H, KO = CLS ? 0 : H;
   __shared__ __attribute__((aligned(16))) float sK[AL * DH];
   __shared__ __attribute__((aligned(16))) float sV[AL * DH];
   __shared__ float sBias[AL];
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   const int b = blockIdx.x / NH, h = blockIdx.x - (blockIdx.x / NH) * NH;
-  const float* base = qkv + (size_t)b * AL * (3 * H) + h * DH;
+  const float* base = qkv + (size_t)b * AL * LD + h * DH;
 #pragma unroll
   for (int i = 0; i < 8; ++i) {
     const int c = tid + 256 * i;
     const int row = c >> 4, kc = c & 15;
-    const float* src = base + (size_t)row * (3 * H) + kc * 4;
-    const float4 k = *reinterpret_cast<const float4*>(src + H);
-    const float4 v = *reinterpret_cast<const float4*>(src + 2 * H);
+    const float* src = base + (size_t)row * LD + kc * 4;
+    const float4 k = *reinterpret_cast<const float4*>(src + KO);
+    const float4 v = *reinterpret_cast<const float4*>(src + KO + H);
     *reinterpret_cast<float4*>(sK + row * DH + kswz(row, kc) * 4) = k;
     *reinterpret_cast<float4*>(sV + row * DH + kc * 4) = v;
   }
@@ -59,9 +64,18 @@ __global__ __launch_bounds__(256, 2) void bert_attention_f32_kernel(const float*
   const int lr = lane & 31, lh = lane >> 5;
   const int q = 32 * wave + lr;
   float4 qf[8];  // Q[q][8s + 4lh .. +3]
+  if constexpr (CLS) {
+    const bool own = wave == 0 && lr == 0;
+    const float* qrow = qc + (size_t)b * H + h * DH;
 #pragma unroll
-  for (int s = 0; s < 8; ++s) qf[s] = *reinterpret_cast<const float4*>(base + (size_t)q * (3 * H) + (2 * s + lh) * 4);
+    for (int s = 0; s < 8; ++s)
+      qf[s] = own ? *reinterpret_cast<const float4*>(qrow + (2 * s + lh) * 4) : make_float4(0.f, 0.f, 0.f, 0.f);
+  } else {
+#pragma unroll
+    for (int s = 0; s < 8; ++s) qf[s] = *reinterpret_cast<const float4*>(base + (size_t)q * LD + (2 * s + lh) * 4);
+  }
   __syncthreads();
+  if (CLS && wave != 0) return;
 
   floatx16 st[4];  // st[t][e] = S[q][key 32t + (e&3) + 8(e>>2) + 4lh]
 #pragma unroll
@@ -116,7 +130,8 @@ __global__ __launch_bounds__(256, 2) void bert_attention_f32_kernel(const float*
 #pragma unroll
       for (int u = 0; u < 2; ++u) o[u] = __builtin_amdgcn_mfma_f32_32x32x2f32(sV[key * DH + 32 * u + lr], p, o[u], 0, 0, 0);
     }
-  const size_t obase = ((size_t)b * AL + q) * H + h * DH;
+  if (CLS && lr != 0) return;
+  const size_t obase = ((size_t)b * (CLS ? 1 : AL) + q) * H + h * DH;
 #pragma unroll
   for (int u = 0; u < 2; ++u)
 #pragma unroll
@@ -142,15 +157,22 @@ int TextModel::forward_f32(const int32_t* ids, const int32_t* mask, int B, int L
                            float* probs, hipStream_t s) {
   MEC_REQUIRE(wts32.p, "text: fp32 weights missing (handle created at f16 precision)");
   const int M = B * L;
-  // workspace: h32 | t32 | ctx32 (f32 [M,768]) ; big32 f32 [M,3072] (qkv [M,2304], then FFN) ; pooled [B,768]
-  const size_t need = (size_t)M * H * 4 * 3 + (size_t)M * FF * 4 + (size_t)B * H * 4;
+  // workspace: h32 | t32 | ctx32 (f32 [M,768]) ; big32 f32 [M,3072] (qkv [M,2304], then FFN) ; pooled [B,768] ;
+  // the [CLS]-row buffers of the last layer (bert_cls_last): h32c | t32c | qc | ctxc [B,768], fc [B,3072]
+  const size_t need = (size_t)M * H * 4 * 3 + (size_t)M * FF * 4 + (size_t)B * H * 4 * 5 + (size_t)B * FF * 4;
   if (ws.bytes < need) MEC_TRY(ws.ensure(need));
   char* p = ws.as<char>();
   float* h32 = reinterpret_cast<float*>(p); p += (size_t)M * H * 4;
   float* t32 = reinterpret_cast<float*>(p); p += (size_t)M * H * 4;
   float* ctx32 = reinterpret_cast<float*>(p); p += (size_t)M * H * 4;
   float* big32 = reinterpret_cast<float*>(p); p += (size_t)M * FF * 4;
-  float* pooled = reinterpret_cast<float*>(p);
+  float* pooled = reinterpret_cast<float*>(p); p += (size_t)B * H * 4;
+  float* h32c = reinterpret_cast<float*>(p); p += (size_t)B * H * 4;
+  float* t32c = reinterpret_cast<float*>(p); p += (size_t)B * H * 4;
+  float* qc = reinterpret_cast<float*>(p); p += (size_t)B * H * 4;
+  float* ctxc = reinterpret_cast<float*>(p); p += (size_t)B * H * 4;
+  float* fc = reinterpret_cast<float*>(p);
+  const bool cls_last = opt().bert_cls_last != 0;
 
   MEC_TRY(launch_bert_embed_ln(ids, M, L, emb.as<float>(), h32, nullptr, s));
   const float* W = wts32.as<float>();
@@ -164,10 +186,39 @@ int TextModel::forward_f32(const int32_t* ids, const int32_t* mask, int B, int L
     const float *bqkv = pl, *bo = pl + 2304, *g1 = pl + 3072, *b1 = pl + 3840, *bi = pl + 4608, *bo2 = pl + 7680,
                 *g2 = pl + 8448, *b2 = pl + 9216;
     GemmParams g;
+    if (cls_last && l == NL - 1) {
+      // [CLS]-only last layer (TextModel::forward): K / V for every token, the rest on the [CLS] rows
+      RowGather rg{};
+      rg.n = 1;
+      rg.src[0] = reinterpret_cast<const char*>(h32); rg.dst[0] = reinterpret_cast<char*>(h32c);
+      rg.sstride[0] = (long long)AL * H * 4; rg.bytes[0] = H * 4;
+      MEC_TRY(launch_gather_rows(rg, B, s));
+      g.A = h32; g.B32 = wqkv + (size_t)H * H; g.bias = bqkv + H; g.C32 = big32; g.M = M; g.N = 2 * H; g.K = H;
+      MEC_TRY(launch_gemm_f32(g, s, &prof, TAG_NONE));  // K | V [M, 1536]
+      g = GemmParams();
+      g.A = h32c; g.B32 = wqkv; g.bias = bqkv; g.C32 = qc; g.M = B; g.N = H; g.K = H;
+      MEC_TRY(launch_gemm_f32(g, s, &prof, TAG_NONE));  // Q of the [CLS] rows
+      hipLaunchKernelGGL((bert_attention_f32_kernel<0, 1>), dim3(B * NH), dim3(256), 0, s, big32, mask, ctxc, nullptr,
+                         0LL, qc);
+      MEC_LAUNCH_CHECK();
+      g = GemmParams();
+      g.A = ctxc; g.B32 = wo; g.bias = bo; g.R = h32c; g.r_f32 = 1; g.C32 = t32c; g.M = B; g.N = H; g.K = H;
+      MEC_TRY(launch_gemm_f32(g, s, &prof, TAG_NONE));
+      MEC_TRY(launch_bert_layernorm(t32c, B, g1, b1, h32c, nullptr, nullptr, s));
+      g = GemmParams();
+      g.A = h32c; g.B32 = wi; g.bias = bi; g.act = ACT_GELU_EXACT; g.C32 = fc; g.M = B; g.N = FF; g.K = H;
+      MEC_TRY(launch_gemm_f32(g, s, &prof, TAG_NONE));
+      g = GemmParams();
+      g.A = fc; g.B32 = wo2; g.bias = bo2; g.R = h32c; g.r_f32 = 1; g.C32 = t32c; g.M = B; g.N = H; g.K = FF;
+      MEC_TRY(launch_gemm_f32(g, s, &prof, TAG_NONE));
+      MEC_TRY(launch_bert_layernorm(t32c, B, g2, b2, h32c, nullptr, nullptr, s));
+      break;
+    }
     g.A = h32; g.B32 = wqkv; g.bias = bqkv; g.C32 = big32; g.M = M; g.N = 2304; g.K = H;
     MEC_TRY(launch_gemm_f32(g, s, &prof, TAG_BERT_QKV));
     MEC_TRY(prof.begin(TAG_BERT_ATTN, s));
-    hipLaunchKernelGGL(bert_attention_f32_kernel<0>, dim3(B * NH), dim3(256), 0, s, big32, mask, ctx32, nullptr, 0LL);
+    hipLaunchKernelGGL((bert_attention_f32_kernel<0, 0>), dim3(B * NH), dim3(256), 0, s, big32, mask, ctx32, nullptr, 0LL,
+                       nullptr);
     MEC_LAUNCH_CHECK();
     MEC_TRY(prof.end(TAG_BERT_ATTN, s));
     g = GemmParams();
@@ -188,7 +239,8 @@ int TextModel::forward_f32(const int32_t* ids, const int32_t* mask, int B, int L
   }
   const float* head = P + PRM_LAYER * NL;
   const float *WpT = head, *bp = WpT + (size_t)H * H, *WcT = bp + H, *bc = WcT + (size_t)H * 7;
-  MEC_TRY(launch_linear_mfma<BACT_TANH>(h32, (size_t)L * H, B, H, WpT, bp, H, pooled, H, cls, H, s));
+  MEC_TRY(launch_linear_mfma<BACT_TANH>(cls_last ? h32c : h32, cls_last ? (size_t)H : (size_t)L * H, B, H, WpT, bp,
+                                        H, pooled, H, cls, H, s));
   MEC_TRY(launch_head7(pooled, B, H, WcT, bc, logits, probs, s));
   return 0;
 }
@@ -210,7 +262,11 @@ int TextModel::forward_x3(const int32_t* ids, const int32_t* mask, int B, int L,
   const long long MH = (long long)M * H, MF = (long long)M * FF;
   // workspace: h32 | t32 (f32 [M,768]) ; h hi|lo, ctx hi|lo (f16 2x[M,768]) ; big: qkv hi|lo
   // (f16 2x[M,2304]), then the FFN intermediate hi|lo (f16 2x[M,3072]) ; pooled [B,768]
-  const size_t need = (size_t)MH * 4 * 2 + (size_t)MH * 2 * 4 + (size_t)MF * 4 + (size_t)B * H * 4;
+  // + the [CLS]-row buffers of the last layer (bert_cls_last): h32c | t32c (f32 [B,768]) ; hsc | qsc | csc
+  // (f16 planes 2x[B,768]) ; fsc (f16 planes 2x[B,3072])
+  const long long BHc = (long long)B * H, BFc = (long long)B * FF;
+  const size_t need = (size_t)MH * 4 * 2 + (size_t)MH * 2 * 4 + (size_t)MF * 4 + (size_t)B * H * 4 +
+                      (size_t)BHc * 4 * 2 + (size_t)BHc * 4 * 3 + (size_t)BFc * 4;
   if (ws.bytes < need) MEC_TRY(ws.ensure(need));
   char* p = ws.as<char>();
   float* h32 = reinterpret_cast<float*>(p); p += (size_t)MH * 4;
@@ -219,7 +275,14 @@ int TextModel::forward_x3(const int32_t* ids, const int32_t* mask, int B, int L,
   f16* cs = reinterpret_cast<f16*>(p); p += (size_t)MH * 2 * 2;
   float* big32 = reinterpret_cast<float*>(p);
   f16* bigs = reinterpret_cast<f16*>(p); p += (size_t)MF * 4;
-  float* pooled = reinterpret_cast<float*>(p);
+  float* pooled = reinterpret_cast<float*>(p); p += (size_t)B * H * 4;
+  float* h32c = reinterpret_cast<float*>(p); p += (size_t)BHc * 4;
+  float* t32c = reinterpret_cast<float*>(p); p += (size_t)BHc * 4;
+  f16* hsc = reinterpret_cast<f16*>(p); p += (size_t)BHc * 4;
+  f16* qsc = reinterpret_cast<f16*>(p); p += (size_t)BHc * 4;
+  f16* csc = reinterpret_cast<f16*>(p); p += (size_t)BHc * 4;
+  f16* fsc = reinterpret_cast<f16*>(p);
+  const bool cls_last = opt().bert_cls_last != 0;
 
   MEC_TRY(launch_bert_embed_ln(ids, M, L, emb.as<float>(), h32, hs, s, MH));
   const f16* W = wts.as<f16>();
@@ -235,6 +298,42 @@ int TextModel::forward_x3(const int32_t* ids, const int32_t* mask, int B, int L,
     const float *bqkv = pl, *bo = pl + 2304, *g1 = pl + 3072, *b1 = pl + 3840, *bi = pl + 4608, *bo2 = pl + 7680,
                 *g2 = pl + 8448, *b2 = pl + 9216;
     GemmParams g;
+    if (cls_last && l == NL - 1) {
+      // [CLS]-only last layer (TextModel::forward): K / V for every token, the rest on the [CLS] rows
+      RowGather rg{};
+      rg.n = 3;
+      rg.src[0] = reinterpret_cast<const char*>(h32); rg.dst[0] = reinterpret_cast<char*>(h32c);
+      rg.sstride[0] = (long long)AL * H * 4; rg.bytes[0] = H * 4;
+      rg.src[1] = reinterpret_cast<const char*>(hs); rg.dst[1] = reinterpret_cast<char*>(hsc);
+      rg.sstride[1] = (long long)AL * H * 2; rg.bytes[1] = H * 2;
+      rg.src[2] = reinterpret_cast<const char*>(hs + MH); rg.dst[2] = reinterpret_cast<char*>(hsc + BHc);
+      rg.sstride[2] = (long long)AL * H * 2; rg.bytes[2] = H * 2;
+      MEC_TRY(launch_gather_rows(rg, B, s));
+      const long long kvlo = (long long)M * 2 * H;
+      g.split = 1; g.A = hs; g.a_lo = MH; g.B = wqkv + (size_t)H * H; g.b_lo = wlo; g.oscale = sc[0];
+      g.bias = bqkv + H; g.C16 = bigs; g.c_lo = kvlo; g.M = M; g.N = 2 * H; g.K = H;
+      MEC_TRY(launch_gemm(g, s, &prof, TAG_NONE));  // K | V planes [M, 1536]
+      g = GemmParams();
+      g.split = 1; g.A = hsc; g.a_lo = BHc; g.B = wqkv; g.b_lo = wlo; g.oscale = sc[0];
+      g.bias = bqkv; g.C16 = qsc; g.c_lo = BHc; g.M = B; g.N = H; g.K = H;
+      MEC_TRY(launch_gemm(g, s, &prof, TAG_NONE));  // Q planes of the [CLS] rows
+      MEC_TRY(launch_bert_attention_x3_cls(bigs, kvlo, mask, qsc, BHc, csc, BHc, B, s));
+      g = GemmParams();
+      g.split = 1; g.A = csc; g.a_lo = BHc; g.B = wo; g.b_lo = wlo; g.oscale = sc[1];
+      g.bias = bo; g.R = h32c; g.r_f32 = 1; g.C32 = t32c; g.M = B; g.N = H; g.K = H;
+      MEC_TRY(launch_gemm(g, s, &prof, TAG_NONE));
+      MEC_TRY(launch_bert_layernorm(t32c, B, g1, b1, h32c, hsc, nullptr, s, BHc));
+      g = GemmParams();
+      g.split = 1; g.A = hsc; g.a_lo = BHc; g.B = wi; g.b_lo = wlo; g.oscale = sc[2];
+      g.bias = bi; g.act = ACT_GELU_EXACT; g.C16 = fsc; g.c_lo = BFc; g.M = B; g.N = FF; g.K = H;
+      MEC_TRY(launch_gemm(g, s, &prof, TAG_NONE));
+      g = GemmParams();
+      g.split = 1; g.A = fsc; g.a_lo = BFc; g.B = wo2; g.b_lo = wlo; g.oscale = sc[3];
+      g.bias = bo2; g.R = h32c; g.r_f32 = 1; g.C32 = t32c; g.M = B; g.N = H; g.K = FF;
+      MEC_TRY(launch_gemm(g, s, &prof, TAG_NONE));
+      MEC_TRY(launch_bert_layernorm(t32c, B, g2, b2, h32c, hsc, nullptr, s, BHc));
+      break;
+    }
     g.split = 1; g.A = hs; g.a_lo = MH; g.B = wqkv; g.b_lo = wlo; g.oscale = sc[0];
     g.bias = bqkv; g.C16 = bigs; g.c_lo = (long long)M * 2304; g.M = M; g.N = 2304; g.K = H;
     MEC_TRY(launch_gemm(g, s, &prof, TAG_BERT_QKV));
@@ -262,7 +361,8 @@ int TextModel::forward_x3(const int32_t* ids, const int32_t* mask, int B, int L,
   }
   const float* head = P + PRM_LAYER * NL;
   const float *WpT = head, *bp = WpT + (size_t)H * H, *WcT = bp + H, *bc = WcT + (size_t)H * 7;
-  MEC_TRY(launch_linear_mfma<BACT_TANH>(h32, (size_t)L * H, B, H, WpT, bp, H, pooled, H, cls, H, s));
+  MEC_TRY(launch_linear_mfma<BACT_TANH>(cls_last ? h32c : h32, cls_last ? (size_t)H : (size_t)L * H, B, H, WpT, bp,
+                                        H, pooled, H, cls, H, s));
   MEC_TRY(launch_head7(pooled, B, H, WcT, bc, logits, probs, s));
   return 0;
 }

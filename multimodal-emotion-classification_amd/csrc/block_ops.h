@@ -394,4 +394,32 @@ __global__ __launch_bounds__(256) static __attribute__((unused)) void avgpool_f3
   y[(size_t)b * C + c] = s / (float)HW;
 }
 
+// Row gather of up to four arrays in one launch: row b of array i is copied from
+// src[i] + b * sstride[i] to dst[i] + b * bytes[i] (bytes % 4 == 0). BERT's last layer runs on the
+// [CLS] rows only (bert_cls_last): this packs those rows of the residual stream / GEMM operand
+// planes / LayerNorm stats into dense [B, .] buffers. Grid B, 256 threads.
+struct RowGather {
+  const char* src[4];
+  char* dst[4];
+  long long sstride[4];
+  int bytes[4];
+  int n;
+};
+__global__ __launch_bounds__(256) static __attribute__((unused)) void gather_rows_kernel(const RowGather g) {
+  const int b = blockIdx.x;
+  for (int i = 0; i < g.n; ++i) {
+    const uint32_t* s = reinterpret_cast<const uint32_t*>(g.src[i] + (size_t)b * g.sstride[i]);
+    uint32_t* d = reinterpret_cast<uint32_t*>(g.dst[i] + (size_t)b * g.bytes[i]);
+    for (int w = threadIdx.x; w < g.bytes[i] / 4; w += 256) d[w] = s[w];
+  }
+}
+static inline int launch_gather_rows(const RowGather& g, int B, hipStream_t s) {
+  MEC_REQUIRE(g.n >= 1 && g.n <= 4, "gather_rows: 1..4 arrays");
+  for (int i = 0; i < g.n; ++i) MEC_REQUIRE(g.bytes[i] % 4 == 0 && g.sstride[i] % 4 == 0, "gather_rows: 4-B rows");
+  if (B <= 0) return 0;
+  hipLaunchKernelGGL(gather_rows_kernel, dim3(B), dim3(256), 0, s, g);
+  MEC_LAUNCH_CHECK();
+  return 0;
+}
+
 }  // namespace mec

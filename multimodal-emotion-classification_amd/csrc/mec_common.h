@@ -95,6 +95,11 @@ struct Options {
   int pw_chain_form = 0;
   int bert_qkv_attn = 1;    // fused BERT QKV projection + attention
   int bert_ln_rows = 2;     // BERT LayerNorm rows per wave (1 | 2 | 4): 27.0 / 25.7 / 26.3 us at B = 256
+  // BERT's last layer on the [CLS] rows only (the outputs -- pooler, logits, CLS feature -- read
+  // nothing else of it): K / V for every token, Q, attention, O-projection, LayerNorms and FFN for
+  // the B [CLS] rows. Same bits as the full layer (every kernel is row-independent; the attention
+  // computes the [CLS] query with the full kernel's instruction sequence). 0 = the full layer
+  int bert_cls_last = 1;
   int mbv2_impl = 0;
   // ping-pong GEMM tile order inside each XCD's contiguous tile range: 0 = row-major (all N
   // panels of one M panel in turn), G = groups of G M panels walked M-fastest, so the 32

@@ -106,6 +106,10 @@ int launch_bert_layernorm(const float* x, int M, const float* g, const float* b,
 // written as hi / lo planes [B*128, 768] (lo at ctx + clo)
 int launch_bert_attention_x3(const f16* qkv, long long lo, const int32_t* mask, f16* ctx, long long clo, int B,
                              hipStream_t s);
+// its [CLS]-only form (bert_cls_last): K | V planes [B*128, 1536] (lo at kv + lo), the [CLS] query
+// planes [B, 768] (lo at qc + qclo), the [CLS] context planes [B, 768] (lo at ctx + clo)
+int launch_bert_attention_x3_cls(const f16* kv, long long lo, const int32_t* mask, const f16* qc, long long qclo,
+                                 f16* ctx, long long clo, int B, hipStream_t s);
 
 // Split n fp32 weights into f16 planes for the fp32x3 path: hi = f16(w 2^e), lo = f16(w 2^e - hi)
 // with e the largest power of two keeping max |w| 2^e <= 2^14 (so hi never overflows and lo
