@@ -78,7 +78,8 @@ def tile_name(tile: int, M: int) -> str:
         return f'gemm tile {tile}'
     mf = 32 if v == 0 else 16
     bk = 32 if v >= 2 else 64
-    return f'gemm_glds_kernel<{bm}x{bn}x{bk}, mfma{mf}> grid={((M + bm - 1) // bm) * (3072 // bn)}'
+    x3i = ' K-interleaved split terms' if v == 7 else ''
+    return f'gemm_glds_kernel<{bm}x{bn}x{bk}, mfma{mf}{x3i}> grid={((M + bm - 1) // bm) * (3072 // bn)}'
 
 
 def tile_name_f32(tile: int, M: int) -> str:
@@ -405,12 +406,14 @@ def run(a, precision, B, world, rank, dev, inputs):
     iso = ffn_flop / ((iso_ms / max(iso_n, 1)) / 1e3) / 1e12 if iso_n else None
     tile = pipe.text.gemm_tile(M, 3072, 768)  # the text handle's own autotune choice
     if precision == 'fp32x3' and not tile:
-        tile = 10256  # the split FFN1 is pinned, never autotuned (csrc/gemm.hip: launch_gemm)
+        # the split FFN1 is pinned, never autotuned (csrc/gemm.hip: launch_gemm): 70256 at the default
+        # K-interleaved term order (gemm_x3_order 1), 10256 at the pass-major order
+        tile = 70256
     if precision == 'f16':
         kname = tile_name(tile, M) + ' + GELU'
         ebytes, tfile = 2, 'ffn1_traffic.json'
     elif precision == 'fp32x3':
-        kname = tile_name(tile, M) + ' split-f16 (3 K passes) + erf-GELU, hi/lo f16 out'
+        kname = tile_name(tile, M) + ' split-f16 (hi.hi + hi.lo + lo.hi) + erf-GELU, hi/lo f16 out'
         ebytes, tfile = 4, 'ffn1_x3_traffic.json'
     else:
         kname = tile_name_f32(tile, M) + ' + erf-GELU'

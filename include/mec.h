@@ -145,7 +145,8 @@ int mec_conv_f32(const float* x, const float* w, const float* bias, const float*
  * each other: mec_model_set_option sets one handle's knob; mec_set_option sets the process
  * default that handles created AFTERWARDS copy (and that the handle-less kernel entry points
  * use). Every pair of settings of one knob gives bit-identical outputs, except "fusion_r" 4 vs
- * 1|2 and "conv3x3_halo" 0 vs 1 (fp32 reassociation, both within the oracle tolerance).
+ * 1|2, "conv3x3_halo" 0 vs 1 and "gemm_x3_order" 0 vs 1 (fp32 reassociation, all within the
+ * oracle tolerance).
  *   "gemm_bn" [0]|id       force one f16 GEMM tile (0 = autotune), "gemm_autotune" 0|[1]
  *   "gemm_bn_tag" tag*100000+id   force a tile for one launch class (e.g. 3 = BERT O-proj)
  *   "gemm_f32_tile" [0]|1..8  force one fp32 GEMM tile (0 = autotune; 5..8 = 1..4 on 16x16x4)
@@ -156,6 +157,10 @@ int mec_conv_f32(const float* x, const float* w, const float* bias, const float*
  *   "gemm_group_m" 0|2|4|[8]|16  ping-pong GEMM tile order inside each XCD's tile range (0: row-major,
  *                          G: G-panel groups of M walked M-fastest, fewer weight re-fetches)
  *   "gemm_glds_group_m" 0|2|4|[8]|16  the same tile order for the multi-stage GEMM engine
+ *   "gemm_x3_order" 0|[1]  split-f16 (fp32x3) GEMM term order: 0 = pass-major (K for lo.hi, then
+ *                          hi.lo, then hi.hi), 1 = K-interleaved (each 32-deep k chunk's three terms
+ *                          back to back, 16x16x32 tiles 70256 / 70128 / 71128 / 71064 / 70064 only);
+ *                          both fp32-accurate, not the same bits
  *   "conv3x3_direct" 0|[1] layer1 3x3 conv on the halo-tile kernel (mec_conv_f16 too)
  *   "conv3x3_halo" 0|[1]   layers 2-3 stride-1 3x3 convs on the halo kernel (mec_conv_f16 too;
  *                          fp32 accumulation in another order: not bit-identical to 0)

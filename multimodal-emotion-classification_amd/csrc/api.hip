@@ -285,6 +285,7 @@ int set_option(Options& o, const std::string& k, int value) {
     return 0;
   }
   if (k == "bert_cls_last" && (value == 0 || value == 1)) { o.bert_cls_last = value; return 0; }
+  if (k == "gemm_x3_order" && (value == 0 || value == 1)) { o.gemm_x3_order = value; return 0; }
   if (k == "bert_ln_rows" && (value == 1 || value == 2 || value == 4)) {
     o.bert_ln_rows = value;
     return 0;
@@ -338,7 +339,8 @@ int set_option(Options& o, const std::string& k, int value) {
   auto tile_ok = [](int id) {
     const int v = id % 10000;
     const bool deep = id == 20256 || id == 30256 || id == 20128 || id == 40256 || id == 41256 || id == 50128 ||
-                      id == 60128 || id == 50256;
+                      id == 60128 || id == 50256 || id == 70256 || id == 70128 || id == 71128 || id == 71064 ||
+                      id == 70064;
     return id == 0 || deep || (id < 20000 && (v == 64 || v == 128 || v == 256 || v == 1064 || v == 1128));
   };
   if (k == "gemm_bn" && tile_ok(value)) {

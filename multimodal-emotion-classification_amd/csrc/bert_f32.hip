@@ -250,11 +250,11 @@ int TextModel::forward_f32(const int32_t* ids, const int32_t* mask, int B, int L
 //   qkv hi/lo   = [h_hi|h_lo] . [Wqkv_hi|Wqkv_lo]^T 2^-e + b        split GEMM, split out
 //   ctx hi/lo   = softmax(QK^T/8 + mask_bias) V                     bert_attention_x3_kernel (split
 //                                                                    MFMA products, fp32 softmax)
-//   t32         = ctx . Wo^T 2^-e + bo + h32                        split GEMM, f32 residual
-//   h32, h hi/lo = LN(t32)                                          bert_layernorm_kernel (lo plane)
+//   t32         = ctx . Wo^T 2^-e + bo + LN2'(h32)                  split GEMM, f32 residual (deferred LN)
+//   h hi/lo, st1 = LN(t32)                                          bert_layernorm_kernel (lo plane, stats)
 //   i hi/lo     = GELU(h . Wi^T 2^-e + bi)                          split GEMM, exact erf, split out
-//   t32         = i . Wo2^T 2^-e + bo2 + h32                        split GEMM
-//   h32, h hi/lo = LN(t32)
+//   h32         = i . Wo2^T 2^-e + bo2 + LN1'(t32)                  split GEMM (deferred LN)
+//   h hi/lo, st2 = LN(h32)
 int TextModel::forward_x3(const int32_t* ids, const int32_t* mask, int B, int L, float* cls, float* logits,
                           float* probs, hipStream_t s) {
   MEC_REQUIRE(wts.p && x3_lo && x3_scale.size() == 4 * NL, "text: fp32x3 weights missing");
@@ -265,8 +265,9 @@ int TextModel::forward_x3(const int32_t* ids, const int32_t* mask, int B, int L,
   // + the [CLS]-row buffers of the last layer (bert_cls_last): h32c | t32c (f32 [B,768]) ; hsc | qsc | csc
   // (f16 planes 2x[B,768]) ; fsc (f16 planes 2x[B,3072])
   const long long BHc = (long long)B * H, BFc = (long long)B * FF;
+  // + the LayerNorm row stats st1 | st2 ([M] float2; deferred LayerNorm, below) and st2c ([B] float2)
   const size_t need = (size_t)MH * 4 * 2 + (size_t)MH * 2 * 4 + (size_t)MF * 4 + (size_t)B * H * 4 +
-                      (size_t)BHc * 4 * 2 + (size_t)BHc * 4 * 3 + (size_t)BFc * 4;
+                      (size_t)BHc * 4 * 2 + (size_t)BHc * 4 * 3 + (size_t)BFc * 4 + (size_t)M * 8 * 2 + (size_t)B * 8;
   if (ws.bytes < need) MEC_TRY(ws.ensure(need));
   char* p = ws.as<char>();
   float* h32 = reinterpret_cast<float*>(p); p += (size_t)MH * 4;
@@ -281,7 +282,10 @@ int TextModel::forward_x3(const int32_t* ids, const int32_t* mask, int B, int L,
   f16* hsc = reinterpret_cast<f16*>(p); p += (size_t)BHc * 4;
   f16* qsc = reinterpret_cast<f16*>(p); p += (size_t)BHc * 4;
   f16* csc = reinterpret_cast<f16*>(p); p += (size_t)BHc * 4;
-  f16* fsc = reinterpret_cast<f16*>(p);
+  f16* fsc = reinterpret_cast<f16*>(p); p += (size_t)BFc * 4;
+  float2* st1 = reinterpret_cast<float2*>(p);  // LN1 row stats [M]
+  float2* st2 = st1 + M;                       // LN2 row stats [M]
+  float2* st2c = st2 + M;                      // LN2 row stats of the [CLS] rows [B]
   const bool cls_last = opt().bert_cls_last != 0;
 
   MEC_TRY(launch_bert_embed_ln(ids, M, L, emb.as<float>(), h32, hs, s, MH));
@@ -308,7 +312,13 @@ int TextModel::forward_x3(const int32_t* ids, const int32_t* mask, int B, int L,
       rg.sstride[1] = (long long)AL * H * 2; rg.bytes[1] = H * 2;
       rg.src[2] = reinterpret_cast<const char*>(hs + MH); rg.dst[2] = reinterpret_cast<char*>(hsc + BHc);
       rg.sstride[2] = (long long)AL * H * 2; rg.bytes[2] = H * 2;
+      if (l > 0) {  // h32 holds layer l-1's pre-LN2 sum (deferred LayerNorm): its stats too
+        rg.n = 4;
+        rg.src[3] = reinterpret_cast<const char*>(st2); rg.dst[3] = reinterpret_cast<char*>(st2c);
+        rg.sstride[3] = (long long)AL * 8; rg.bytes[3] = 8;
+      }
       MEC_TRY(launch_gather_rows(rg, B, s));
+      const float* pg2 = P + PRM_LAYER * (l - 1) + 8448;  // layer l-1's LN2 (g2, b2)
       const long long kvlo = (long long)M * 2 * H;
       g.split = 1; g.A = hs; g.a_lo = MH; g.B = wqkv + (size_t)H * H; g.b_lo = wlo; g.oscale = sc[0];
       g.bias = bqkv + H; g.C16 = bigs; g.c_lo = kvlo; g.M = M; g.N = 2 * H; g.K = H;
@@ -321,6 +331,7 @@ int TextModel::forward_x3(const int32_t* ids, const int32_t* mask, int B, int L,
       g = GemmParams();
       g.split = 1; g.A = csc; g.a_lo = BHc; g.B = wo; g.b_lo = wlo; g.oscale = sc[1];
       g.bias = bo; g.R = h32c; g.r_f32 = 1; g.C32 = t32c; g.M = B; g.N = H; g.K = H;
+      if (l > 0) { g.r_stats = st2c; g.r_g = pg2; g.r_b = pg2 + H; }
       MEC_TRY(launch_gemm(g, s, &prof, TAG_NONE));
       MEC_TRY(launch_bert_layernorm(t32c, B, g1, b1, h32c, hsc, nullptr, s, BHc));
       g = GemmParams();
@@ -340,12 +351,20 @@ int TextModel::forward_x3(const int32_t* ids, const int32_t* mask, int B, int L,
     MEC_TRY(prof.begin(TAG_BERT_ATTN, s));
     MEC_TRY(launch_bert_attention_x3(bigs, (long long)M * 2304, mask, cs, MH, B, s));
     MEC_TRY(prof.end(TAG_BERT_ATTN, s));
+    // deferred LayerNorm (as on the f16 path): the LN kernels write the GEMM operand planes and the
+    // row (mean, rstd) only; the f32 LN output is needed only as the next residual, which the
+    // O-proj / FFN2 epilogue re-derives from the pre-LN sum with the LN kernel's own expression
+    // (GemmParams::r_stats): same bits, two 100-MB f32 writes per layer fewer at B = 256. The f32
+    // stream ping-pongs (O-proj h32 -> t32, FFN2 t32 -> h32) so no GEMM reads its own output.
+    const bool first = l == 0, last = l == NL - 1;
+    const float* pg2 = P + PRM_LAYER * (l - 1) + 8448;  // layer l-1's LN2 (g2, b2)
     g = GemmParams();
     g.split = 1; g.A = cs; g.a_lo = MH; g.B = wo; g.b_lo = wlo; g.oscale = sc[1];
     g.bias = bo; g.R = h32; g.r_f32 = 1; g.C32 = t32; g.M = M; g.N = H; g.K = H;
+    if (!first) { g.r_stats = st2; g.r_g = pg2; g.r_b = pg2 + H; }  // else: the embedding LN, written in full
     MEC_TRY(launch_gemm(g, s, &prof, TAG_BERT_OPROJ));
     MEC_TRY(prof.begin(TAG_BERT_LN, s));
-    MEC_TRY(launch_bert_layernorm(t32, M, g1, b1, h32, hs, nullptr, s, MH));
+    MEC_TRY(launch_bert_layernorm(t32, M, g1, b1, nullptr, hs, st1, s, MH));
     MEC_TRY(prof.end(TAG_BERT_LN, s));
     g = GemmParams();
     g.split = 1; g.A = hs; g.a_lo = MH; g.B = wi; g.b_lo = wlo; g.oscale = sc[2];
@@ -353,10 +372,12 @@ int TextModel::forward_x3(const int32_t* ids, const int32_t* mask, int B, int L,
     MEC_TRY(launch_gemm(g, s, &prof, TAG_BERT_FFN1));
     g = GemmParams();
     g.split = 1; g.A = bigs; g.a_lo = MF; g.B = wo2; g.b_lo = wlo; g.oscale = sc[3];
-    g.bias = bo2; g.R = h32; g.r_f32 = 1; g.C32 = t32; g.M = M; g.N = H; g.K = FF;
+    g.bias = bo2; g.R = t32; g.r_f32 = 1; g.r_stats = st1; g.r_g = g1; g.r_b = b1; g.C32 = h32;
+    g.M = M; g.N = H; g.K = FF;
     MEC_TRY(launch_gemm(g, s, &prof, TAG_BERT_FFN2));
     MEC_TRY(prof.begin(TAG_BERT_LN, s));
-    MEC_TRY(launch_bert_layernorm(t32, M, g2, b2, h32, hs, nullptr, s, MH));
+    // the last LN's f32 output feeds the pooler, so it is written in full (in place)
+    MEC_TRY(launch_bert_layernorm(h32, M, g2, b2, last ? h32 : nullptr, hs, st2, s, MH));
     MEC_TRY(prof.end(TAG_BERT_LN, s));
   }
   const float* head = P + PRM_LAYER * NL;

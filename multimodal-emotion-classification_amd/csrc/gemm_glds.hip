@@ -38,10 +38,15 @@ __global__ __launch_bounds__(64 * WM * WN, (WM * WN == 4) ? 2 : 1) void gemm_gld
   // loaded into registers before the main loop,
   // so its HBM read hides under the operand loads and MFMAs instead of following them
   // (ResNet's short-K conv3 GEMMs, BERT's O-projection)
-  // SP: split-f16 operands (GemmParams::split): the K loop runs over 3 K passes, pass 0 reading
-  // the A lo plane, pass 1 the B lo plane, pass 2 both hi planes
+  // SP: split-f16 operands (GemmParams::split). SP = 1 (pass-major): the K loop runs over 3 K
+  // passes, pass 0 reading the A lo plane, pass 1 the B lo plane, pass 2 both hi planes. SP = 2
+  // (interleaved, opt().gemm_x3_order 1): one K loop; a stage holds the hi AND lo tiles of A and B
+  // (two halves), and each 32-deep k chunk runs its three MFMA terms (lo.hi, hi.lo, hi.hi) back to
+  // back: every operand byte is fetched and staged once instead of 1.5 times on average, and four
+  // fragment reads feed three MFMAs instead of six. 16x16x32 tiles only (one k-chunk order).
   static_assert(BK == 64 || BK == 32, "BK");
   static_assert(SP == 0 || PRE == 0 || PRE == 3, "split operands: split residual prefetch only");
+  static_assert(SP != 2 || MF == 16, "interleaved split: 16x16x32 tiles only");
   constexpr int CH = BK / 8;                   // 16-B chunks per LDS row
   constexpr int RPI = 64 / CH;                 // rows per glds wave-instruction (1 KB)
   constexpr int NW = WM * WN;
@@ -53,8 +58,10 @@ __global__ __launch_bounds__(64 * WM * WN, (WM * WN == 4) ? 2 : 1) void gemm_gld
   constexpr int AI = BM / RPI / NW;            // glds wave-instructions per stage (A)
   constexpr int BI = BN / RPI / NW;            // (B)
   static_assert(BI >= 1 && AI >= 1, "tile too small for 8 waves");
-  constexpr int LPT = AI + BI;
-  constexpr int STAGE = (BM + BN) * BK;        // halfs per stage
+  constexpr int NPL = SP == 2 ? 2 : 1;         // operand planes per stage
+  constexpr int LPT = (AI + BI) * NPL;
+  constexpr int HALF = (BM + BN) * BK;         // halfs per plane of a stage
+  constexpr int STAGE = HALF * NPL;            // halfs per stage
   constexpr int EPI_LD = TN + 4;               // f32 staging row (padded)
   constexpr int EPI = NW * 32 * EPI_LD;        // floats for the epilogue staging
   constexpr int SMEM_H = (NS * STAGE > EPI * 2) ? NS * STAGE : EPI * 2;
@@ -121,16 +128,10 @@ __global__ __launch_bounds__(64 * WM * WN, (WM * WN == 4) ? 2 : 1) void gemm_gld
   const f16* zero = reinterpret_cast<const f16*>(g_zero_page);
 
   const int nk0 = K / BK;  // K tiles per pass
-  auto issue = [&](int stage, int kt) {
-    long long aoff = 0, boff = 0;
-    if constexpr (SP) {  // pass 0: A_lo . B_hi, pass 1: A_hi . B_lo, pass 2: A_hi . B_hi
-      const int pl = (kt >= nk0) + (kt >= 2 * nk0);
-      kt -= pl * nk0;
-      aoff = pl == 0 ? p.a_lo : 0;
-      boff = pl == 1 ? p.b_lo : 0;
-    }
+  // one plane of K tile kt into stage `stage` (its half h): A at aoff, B at boff from the hi planes
+  auto issue_plane = [&](int stage, int kt, int h, long long aoff, long long boff) {
     const int k0 = kt * BK;
-    f16* sA = smem + stage * STAGE;
+    f16* sA = smem + stage * STAGE + h * HALF;
     f16* sB = sA + BM * BK;
     if constexpr (AM == A_PLAIN) {
 #pragma unroll
@@ -162,6 +163,17 @@ __global__ __launch_bounds__(64 * WM * WN, (WM * WN == 4) ? 2 : 1) void gemm_gld
     for (int j = 0; j < BI; ++j)
       __builtin_amdgcn_global_load_lds((const void*)(b_src[j] + boff + k0), (lds_vptr)(sB + (wave * BI + j) * RPI * BK),
                                        16, 0, 0);
+  };
+  auto issue = [&](int stage, int kt) {
+    if constexpr (SP == 1) {  // pass 0: A_lo . B_hi, pass 1: A_hi . B_lo, pass 2: A_hi . B_hi
+      const int pl = (kt >= nk0) + (kt >= 2 * nk0);
+      issue_plane(stage, kt - pl * nk0, 0, pl == 0 ? p.a_lo : 0, pl == 1 ? p.b_lo : 0);
+    } else if constexpr (SP == 2) {  // hi planes into half 0, lo planes into half 1
+      issue_plane(stage, kt, 0, 0, 0);
+      issue_plane(stage, kt, 1, p.a_lo, p.b_lo);
+    } else {
+      issue_plane(stage, kt, 0, 0, 0);
+    }
   };
 
   using EG = EpiGeom<BM, BN, WM, WN>;
@@ -195,7 +207,7 @@ __global__ __launch_bounds__(64 * WM * WN, (WM * WN == 4) ? 2 : 1) void gemm_gld
 #pragma unroll
       for (int e = 0; e < NACC; ++e) acc[i][j][e] = 0.f;
 
-  const int nk = SP ? 3 * nk0 : nk0;
+  const int nk = SP == 1 ? 3 * nk0 : nk0;
 #pragma unroll
   for (int s = 0; s < NS - 1; ++s)
     if (s < nk) issue(s, s);
@@ -245,6 +257,45 @@ __global__ __launch_bounds__(64 * WM * WN, (WM * WN == 4) ? 2 : 1) void gemm_gld
 #pragma unroll
           for (int j = 0; j < TJ; ++j)
             acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_f16(af[i], bf[j], acc[i][j], 0, 0, 0);
+      }
+    } else if constexpr (SP == 2) {
+      // interleaved split: per 32-deep k chunk the hi and lo fragments of A and B, then the three
+      // terms term-major (each accumulator: lo.hi, hi.lo, hi.hi of the chunk, in that order)
+      const int l16 = lane & 15, lq = lane >> 4;
+      constexpr int KS = BK / 32;
+#pragma unroll
+      for (int s = 0; s < KS; ++s) {
+        const int kcs = 4 * s + lq;
+        half8 af[2][TI], bf[2][TJ];  // [plane: 0 hi, 1 lo]
+#pragma unroll
+        for (int h = 0; h < 2; ++h) {
+#pragma unroll
+          for (int i = 0; i < TI; ++i) {
+            const int r = wm * TM + i * 16 + l16;
+            af[h][i] = *reinterpret_cast<const half8*>(sA + h * HALF + r * BK + sw<BK>(r, kcs) * 8);
+          }
+#pragma unroll
+          for (int j = 0; j < TJ; ++j) {
+            const int r = wn * TN + j * 16 + l16;
+            bf[h][j] = *reinterpret_cast<const half8*>(sB + h * HALF + r * BK + sw<BK>(r, kcs) * 8);
+          }
+        }
+        __builtin_amdgcn_sched_barrier(0);
+#pragma unroll
+        for (int i = 0; i < TI; ++i)
+#pragma unroll
+          for (int j = 0; j < TJ; ++j)
+            acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_f16(af[1][i], bf[0][j], acc[i][j], 0, 0, 0);
+#pragma unroll
+        for (int i = 0; i < TI; ++i)
+#pragma unroll
+          for (int j = 0; j < TJ; ++j)
+            acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_f16(af[0][i], bf[1][j], acc[i][j], 0, 0, 0);
+#pragma unroll
+        for (int i = 0; i < TI; ++i)
+#pragma unroll
+          for (int j = 0; j < TJ; ++j)
+            acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_f16(af[0][i], bf[0][j], acc[i][j], 0, 0, 0);
       }
     } else {
       // 16x16x32: lane l holds A[row l&15][k 8(l>>4)..+7] of each 32-deep k step. Both
@@ -683,7 +734,22 @@ __global__ __launch_bounds__(512) void gemm_pp_kernel(const GemmParams p) {
 
 template <int BM, int BN, int WM, int WN, int NS, int MF, int BK, int ACT>
 static int launch_cfg_act(const GemmParams& p, hipStream_t s, int nwg, dim3 blk) {
-  if (p.split) {  // split-f16 operands (fp32x3 path): three K passes, runtime activation
+  if (p.split == 2) {  // split-f16 operands, K-interleaved terms (16x16x32 tiles only)
+    if constexpr (MF == 16 && BK == 32 && 4 * (BM + BN) * BK * NS <= 160 * 1024) {
+      if (BM * BN <= 128 * 128 && opt().gemm_prefetch_r && p.amode == A_PLAIN && p.R && p.r_lo && p.K <= 512) {
+        if constexpr (BM * BN <= 128 * 128)
+          hipLaunchKernelGGL((gemm_glds_kernel<BM, BN, WM, WN, NS, A_PLAIN, 0, MF, BK, 3, -1, 2>), dim3(nwg), blk, 0, s, p);
+      } else if (p.amode == A_PLAIN)
+        hipLaunchKernelGGL((gemm_glds_kernel<BM, BN, WM, WN, NS, A_PLAIN, 0, MF, BK, 0, -1, 2>), dim3(nwg), blk, 0, s, p);
+      else if (p.amode == A_CONV)
+        hipLaunchKernelGGL((gemm_glds_kernel<BM, BN, WM, WN, NS, A_CONV, 0, MF, BK, 0, -1, 2>), dim3(nwg), blk, 0, s, p);
+      else
+        hipLaunchKernelGGL((gemm_glds_kernel<BM, BN, WM, WN, NS, A_DUAL, 0, MF, BK, 0, -1, 2>), dim3(nwg), blk, 0, s, p);
+    } else {
+      set_error("gemm_glds: interleaved split operands need a 16x16x32 tile with 32-deep stages (tiles 7xxxx)");
+      return -1;
+    }
+  } else if (p.split) {  // split-f16 operands (fp32x3 path): three K passes, runtime activation
     if (BM * BN <= 128 * 128 && opt().gemm_prefetch_r && p.amode == A_PLAIN && p.R && p.r_lo && p.K <= 512) {
       // split identity residual of ResNet's conv3 GEMMs, both planes prefetched (PRE = 3)
       if constexpr (BM * BN <= 128 * 128)
@@ -739,8 +805,8 @@ static int launch_cfg(const GemmParams& p0, hipStream_t s) {
 // being captured into a graph) and caches the fastest; `gemm_bn` forces a width.
 // Cache key: engine 0 (this engine) + the shape; the cache is the calling handle's
 // (tune_cache(), mec_common.h).
-static std::array<int, 11> gemm_key(const GemmParams& p) {  // engine slot: 0, or 2 for split operands
-  return {p.split ? 2 : 0, p.amode, p.M, p.N, p.K, p.H, p.W, p.C, p.ks, p.stride, p.pad};
+static std::array<int, 11> gemm_key(const GemmParams& p) {  // engine slot: 0, 2 split pass-major, 3 interleaved
+  return {p.split == 2 ? 3 : p.split ? 2 : 0, p.amode, p.M, p.N, p.K, p.H, p.W, p.C, p.ks, p.stride, p.pad};
 }
 
 // Tile configs (id): 256 / 128 / 64 = 256 x BN with 8 waves; 1128 / 1064 = 128 x BN with
@@ -778,6 +844,14 @@ static int launch_bn(const GemmParams& p, hipStream_t s, int id) {
     case 50128: return launch_cfg<256, 128, 2, 2, 3, 16, 32>(p, s);
     case 60128: return launch_cfg<256, 128, 2, 2, 2, 16, 32>(p, s);
     case 50256: return launch_cfg<128, 256, 2, 2, 3, 16, 32>(p, s);
+    // interleaved split operands only (split == 2, gemm_x3_order 1): 32-deep K stages holding the
+    // hi and lo tiles of A and B (LDS: 256 x 256 2 x 64 KB; 256 x 128 3 x 48 KB; 128 x 128 2 x 32 KB,
+    // two blocks per CU; 128 x 64 2 x 24 KB; 256 x 64 on 4 waves 2 x 40 KB)
+    case 70256: return launch_cfg<256, 256, 2, 4, 2, 16, 32>(p, s);
+    case 70128: return launch_cfg<256, 128, 4, 2, 3, 16, 32>(p, s);
+    case 71128: return launch_cfg<128, 128, 2, 2, 2, 16, 32>(p, s);
+    case 71064: return launch_cfg<128, 64, 2, 2, 2, 16, 32>(p, s);
+    case 70064: return launch_cfg<256, 64, 2, 2, 2, 16, 32>(p, s);
     case 40256:
     case 41256: {
       if (p0.amode != A_PLAIN) { set_error("gemm_glds: ping-pong tiles take a plain A only"); return -1; }
@@ -838,15 +912,21 @@ static int heuristic_bn(const GemmParams& p) {
   return 64;
 }
 
+static bool x3i_tile(int id) { return id >= 70000 && id < 80000; }
+
 static int tune_bn(const GemmParams& p, hipStream_t s, int* out_bn) {
   constexpr int REPS = 5;
   const int cands[] = {64,    128,   256,   1128,  1064,  10064, 10128, 10256, 11128,
                        11064, 20256, 30256, 20128, 40256, 41256, 50128, 60128, 50256};
+  const int cands_x3i[] = {70256, 70128, 71128, 71064, 70064};
   hipEvent_t ev[REPS + 1];
   for (auto& e : ev) MEC_HIP(hipEventCreate(&e));
   float best = 1e30f;
-  int best_bn = heuristic_bn(p);
-  for (int bn : cands) {
+  int best_bn = p.split == 2 ? 71064 : heuristic_bn(p);
+  const int* cb = p.split == 2 ? cands_x3i : cands;
+  const int nc = p.split == 2 ? (int)(sizeof(cands_x3i) / sizeof(int)) : (int)(sizeof(cands) / sizeof(int));
+  for (int ci = 0; ci < nc; ++ci) {
+    const int bn = cb[ci];
     if (p.N % tile_bn(bn)) continue;
     if (bn >= 40000 && bn < 50000 && p.amode != A_PLAIN) continue;
     MEC_TRY(launch_bn(p, s, bn));  // warm
@@ -867,13 +947,17 @@ static int tune_bn(const GemmParams& p, hipStream_t s, int* out_bn) {
 }
 
 int gemm_tuned_bn(int amode, int M, int N, int K) {
-  const int t = tune_cache().find_shape(0, amode, M, N, K);
-  return t ? t : tune_cache().find_shape(2, amode, M, N, K);  // else the split-operand engine's
+  int t = tune_cache().find_shape(0, amode, M, N, K);
+  if (!t) t = tune_cache().find_shape(2, amode, M, N, K);  // else the split-operand engines'
+  return t ? t : tune_cache().find_shape(3, amode, M, N, K);
 }
 
-int launch_gemm_glds(const GemmParams& p, hipStream_t s, int force_bn) {
+int launch_gemm_glds(const GemmParams& p0, hipStream_t s, int force_bn) {
+  GemmParams p = p0;
+  if (p.split && opt().gemm_x3_order == 1) p.split = 2;  // K-interleaved split terms
   if (force_bn) {
     MEC_REQUIRE(p.N % tile_bn(force_bn) == 0, "gemm_glds: forced tile width does not divide N");
+    MEC_REQUIRE((p.split == 2) == x3i_tile(force_bn), "gemm_glds: tiles 7xxxx serve (only) interleaved split operands");
     return launch_bn(p, s, force_bn);
   }
   const auto key = gemm_key(p);

@@ -68,8 +68,8 @@ enum KernelTag : int {
 // owns a copy, taken from the process defaults when it is created, and kernels read the
 // options of the handle whose call they serve (opt()), so handles never perturb each other.
 // Every setting of a knob gives the same results bit for bit, with these exceptions:
-//   * conv3x3_halo 0 vs 1 and fusion_r 4 vs 1|2 sum in other fp32 orders (same values to
-//     rounding, not the same bits; include/mec.h);
+//   * conv3x3_halo 0 vs 1, fusion_r 4 vs 1|2 and gemm_x3_order 0 vs 1 sum in other fp32 orders
+//     (same values to rounding, not the same bits; include/mec.h);
 //   * the probe-build values (compiled only with -DMEC_PROBES: they skip work to time a
 //     kernel's parts and return wrong results).
 struct Options {
@@ -110,6 +110,13 @@ struct Options {
   // (8: the fp32x3 FFN1 reads 911 -> 663 MB per launch at B = 256, time unchanged;
   // profiles/ffn1_x3_traffic*.json)
   int gemm_glds_group_m = 8;
+  // split-f16 (fp32x3) GEMM term order: 0 = pass-major (all of K for lo.hi, then hi.lo, then
+  // hi.hi), 1 = K-interleaved (each 32-deep k chunk's three terms back to back; tiles 7xxxx). Both
+  // are fp32-accurate; they sum in different orders (not the same bits). 1: every operand byte is
+  // fetched and staged once (not 1.5x) and 4 fragment reads feed 3 MFMAs (not 6): less energy per
+  // MFMA, a higher held clock: text 18.84 -> 17.96 ms, ResNet50 10.06 -> 9.00, fused step 28.05 ->
+  // 26.19 ms at B = 256 (profiles/r03_ab_x3order_*.txt)
+  int gemm_x3_order = 1;
   int fusion_r = 4;         // samples per fusion workgroup
   int fusion_split = 1;     // fusion as 3 launches
   int gemm_debug = 0, conv3x3_debug = 0, stem_debug = 0, audio_debug = 0, speech_debug = 0;  // probe builds only

@@ -121,19 +121,44 @@ def _split(a, scale=1.0):
     return np.concatenate([hi.ravel(), lo.ravel()]).reshape((2,) + x.shape)
 
 
-SPLIT_TILES = [64, 128, 256, 1128, 1064, 10064, 10128, 10256, 11128, 11064, 20256, 30256, 20128, 50128, 60128, 50256,
-               40256, 41256]
+SPLIT_TILES = {0: [64, 128, 256, 1128, 1064, 10064, 10128, 10256, 11128, 11064, 20256, 30256, 20128, 50128, 60128,
+                   50256, 40256, 41256],
+               1: [70256, 70128, 71128, 71064, 70064]}
 
 
+class x3_order:
+    """The split engine's term order (option gemm_x3_order: 0 pass-major, 1 K-interleaved, the
+    default) as the process default for the handle-less entry points, restored on exit."""
+
+    def __init__(self, order):
+        from mec import _lib
+        self.lib, self.order = _lib.load(), order
+
+    def __enter__(self):
+        from mec import _lib
+        _lib.check(self.lib.mec_set_option(b'gemm_x3_order', self.order), 'gemm_x3_order')
+
+    def __exit__(self, *exc):
+        self.lib.mec_set_option(b'gemm_x3_order', 1)
+
+
+@pytest.mark.parametrize('order', [0, 1])
 @pytest.mark.parametrize('M,N,K,act', [(512, 256, 768, 0), (1000, 768, 3072, 4), (300, 512, 128, 1)])
-def test_split_gemm_vs_fp64_and_every_tile_bit_identical(dev, M, N, K, act):
+def test_split_gemm_vs_fp64_and_every_tile_bit_identical(dev, M, N, K, act, order):
     """mec_gemm_f16x3 (the fp32x3 engine) against float64 A . B^T of the fp32 operands: within the
     fp32 GEMM engine's bar (2e-6 x sum |a b|, tests/test_gpu_fp32.py), with the weights pre-scaled
-    by 2^8 and undone by oscale; and every tile computes the same bits (each output's passes and
-    k chain are tile-independent)."""
+    by 2^8 and undone by oscale; and, per term order, every tile computes the same bits (each
+    output's terms and k chain are tile-independent)."""
     import ctypes
     from mec import _lib
     lib = _lib.load()
+    with x3_order(order):
+        _split_gemm_tiles(dev, lib, M, N, K, act, order)
+
+
+def _split_gemm_tiles(dev, lib, M, N, K, act, order):
+    import ctypes
+    from mec import _lib
     rng = np.random.default_rng(M + N + K)
     A = rng.standard_normal((M, K)).astype(np.float32)
     Bw = (rng.standard_normal((N, K)) * 0.03).astype(np.float32)
@@ -154,8 +179,8 @@ def test_split_gemm_vs_fp64_and_every_tile_bit_identical(dev, M, N, K, act):
         ref = 0.5 * ref * (1 + erf(ref / np.sqrt(2)))
     bound = 2e-6 * (np.abs(A).astype(np.float64) @ np.abs(Bw).astype(np.float64).T + np.abs(bias) + 1)
     outs = {}
-    for tile in [0] + SPLIT_TILES:
-        width = 256 if tile >= 40000 else (tile % 10000 if tile % 10000 < 1000 else tile % 10000 - 1000)
+    for tile in [0] + SPLIT_TILES[order]:
+        width = 256 if 40000 <= tile < 50000 else (tile % 10000 if tile % 10000 < 1000 else tile % 10000 - 1000)
         if tile and N % width:
             continue
         _lib.check(lib.mec_set_option(b'gemm_bn', tile), 'gemm_bn')
@@ -169,22 +194,29 @@ def test_split_gemm_vs_fp64_and_every_tile_bit_identical(dev, M, N, K, act):
         outs[tile] = C.cpu().numpy()
     got = outs[0]
     err = np.abs(got - ref)
-    print(f'split GEMM {M}x{N}x{K} act {act}: max err {err.max():.3g}, max err / bound {(err / bound).max():.3g}, '
-          f'tiles {len(outs) - 1}')
+    print(f'split GEMM (order {order}) {M}x{N}x{K} act {act}: max err {err.max():.3g}, '
+          f'max err / bound {(err / bound).max():.3g}, tiles {len(outs) - 1}')
     assert (err <= bound).all()
     for tile, o in outs.items():
         assert np.array_equal(o, got), f'tile {tile} differs from the autotuned tile'
 
 
+@pytest.mark.parametrize('order', [0, 1])
 @pytest.mark.parametrize('M,N,K', [(4096, 768, 768), (4096, 768, 3072), (2048, 512, 4608)])
-def test_split_gemm_error_vs_exact_fp32_gemm(dev, M, N, K):
+def test_split_gemm_error_vs_exact_fp32_gemm(dev, M, N, K, order):
     """Against float64 on the same fp32 operands (BERT-like scales: activations O(1), weights
     ~0.02-0.05), the split-f16 engine's error is of the exact-fp32 MFMA engine's size (the
     split's 2^-22 operand rounding sits below the fp32 accumulation error): max and RMS error of
-    both printed; the split's max error may exceed the exact engine's by at most 50%."""
+    both printed; the split's max error may exceed the exact engine's by at most 50%, at either
+    term order."""
+    from mec import _lib
+    with x3_order(order):
+        _split_vs_exact(dev, _lib.load(), M, N, K, order)
+
+
+def _split_vs_exact(dev, lib, M, N, K, order):
     import ctypes
     from mec import _lib
-    lib = _lib.load()
     rng = np.random.default_rng(K)
     A = rng.standard_normal((M, K)).astype(np.float32)
     W = (rng.standard_normal((N, K)) * (0.02 if K < 4000 else 0.05)).astype(np.float32)
@@ -202,18 +234,23 @@ def test_split_gemm_error_vs_exact_fp32_gemm(dev, M, N, K):
     e32 = np.abs(C32.cpu().numpy() - ref)
     ex3 = np.abs(Cx.cpu().numpy() - ref)
     print(f'{M}x{N}x{K}: exact-fp32 engine max {e32.max():.3g} rms {np.sqrt((e32 ** 2).mean()):.3g}; '
-          f'split-f16 engine max {ex3.max():.3g} rms {np.sqrt((ex3 ** 2).mean()):.3g}')
+          f'split-f16 engine (order {order}) max {ex3.max():.3g} rms {np.sqrt((ex3 ** 2).mean()):.3g}')
     assert ex3.max() <= 1.5 * e32.max()
 
 
-@pytest.mark.parametrize('tile', [0, 40256, 10256, 11128])
-def test_split_gemm_plane_output(dev, tile):
+@pytest.mark.parametrize('order,tile', [(0, 0), (0, 40256), (0, 10256), (0, 11128), (1, 0), (1, 70256), (1, 71128)])
+def test_split_gemm_plane_output(dev, order, tile):
     """C16 written as hi / lo planes (c_lo): hi = f16(v), lo = f16(v - hi), for v the fp32 result
     the same launch writes to C32 on another call; on the ping-pong tile this is its staged
     f16 fast-path epilogue run once per plane."""
+    from mec import _lib
+    with x3_order(order):
+        _plane_output(dev, _lib.load(), tile)
+
+
+def _plane_output(dev, lib, tile):
     import ctypes
     from mec import _lib
-    lib = _lib.load()
     M, N, K = 700, 512, 768
     rng = np.random.default_rng(7)
     A = rng.standard_normal((M, K)).astype(np.float32)
