@@ -1,11 +1,11 @@
 #!/bin/bash
 # HBM traffic of the fp32x3 BERT FFN1 GEMM (the headline's roofline kernel): separate rocprofv3
 # --pmc passes (FETCH_SIZE, WRITE_SIZE, MFMA busy) over the fp32x3 text encoder at B=256 with
-# the split tile pinned to the autotuner's FFN1 choice (TILE, default 10256), then
+# the split tile pinned to the FFN1 pin (TILE, default 70256: the K-interleaved split tile), then
 # profiles/ffn1_x3_traffic.json (FETCH_SIZE doubled: MI355X_MICROARCH.md gfx950).
 cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
 export TMPDIR=/tmp
-TILE=${TILE:-10256}
+TILE=${TILE:-70256}
 OUT=gpurun_out/pmc_ffn1_x3
 EXTRA=${GM:+--opt gemm_glds_group_m=$GM}  # optional glds tile order
 rm -rf $OUT; mkdir -p $OUT
