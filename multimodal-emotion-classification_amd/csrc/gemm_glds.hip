@@ -821,6 +821,7 @@ static std::array<int, 11> gemm_key(const GemmParams& p) {  // engine slot: 0, 2
 // 50256: the same for 128 x 256.
 static int tile_bn(int id) {
   if (id >= 40000 && id < 50000) return 256;  // ping-pong tiles are 256 wide
+  if (id >= 70000 && id < 80000) return id % 1000;  // interleaved split tiles: 7 | shape | width
   id %= 10000;
   return id > 1000 ? id - 1000 : id;
 }
@@ -844,14 +845,19 @@ static int launch_bn(const GemmParams& p, hipStream_t s, int id) {
     case 50128: return launch_cfg<256, 128, 2, 2, 3, 16, 32>(p, s);
     case 60128: return launch_cfg<256, 128, 2, 2, 2, 16, 32>(p, s);
     case 50256: return launch_cfg<128, 256, 2, 2, 3, 16, 32>(p, s);
-    // interleaved split operands only (split == 2, gemm_x3_order 1): 32-deep K stages holding the
-    // hi and lo tiles of A and B (LDS: 256 x 256 2 x 64 KB; 256 x 128 3 x 48 KB; 128 x 128 2 x 32 KB,
-    // two blocks per CU; 128 x 64 2 x 24 KB; 256 x 64 on 4 waves 2 x 40 KB)
+    // interleaved split operands only (split == 2, gemm_x3_order 1; id = 7 | shape | width): 32-deep
+    // K stages holding the hi and lo tiles of A and B (LDS: 256 x 256 2 x 64 KB; 256 x 128 3 x 48 KB;
+    // 128 x 128 2 x 32 KB, two blocks per CU; 128 x 64 2 x 24 KB; 256 x 64 on 4 waves 2 x 40 KB)
     case 70256: return launch_cfg<256, 256, 2, 4, 2, 16, 32>(p, s);
     case 70128: return launch_cfg<256, 128, 4, 2, 3, 16, 32>(p, s);
     case 71128: return launch_cfg<128, 128, 2, 2, 2, 16, 32>(p, s);
     case 71064: return launch_cfg<128, 64, 2, 2, 2, 16, 32>(p, s);
     case 70064: return launch_cfg<256, 64, 2, 2, 2, 16, 32>(p, s);
+    // 4-wave tiles with 128 x 128 / 64 x 128 / 128 x 64 wave tiles (one wave per SIMD): fewer LDS
+    // fragment bytes per MFMA than the 8-wave tiles (LDS 2 x 48 / 64 KB)
+    case 71256: return launch_cfg<128, 256, 2, 2, 2, 16, 32>(p, s);
+    case 72128: return launch_cfg<256, 128, 2, 2, 2, 16, 32>(p, s);
+    case 72256: return launch_cfg<256, 256, 2, 2, 2, 16, 32>(p, s);
     case 40256:
     case 41256: {
       if (p0.amode != A_PLAIN) { set_error("gemm_glds: ping-pong tiles take a plain A only"); return -1; }
@@ -918,7 +924,7 @@ static int tune_bn(const GemmParams& p, hipStream_t s, int* out_bn) {
   constexpr int REPS = 5;
   const int cands[] = {64,    128,   256,   1128,  1064,  10064, 10128, 10256, 11128,
                        11064, 20256, 30256, 20128, 40256, 41256, 50128, 60128, 50256};
-  const int cands_x3i[] = {70256, 70128, 71128, 71064, 70064};
+  const int cands_x3i[] = {70256, 70128, 71128, 71064, 70064, 71256, 72128, 72256};
   hipEvent_t ev[REPS + 1];
   for (auto& e : ev) MEC_HIP(hipEventCreate(&e));
   float best = 1e30f;

@@ -123,7 +123,7 @@ def _split(a, scale=1.0):
 
 SPLIT_TILES = {0: [64, 128, 256, 1128, 1064, 10064, 10128, 10256, 11128, 11064, 20256, 30256, 20128, 50128, 60128,
                    50256, 40256, 41256],
-               1: [70256, 70128, 71128, 71064, 70064]}
+               1: [70256, 70128, 71128, 71064, 70064, 71256, 72128, 72256]}
 
 
 class x3_order:
@@ -180,7 +180,8 @@ def _split_gemm_tiles(dev, lib, M, N, K, act, order):
     bound = 2e-6 * (np.abs(A).astype(np.float64) @ np.abs(Bw).astype(np.float64).T + np.abs(bias) + 1)
     outs = {}
     for tile in [0] + SPLIT_TILES[order]:
-        width = 256 if 40000 <= tile < 50000 else (tile % 10000 if tile % 10000 < 1000 else tile % 10000 - 1000)
+        width = (256 if 40000 <= tile < 50000 else tile % 1000 if tile >= 70000 else
+                 tile % 10000 if tile % 10000 < 1000 else tile % 10000 - 1000)
         if tile and N % width:
             continue
         _lib.check(lib.mec_set_option(b'gemm_bn', tile), 'gemm_bn')

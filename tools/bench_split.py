@@ -1,7 +1,9 @@
 """Time every tile of the split-f16 (fp32x3) GEMM engine on the BERT shapes at B=256
 (mec_gemm_f16x3, gemm_bn forced), interleaved rounds, median; one JSON line per (shape, tile).
 
-    python tools/bench_split.py [--rounds 5] [--iters 10] [--shapes ffn1 ffn2 qkv oproj]
+    python tools/bench_split.py [--rounds 5] [--iters 10] [--shapes ffn1 ffn2 qkv oproj] [--order 0|1]
+
+--order 1 (the default term order, K-interleaved) times the 7xxxx tiles; --order 0 the pass-major ones.
 """
 import argparse
 import ctypes
@@ -19,9 +21,12 @@ from mec import _lib  # noqa: E402
 SHAPES = {'qkv': (32768, 2304, 768, 0, False), 'oproj': (32768, 768, 768, 0, True),
           'ffn1': (32768, 3072, 768, 4, False), 'ffn2': (32768, 768, 3072, 0, True)}
 TILES = [128, 256, 1128, 10128, 10256, 11128, 20256, 30256, 20128, 50128, 60128, 50256, 40256, 41256]
+TILES_X3I = [70256, 70128, 71128, 71064, 70064, 71256, 72128, 72256]
 
 
 def width(t):
+    if 70000 <= t < 80000:  # interleaved split tiles (gemm_x3_order 1): 7 | shape | width
+        return t % 1000
     if t >= 40000:
         return 256
     t %= 10000
@@ -33,9 +38,13 @@ def main():
     ap.add_argument('--rounds', type=int, default=5)
     ap.add_argument('--iters', type=int, default=10)
     ap.add_argument('--shapes', nargs='+', default=list(SHAPES))
-    ap.add_argument('--tiles', type=int, nargs='+', default=TILES)
+    ap.add_argument('--tiles', type=int, nargs='+', default=None)
+    ap.add_argument('--order', type=int, default=1, choices=[0, 1])
     a = ap.parse_args()
     lib = _lib.load()
+    _lib.check(lib.mec_set_option(b'gemm_x3_order', a.order), 'gemm_x3_order')
+    if a.tiles is None:
+        a.tiles = TILES_X3I if a.order == 1 else TILES
     dev = torch.device('cuda', 0)
     st = ctypes.c_void_p(torch.cuda.current_stream(dev).cuda_stream)
     p = lambda t: ctypes.c_void_p(t.data_ptr()) if t is not None else ctypes.c_void_p(0)  # noqa: E731
