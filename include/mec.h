@@ -161,6 +161,8 @@ int mec_conv_f32(const float* x, const float* w, const float* bias, const float*
  *                          hi.lo, then hi.hi), 1 = K-interleaved (each 32-deep k chunk's three terms
  *                          back to back, 16x16x32 tiles 70256 / 70128 / 71128 / 71064 / 70064 only);
  *                          both fp32-accurate, not the same bits
+ *   "gemm_x3_tag" tag*100000+id  pin an interleaved split tile (7xxxx; 0 = autotune) for one launch
+ *                          class (FusedPipeline pins BERT FFN2 to 70256 at fp32x3)
  *   "conv3x3_direct" 0|[1] layer1 3x3 conv on the halo-tile kernel (mec_conv_f16 too)
  *   "conv3x3_halo" 0|[1]   layers 2-3 stride-1 3x3 convs on the halo kernel (mec_conv_f16 too;
  *                          fp32 accumulation in another order: not bit-identical to 0)

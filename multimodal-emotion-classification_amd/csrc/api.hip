@@ -340,7 +340,7 @@ int set_option(Options& o, const std::string& k, int value) {
     const int v = id % 10000;
     const bool deep = id == 20256 || id == 30256 || id == 20128 || id == 40256 || id == 41256 || id == 50128 ||
                       id == 60128 || id == 50256 || id == 70256 || id == 70128 || id == 71128 || id == 71064 ||
-                      id == 70064 || id == 71256 || id == 72128 || id == 72256;
+                      id == 70064;
     return id == 0 || deep || (id < 20000 && (v == 64 || v == 128 || v == 256 || v == 1064 || v == 1128));
   };
   if (k == "gemm_bn" && tile_ok(value)) {
@@ -350,6 +350,11 @@ int set_option(Options& o, const std::string& k, int value) {
   // one launch class only: value = tag * 100000 + tile id (tags: mec_common.h KernelTag)
   if (k == "gemm_bn_tag" && value >= 0 && value / 100000 > 0 && value / 100000 < TAG_COUNT && tile_ok(value % 100000)) {
     o.gemm_bn_tag[value / 100000] = value % 100000;
+    return 0;
+  }
+  if (k == "gemm_x3_tag" && value >= 0 && value / 100000 > 0 && value / 100000 < TAG_COUNT &&
+      (value % 100000 == 0 || (value % 100000 >= 70000 && tile_ok(value % 100000)))) {
+    o.gemm_x3_tag[value / 100000] = value % 100000;
     return 0;
   }
   set_error("mec_set_option: unknown key or bad value: " + k + " = " + std::to_string(value) +

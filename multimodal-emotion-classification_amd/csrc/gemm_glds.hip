@@ -853,11 +853,9 @@ static int launch_bn(const GemmParams& p, hipStream_t s, int id) {
     case 71128: return launch_cfg<128, 128, 2, 2, 2, 16, 32>(p, s);
     case 71064: return launch_cfg<128, 64, 2, 2, 2, 16, 32>(p, s);
     case 70064: return launch_cfg<256, 64, 2, 2, 2, 16, 32>(p, s);
-    // 4-wave tiles with 128 x 128 / 64 x 128 / 128 x 64 wave tiles (one wave per SIMD): fewer LDS
-    // fragment bytes per MFMA than the 8-wave tiles (LDS 2 x 48 / 64 KB)
-    case 71256: return launch_cfg<128, 256, 2, 2, 2, 16, 32>(p, s);
-    case 72128: return launch_cfg<256, 128, 2, 2, 2, 16, 32>(p, s);
-    case 72256: return launch_cfg<256, 256, 2, 2, 2, 16, 32>(p, s);
+    // (measured and dropped: 4-wave 128 x 256, 256 x 128 and 256 x 256 forms, one wave per SIMD with
+    // 64 x 128 / 128 x 64 / 128 x 128 wave tiles: 10-45 % slower on every BERT shape,
+    // profiles/r03_split_tiles_x3i.log)
     case 40256:
     case 41256: {
       if (p0.amode != A_PLAIN) { set_error("gemm_glds: ping-pong tiles take a plain A only"); return -1; }
@@ -924,7 +922,7 @@ static int tune_bn(const GemmParams& p, hipStream_t s, int* out_bn) {
   constexpr int REPS = 5;
   const int cands[] = {64,    128,   256,   1128,  1064,  10064, 10128, 10256, 11128,
                        11064, 20256, 30256, 20128, 40256, 41256, 50128, 60128, 50256};
-  const int cands_x3i[] = {70256, 70128, 71128, 71064, 70064, 71256, 72128, 72256};
+  const int cands_x3i[] = {70256, 70128, 71128, 71064, 70064};
   hipEvent_t ev[REPS + 1];
   for (auto& e : ev) MEC_HIP(hipEventCreate(&e));
   float best = 1e30f;

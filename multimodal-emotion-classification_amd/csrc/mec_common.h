@@ -117,6 +117,9 @@ struct Options {
   // MFMA, a higher held clock: text 18.84 -> 17.96 ms, ResNet50 10.06 -> 9.00, fused step 28.05 ->
   // 26.19 ms at B = 256 (profiles/r03_ab_x3order_*.txt)
   int gemm_x3_order = 1;
+  // K-interleaved split engine, per launch class: forced tile (7xxxx), 0 = autotune (BERT FFN1 is
+  // pinned to 70256 separately, gemm.hip)
+  int gemm_x3_tag[TAG_COUNT] = {0};
   int fusion_r = 4;         // samples per fusion workgroup
   int fusion_split = 1;     // fusion as 3 launches
   int gemm_debug = 0, conv3x3_debug = 0, stem_debug = 0, audio_debug = 0, speech_debug = 0;  // probe builds only

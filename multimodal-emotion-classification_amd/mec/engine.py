@@ -330,6 +330,13 @@ class FusedPipeline:
             # win: 11.10 vs 11.37 ms per step (interleaved A/B, tools/gpu_ab_tiles.sh,
             # profiles/r02_ab_tiles_fused.txt). Same k order on both tiles: same bits.
             self.text.set_option('gemm_bn_tag', TAG_BERT_FFN2 * 100000 + 40256)
+        if concurrent and precision == 'fp32x3':
+            # the same for the fp32x3 path: FFN2 on the 256 x 256 K-interleaved split tile (384 tiles,
+            # 1.5 rounds of 256 CUs: the image stream fills the half-empty round) instead of the
+            # autotuner's 128 x 128 / 256 x 128 pick: 26.62 vs 27.49 ms per step (interleaved A/B,
+            # tools/gpu_ab_x3tags.sh, profiles/r03_ab_x3tag_ffn2.txt; the O-projection pinned the
+            # same way measured within 0.3 %). Every interleaved tile gives the same bits.
+            self.text.set_option('gemm_x3_tag', TAG_BERT_FFN2 * 100000 + 70256)
 
     def forward(self, x_speech, ids, mask, gray, epilogue=None):
         """One batch through the path -> dict of per-modality and fusion outputs (and, with

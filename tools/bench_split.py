@@ -21,7 +21,7 @@ from mec import _lib  # noqa: E402
 SHAPES = {'qkv': (32768, 2304, 768, 0, False), 'oproj': (32768, 768, 768, 0, True),
           'ffn1': (32768, 3072, 768, 4, False), 'ffn2': (32768, 768, 3072, 0, True)}
 TILES = [128, 256, 1128, 10128, 10256, 11128, 20256, 30256, 20128, 50128, 60128, 50256, 40256, 41256]
-TILES_X3I = [70256, 70128, 71128, 71064, 70064, 71256, 72128, 72256]
+TILES_X3I = [70256, 70128, 71128, 71064, 70064]
 
 
 def width(t):
