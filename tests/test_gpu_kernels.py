@@ -149,32 +149,40 @@ def test_pingpong_group_order_bit_identical(dev, M, N):
 @pytest.mark.parametrize('tile,M,N', [(10256, 2304 + 100, 768), (1128, 300, 512), (11064, 8192, 3072)])
 def test_glds_group_order_bit_identical(dev, tile, M, N):
     """The same for the multi-stage engine (gemm_glds_group_m), on plain f16 operands and on
-    split-f16 (fp32x3) operands: every tile order writes the same bits."""
+    split-f16 (fp32x3) operands at both term orders (pass-major on the tile itself, K-interleaved
+    on its 7xxxx counterpart): every tile order writes the same bits."""
     lib = _lib.load()
     K = 768
+    tile_x3i = {10256: 70256, 1128: 71128, 11064: 71064}[tile]
     g = torch.Generator().manual_seed(M + N + tile)
     A = (torch.rand(2, M, K, generator=g) * 2 - 1).half().to(dev)
     B = (torch.rand(2, N, K, generator=g) * 2 - 1).mul(K ** -0.5).half().to(dev)
     bias = torch.rand(N, generator=g).to(dev)
-    outs, outs3 = [], []
+    outs, outs3 = [], {0: [], 1: []}
     try:
         for gm in (0, 2, 4, 8, 16):
             _lib.check(lib.mec_set_option(b'gemm_glds_group_m', gm), 'gemm_glds_group_m')
-            C32, D32 = torch.empty(M, N, device=dev), torch.empty(M, N, device=dev)
+            C32 = torch.empty(M, N, device=dev)
             _forced(lib, tile, lambda: _lib.check(lib.mec_gemm_f16(_p(A[0]), _p(B[0]), _p(bias), None, 0, None,
                                                                    _p(C32), M, N, K, 0, _s()), f'gemm gm={gm}'))
-            _forced(lib, tile, lambda: _lib.check(lib.mec_gemm_f16x3(_p(A), M * K, _p(B), N * K, ctypes.c_float(1.0),
-                                                                     _p(bias), None, None, 0, _p(D32), M, N, K, 0,
-                                                                     _s()), f'split gemm gm={gm}'))
             torch.cuda.synchronize()
             outs.append(C32.cpu())
-            outs3.append(D32.cpu())
+            for order, t in ((0, tile), (1, tile_x3i)):
+                _lib.check(lib.mec_set_option(b'gemm_x3_order', order), 'gemm_x3_order')
+                D32 = torch.empty(M, N, device=dev)
+                _forced(lib, t, lambda: _lib.check(lib.mec_gemm_f16x3(_p(A), M * K, _p(B), N * K, ctypes.c_float(1.0),
+                                                                      _p(bias), None, None, 0, _p(D32), M, N, K, 0,
+                                                                      _s()), f'split gemm gm={gm} order={order}'))
+                torch.cuda.synchronize()
+                outs3[order].append(D32.cpu())
     finally:
         lib.mec_set_option(b'gemm_glds_group_m', 8)
+        lib.mec_set_option(b'gemm_x3_order', 1)
     ref = A[0].float() @ B[0].float().t() + bias
     assert _rel_err(outs[0].to(dev), ref) < 1e-5
     assert all(torch.equal(o, outs[0]) for o in outs[1:])
-    assert all(torch.equal(o, outs3[0]) for o in outs3[1:])
+    for order in (0, 1):
+        assert all(torch.equal(o, outs3[order][0]) for o in outs3[order][1:]), f'order {order}'
 
 
 def test_gemm_f16_residual_f16_asymmetric(dev):
