@@ -145,8 +145,8 @@ int mec_conv_f32(const float* x, const float* w, const float* bias, const float*
  * each other: mec_model_set_option sets one handle's knob; mec_set_option sets the process
  * default that handles created AFTERWARDS copy (and that the handle-less kernel entry points
  * use). Every pair of settings of one knob gives bit-identical outputs, except "fusion_r" 4 vs
- * 1|2, "conv3x3_halo" 0 vs 1 and "gemm_x3_order" 0 vs 1 (fp32 reassociation, all within the
- * oracle tolerance).
+ * 1|2, "conv3x3_halo" 0 vs 1, "gemm_x3_order" 0 vs 1 and "gelu_x3" 0 vs 1 (fp32 reassociation or
+ * erf evaluation, all within the oracle tolerance).
  *   "gemm_bn" [0]|id       force one f16 GEMM tile (0 = autotune), "gemm_autotune" 0|[1]
  *   "gemm_bn_tag" tag*100000+id   force a tile for one launch class (e.g. 3 = BERT O-proj)
  *   "gemm_f32_tile" [0]|1..8  force one fp32 GEMM tile (0 = autotune; 5..8 = 1..4 on 16x16x4)
@@ -163,6 +163,8 @@ int mec_conv_f32(const float* x, const float* w, const float* bias, const float*
  *                          both fp32-accurate, not the same bits
  *   "gemm_x3_tag" tag*100000+id  pin an interleaved split tile (7xxxx; 0 = autotune) for one launch
  *                          class (FusedPipeline pins BERT FFN2 to 70256 at fp32x3)
+ *   "gelu_x3" 0|[1]        fp32x3 BERT FFN1 GELU: 1 = branch-free erf with a one-instruction exp
+ *                          (error 1.21e-7 x max(|x|, 1) vs float64), 0 = libm erff (not the same bits)
  *   "conv3x3_direct" 0|[1] layer1 3x3 conv on the halo-tile kernel (mec_conv_f16 too)
  *   "conv3x3_halo" 0|[1]   layers 2-3 stride-1 3x3 convs on the halo kernel (mec_conv_f16 too;
  *                          fp32 accumulation in another order: not bit-identical to 0)

@@ -286,6 +286,7 @@ int set_option(Options& o, const std::string& k, int value) {
   }
   if (k == "bert_cls_last" && (value == 0 || value == 1)) { o.bert_cls_last = value; return 0; }
   if (k == "gemm_x3_order" && (value == 0 || value == 1)) { o.gemm_x3_order = value; return 0; }
+  if (k == "gelu_x3" && (value == 0 || value == 1)) { o.gelu_x3 = value; return 0; }
   if (k == "bert_ln_rows" && (value == 1 || value == 2 || value == 4)) {
     o.bert_ln_rows = value;
     return 0;

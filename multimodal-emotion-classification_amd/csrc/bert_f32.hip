@@ -287,6 +287,7 @@ int TextModel::forward_x3(const int32_t* ids, const int32_t* mask, int B, int L,
   float2* st2 = st1 + M;                       // LN2 row stats [M]
   float2* st2c = st2 + M;                      // LN2 row stats of the [CLS] rows [B]
   const bool cls_last = opt().bert_cls_last != 0;
+  const int gelu_act = opt().gelu_x3 ? ACT_GELU_F32 : ACT_GELU_EXACT;  // FFN1's erf GELU
 
   MEC_TRY(launch_bert_embed_ln(ids, M, L, emb.as<float>(), h32, hs, s, MH));
   const f16* W = wts.as<f16>();
@@ -336,7 +337,7 @@ int TextModel::forward_x3(const int32_t* ids, const int32_t* mask, int B, int L,
       MEC_TRY(launch_bert_layernorm(t32c, B, g1, b1, h32c, hsc, nullptr, s, BHc));
       g = GemmParams();
       g.split = 1; g.A = hsc; g.a_lo = BHc; g.B = wi; g.b_lo = wlo; g.oscale = sc[2];
-      g.bias = bi; g.act = ACT_GELU_EXACT; g.C16 = fsc; g.c_lo = BFc; g.M = B; g.N = FF; g.K = H;
+      g.bias = bi; g.act = gelu_act; g.C16 = fsc; g.c_lo = BFc; g.M = B; g.N = FF; g.K = H;
       MEC_TRY(launch_gemm(g, s, &prof, TAG_NONE));
       g = GemmParams();
       g.split = 1; g.A = fsc; g.a_lo = BFc; g.B = wo2; g.b_lo = wlo; g.oscale = sc[3];
@@ -368,7 +369,7 @@ int TextModel::forward_x3(const int32_t* ids, const int32_t* mask, int B, int L,
     MEC_TRY(prof.end(TAG_BERT_LN, s));
     g = GemmParams();
     g.split = 1; g.A = hs; g.a_lo = MH; g.B = wi; g.b_lo = wlo; g.oscale = sc[2];
-    g.bias = bi; g.act = ACT_GELU_EXACT; g.C16 = bigs; g.c_lo = MF; g.M = M; g.N = FF; g.K = H;
+    g.bias = bi; g.act = gelu_act; g.C16 = bigs; g.c_lo = MF; g.M = M; g.N = FF; g.K = H;
     MEC_TRY(launch_gemm(g, s, &prof, TAG_BERT_FFN1));
     g = GemmParams();
     g.split = 1; g.A = bigs; g.a_lo = MF; g.B = wo2; g.b_lo = wlo; g.oscale = sc[3];

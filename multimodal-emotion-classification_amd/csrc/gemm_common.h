@@ -42,6 +42,33 @@ __device__ __forceinline__ float gelu_rat(float x) {
 }
 __device__ __forceinline__ f32x2 gelu_erf_x2(f32x2 x) { return f32x2{gelu_rat(x.x), gelu_rat(x.y)}; }
 
+// fp32 GELU for the fp32x3 path (ACT_GELU_F32): x/2 (1 + erf(x/sqrt2)) with the device library's
+// erff polynomials (|z| < 1: z + z p(z^2); |z| >= 1: 1 - exp(-(|z| + |z| q(|z|)))) evaluated
+// branch-free, the exp as one v_exp_f32 of the exponent times -log2(e) instead of the library's
+// extended-precision range reduction: ~20 VALU instead of ~38 for the two branches a wave64 takes
+// anyway; |erf error| grows by at most ~0.3 f32 ulp (tests/test_gpu_fp32x3.py: the GEMM against
+// float64 GELU within the fp32 engine's bar)
+__device__ __forceinline__ float gelu_f32(float x) {
+  const float z = x * 0.70710678118654752f, a = fabsf(z);
+  const float s = z * z;
+  float ps = __builtin_fmaf(s, __builtin_bit_cast(float, 0xba1345e1u), __builtin_bit_cast(float, 0x3ba10414u));
+  ps = __builtin_fmaf(s, ps, __builtin_bit_cast(float, 0xbcdac9b8u));
+  ps = __builtin_fmaf(s, ps, __builtin_bit_cast(float, 0x3de703beu));
+  ps = __builtin_fmaf(s, ps, __builtin_bit_cast(float, 0xbec09330u));
+  ps = __builtin_fmaf(s, ps, __builtin_bit_cast(float, 0x3e0375d0u));
+  const float es = __builtin_fmaf(a, ps, a);
+  float q = __builtin_fmaf(a, __builtin_bit_cast(float, 0x378e98abu), __builtin_bit_cast(float, 0xb9c68948u));
+  q = __builtin_fmaf(a, q, __builtin_bit_cast(float, 0x3b7cd369u));
+  q = __builtin_fmaf(a, q, __builtin_bit_cast(float, 0xbcc618b2u));
+  q = __builtin_fmaf(a, q, __builtin_bit_cast(float, 0x3dda74e4u));
+  q = __builtin_fmaf(a, q, __builtin_bit_cast(float, 0x3f228afdu));
+  q = __builtin_fmaf(a, q, __builtin_bit_cast(float, 0x3e03c728u));
+  q = __builtin_fmaf(a, q, a);
+  const float el = 1.0f - __builtin_amdgcn_exp2f(q * -1.44269504088896341f);
+  const float e = copysignf(a < 1.0f ? es : el, z);
+  return (x * 0.5f) * (1.0f + e);
+}
+
 // Tile coordinates of logical tile `bid` (after the XCD remap, which gives each XCD a
 // contiguous range): row-major over (bm, bn), or with group_m = G > 0 groups of G M panels
 // walked M-fastest (the last group may be short), so the tiles an XCD runs at once share G
@@ -225,6 +252,9 @@ __device__ __forceinline__ void gemm_epilogue(const GemmParams& p, accv (&acc)[T
       } else if (act == ACT_GELU_EXACT) {
 #pragma unroll
         for (int q = 0; q < 8; ++q) v[q] = (v[q] * 0.5f) * (1.0f + erff(v[q] * 0.70710678118654752f));
+      } else if (act == ACT_GELU_F32) {
+#pragma unroll
+        for (int q = 0; q < 8; ++q) v[q] = gelu_f32(v[q]);
       }
       if (row < M && (!NOSTORE || v[0] == 1234.5f)) {
         const size_t base = (size_t)row * N + col0;

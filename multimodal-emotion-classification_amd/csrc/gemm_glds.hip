@@ -395,6 +395,9 @@ __device__ __forceinline__ void pp_epilogue(const GemmParams& p, floatx4 (&acc)[
     } else if (act == ACT_GELU_EXACT) {
 #pragma unroll
       for (int e = 0; e < 4; ++e) v[e] = (v[e] * 0.5f) * (1.0f + erff(v[e] * 0.70710678118654752f));
+    } else if (act == ACT_GELU_F32) {
+#pragma unroll
+      for (int e = 0; e < 4; ++e) v[e] = gelu_f32(v[e]);
     }
   };
   const float os = p.oscale;  // 1 except on split operands: fma(acc, 1, b) == acc + b

@@ -68,8 +68,9 @@ enum KernelTag : int {
 // owns a copy, taken from the process defaults when it is created, and kernels read the
 // options of the handle whose call they serve (opt()), so handles never perturb each other.
 // Every setting of a knob gives the same results bit for bit, with these exceptions:
-//   * conv3x3_halo 0 vs 1, fusion_r 4 vs 1|2 and gemm_x3_order 0 vs 1 sum in other fp32 orders
-//     (same values to rounding, not the same bits; include/mec.h);
+//   * conv3x3_halo 0 vs 1, fusion_r 4 vs 1|2 and gemm_x3_order 0 vs 1 sum in other fp32 orders,
+//     gelu_x3 0 vs 1 evaluates erf another way (same values to rounding, not the same bits;
+//     include/mec.h);
 //   * the probe-build values (compiled only with -DMEC_PROBES: they skip work to time a
 //     kernel's parts and return wrong results).
 struct Options {
@@ -120,6 +121,9 @@ struct Options {
   // K-interleaved split engine, per launch class: forced tile (7xxxx), 0 = autotune (BERT FFN1 is
   // pinned to 70256 separately, gemm.hip)
   int gemm_x3_tag[TAG_COUNT] = {0};
+  // fp32x3 BERT FFN1 GELU: 1 = ACT_GELU_F32 (branch-free erf, one-instruction exp; max |error| /
+  // max(|x|, 1) 1.21e-7 against float64, the correctly rounded erf's 1.06e-7), 0 = libm erff
+  int gelu_x3 = 1;
   int fusion_r = 4;         // samples per fusion workgroup
   int fusion_split = 1;     // fusion as 3 launches
   int gemm_debug = 0, conv3x3_debug = 0, stem_debug = 0, audio_debug = 0, speech_debug = 0;  // probe builds only
@@ -209,8 +213,10 @@ struct BlobReader {
 // tensor (conv).
 enum AMode : int { A_PLAIN = 0, A_CONV = 1, A_DUAL = 2 };
 // ACT_GELU: a (4, 3) rational Phi (f16 path, gemm_common.h gelu_rat); ACT_GELU_EXACT: libm erff,
-// x * 0.5 * (1 + erf(x / sqrt2)) as torch's CPU gelu kernel orders it (fp32 path)
-enum Act : int { ACT_NONE = 0, ACT_RELU = 1, ACT_GELU = 2, ACT_RELU6 = 3, ACT_GELU_EXACT = 4 };
+// x * 0.5 * (1 + erf(x / sqrt2)) as torch's CPU gelu kernel orders it (fp32 path); ACT_GELU_F32:
+// the same expression with the library's erf polynomials evaluated branch-free and a one-instruction
+// exp (gemm_common.h gelu_f32; fp32x3 path)
+enum Act : int { ACT_NONE = 0, ACT_RELU = 1, ACT_GELU = 2, ACT_RELU6 = 3, ACT_GELU_EXACT = 4, ACT_GELU_F32 = 5 };
 
 struct GemmParams {
   const void* A = nullptr;   // f16 [M,K] | f16 NHWC [n,H,W,C]

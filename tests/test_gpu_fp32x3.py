@@ -143,7 +143,8 @@ class x3_order:
 
 
 @pytest.mark.parametrize('order', [0, 1])
-@pytest.mark.parametrize('M,N,K,act', [(512, 256, 768, 0), (1000, 768, 3072, 4), (300, 512, 128, 1)])
+@pytest.mark.parametrize('M,N,K,act', [(512, 256, 768, 0), (1000, 768, 3072, 4), (300, 512, 128, 1),
+                                       (1000, 3072, 768, 5)])
 def test_split_gemm_vs_fp64_and_every_tile_bit_identical(dev, M, N, K, act, order):
     """mec_gemm_f16x3 (the fp32x3 engine) against float64 A . B^T of the fp32 operands: within the
     fp32 GEMM engine's bar (2e-6 x sum |a b|, tests/test_gpu_fp32.py), with the weights pre-scaled
@@ -174,7 +175,7 @@ def _split_gemm_tiles(dev, lib, M, N, K, act, order):
         ref = ref + R
     if act == 1:
         ref = np.maximum(ref, 0)
-    elif act == 4:
+    elif act in (4, 5):  # 5: the branch-free erf GELU of the fp32x3 FFN1 (gemm_common.h gelu_f32)
         from scipy.special import erf
         ref = 0.5 * ref * (1 + erf(ref / np.sqrt(2)))
     bound = 2e-6 * (np.abs(A).astype(np.float64) @ np.abs(Bw).astype(np.float64).T + np.abs(bias) + 1)
