@@ -284,6 +284,17 @@ __global__ __launch_bounds__(512, 1) void stem_pool_gray_x3_kernel(const uint8_t
     patch_load(blockIdx.x, pv);
     patch_store(pv);
   }
+  // the B operands for the launch, in registers: nt[q] = (wave + 8 q) & 1 is the same for every q,
+  // so a lane needs one (lo, hi) pair of half4 per k-step (52 VGPRs) instead of 8 two-byte LDS
+  // reads per MFMA pair inside the tile loop
+  __syncthreads();  // swh / swl complete
+  half4 wl[13], wh[13];
+#pragma unroll
+  for (int st = 0; st < 13; ++st) {
+    const int w0 = ((4 * st + 2 * kk) * 2) * 64 + nt[0] * 32 + li;  // [tap t0][ch 0][co]
+    wl[st] = half4{swl[w0], swl[w0 + 64], swl[w0 + 128], swl[w0 + 192]};
+    wh[st] = half4{swh[w0], swh[w0 + 64], swh[w0 + 128], swh[w0 + 192]};
+  }
   for (int t = blockIdx.x; t < ntiles; t += gridDim.x) {
     const int b = t / 49, tt = t - (t / 49) * 49;
     const int py0 = (tt / 7) * 8, px0 = (tt - (tt / 7) * 7) * 8;
@@ -303,11 +314,8 @@ __global__ __launch_bounds__(512, 1) void stem_pool_gray_x3_kernel(const uint8_t
           const hpair p0 = tin[st][0] ? patch[base[q] + toff[st][0]] : hpair{(f16)0.f, (f16)0.f};
           const hpair p1 = tin[st][1] ? patch[base[q] + toff[st][1]] : hpair{(f16)0.f, (f16)0.f};
           const half4 av = {p0.x, p0.y, p1.x, p1.y};
-          const int w0 = ((4 * st + 2 * kk) * 2) * 64 + nt[q] * 32 + li;  // [tap t0][ch 0][co]
-          const half4 bl = {swl[w0], swl[w0 + 64], swl[w0 + 128], swl[w0 + 192]};
-          const half4 bh = {swh[w0], swh[w0 + 64], swh[w0 + 128], swh[w0 + 192]};
-          acc[q] = __builtin_amdgcn_mfma_f32_32x32x8f16(av, bl, acc[q], 0, 0, 0);
-          acc[q] = __builtin_amdgcn_mfma_f32_32x32x8f16(av, bh, acc[q], 0, 0, 0);
+          acc[q] = __builtin_amdgcn_mfma_f32_32x32x8f16(av, wl[st], acc[q], 0, 0, 0);
+          acc[q] = __builtin_amdgcn_mfma_f32_32x32x8f16(av, wh[st], acc[q], 0, 0, 0);
         }
       }
     }
