@@ -456,6 +456,9 @@ def run(a, precision, B, world, rank, dev, inputs):
                                + (' (BASELINE configs[3])' if world == 1 and B == 256 else
                                   ' (BASELINE configs[4] per-rank shard)' if B == 1024 else ''),
                    'batch_per_gpu': B, 'global_batch': world * B, 'seq_len': 128,
+                   # BASELINE.json's metric string names batch 256 (configs[3]); at N > 1 each rank
+                   # runs batch_per_gpu samples (configs[4]: 8192 over 8 GPUs)
+                   'metric_batch_note': None if B == 256 else f'metric string names batch 256; this run: {B} per GPU',
                    'parallelism': f'dp{world} (sample-sharded, all-gather of 34-float rows)'},
         'achieved_tflops_whole_step': flop / el / 1e12,
         'whole_step_frac_of_peak': flop * mf / el / 1e12 / peak,
