@@ -17,6 +17,7 @@ from . import _lib, synthetic
 from ._lib import MecError
 
 TAG_BERT_FFN2 = 5  # launch class of BERT's FFN2 GEMM (mec_common.h Tag)
+TAG_BERT_QKV = 1  # ... and of its QKV GEMM
 
 KINDS = synthetic.KIND_IDS
 
@@ -337,6 +338,10 @@ class FusedPipeline:
             # tools/gpu_ab_x3tags.sh, profiles/r03_ab_x3tag_ffn2.txt; the O-projection pinned the
             # same way measured within 0.3 %). Every interleaved tile gives the same bits.
             self.text.set_option('gemm_x3_tag', TAG_BERT_FFN2 * 100000 + 70256)
+            # QKV (N = 2304: 1152 tiles, 4.5 rounds) on the same tile, which the autotuner picks alone
+            # too but not on every run: 25.45 vs 25.58 ms per step autotuned, 256 x 128 / 128 x 128
+            # 25.95 / 25.86 (profiles/r03_ab_x3tag_qkv.txt)
+            self.text.set_option('gemm_x3_tag', TAG_BERT_QKV * 100000 + 70256)
 
     def forward(self, x_speech, ids, mask, gray, epilogue=None):
         """One batch through the path -> dict of per-modality and fusion outputs (and, with
