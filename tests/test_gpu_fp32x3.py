@@ -225,18 +225,24 @@ def _split_vs_exact(dev, lib, M, N, K, order):
     ref = A.astype(np.float64) @ W.astype(np.float64).T
     st = ctypes.c_void_p(torch.cuda.current_stream(dev).cuda_stream)
     p = lambda t: ctypes.c_void_p(t.data_ptr())  # noqa: E731
-    C32 = torch.empty((M, N), device=dev)
-    _lib.check(lib.mec_gemm_f32(p(torch.from_numpy(A).to(dev)), p(torch.from_numpy(W).to(dev)), None, None, p(C32),
-                                M, N, K, 0, st), 'mec_gemm_f32')
+    # device operands held in locals until the launches have completed (a temporary passed as a raw
+    # pointer is freed on return and its block handed to the next allocation)
+    Ad, Wd = torch.from_numpy(A).to(dev), torch.from_numpy(W).to(dev)
     e = float(np.ceil(np.log2(16384 / np.abs(W).max())) - 1)
+    Axd, Wxd = torch.from_numpy(_split(A)).to(dev), torch.from_numpy(_split(W, 2.0 ** e)).to(dev)
+    C32 = torch.empty((M, N), device=dev)
+    _lib.check(lib.mec_gemm_f32(p(Ad), p(Wd), None, None, p(C32), M, N, K, 0, st), 'mec_gemm_f32')
     Cx = torch.empty((M, N), device=dev)
-    _lib.check(lib.mec_gemm_f16x3(p(torch.from_numpy(_split(A)).to(dev)), M * K,
-                                  p(torch.from_numpy(_split(W, 2.0 ** e)).to(dev)), N * K, ctypes.c_float(2.0 ** -e),
+    _lib.check(lib.mec_gemm_f16x3(p(Axd), M * K, p(Wxd), N * K, ctypes.c_float(2.0 ** -e),
                                   None, None, None, 0, p(Cx), M, N, K, 0, st), 'mec_gemm_f16x3')
+    torch.cuda.synchronize()
     e32 = np.abs(C32.cpu().numpy() - ref)
     ex3 = np.abs(Cx.cpu().numpy() - ref)
     print(f'{M}x{N}x{K}: exact-fp32 engine max {e32.max():.3g} rms {np.sqrt((e32 ** 2).mean()):.3g}; '
           f'split-f16 engine (order {order}) max {ex3.max():.3g} rms {np.sqrt((ex3 ** 2).mean()):.3g}')
+    # both engines within the fp32 GEMM bar (so the comparison below has a sound reference)
+    bound = 2e-6 * (np.abs(A).astype(np.float64) @ np.abs(W).astype(np.float64).T + 1)
+    assert (e32 <= bound).all() and (ex3 <= bound).all()
     assert ex3.max() <= 1.5 * e32.max()
 
 
