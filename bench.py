@@ -27,7 +27,7 @@ twice the measured probs error), the fused output checked end to end against o_f
 At N>1 rank 0 also checks two gathered rows of EVERY rank against the oracle run on that rank's
 inputs (the all-gather's order and content).
 
-    python bench.py [--gpus N] [--steps K] [--warmup W] [--batch B] [--precision both|f16|fp32]
+    python bench.py [--gpus N] [--steps K] [--warmup W] [--batch B] [--precision all|both|fp32x3|fp32|f16]
 
 With --gpus N > 1 and no WORLD_SIZE in the environment, bench.py starts
 `python -m torch.distributed.run --nproc-per-node N ... bench.py` as a child process BEFORE any
@@ -98,7 +98,8 @@ def parse(argv=None):
     ap.add_argument('--warmup', type=int, default=3)
     ap.add_argument('--batch', type=int, default=0, help='samples per rank (default 256 at N=1, 1024 at N>1)')
     ap.add_argument('--precision', default='all', choices=['all', 'both', 'f16', 'fp32', 'fp32x3'],
-                    help="all: fp32 (headline) + f16 + fp32x3 (nested); both: fp32 + f16")
+                    help='all: fp32x3 (headline) + fp32 exact + f16 (nested); both: fp32 (headline) + f16; '
+                         'or one precision')
     ap.add_argument('--no-cpu-baseline', action='store_true')
     ap.add_argument('--no-parity', action='store_true')
     ap.add_argument('--oracle-rows', type=int, default=256,
@@ -160,60 +161,113 @@ def parity_rows(B: int, limit: int):
 
 def host_cpus():
     """(threads usable by this process, physical cores of the host, logical CPUs in the
-    affinity mask). The GPU box shares a many-core host; its share is OMP_NUM_THREADS (16)."""
-    avail = len(os.sched_getaffinity(0))
+    affinity mask, physical cores in the affinity mask). The GPU box shares a many-core host; its
+    share is OMP_NUM_THREADS (16)."""
+    mask = os.sched_getaffinity(0)
+    avail = len(mask)
     try:
         threads = min(avail, int(os.environ.get('OMP_NUM_THREADS', avail)))
     except ValueError:
         threads = avail
-    phys = set()
+    phys, phys_mask = set(), set()
     try:
-        pid = None
+        cpu = pid = None
         with open('/proc/cpuinfo') as fh:
             for line in fh:
-                if line.startswith('physical id'):
+                if line.startswith('processor'):
+                    cpu = int(line.split(':')[1])
+                elif line.startswith('physical id'):
                     pid = line.split(':')[1].strip()
                 elif line.startswith('core id'):
-                    phys.add((pid, line.split(':')[1].strip()))
-    except OSError:
+                    core = (pid, line.split(':')[1].strip())
+                    phys.add(core)
+                    if cpu in mask:
+                        phys_mask.add(core)
+    except (OSError, ValueError):
         pass
-    return threads, (len(phys) or None), avail
+    return threads, (len(phys) or None), avail, (len(phys_mask) or None)
+
+
+# BERT's executed work per sample when the last layer runs on the [CLS] rows only (bert_cls_last,
+# DESIGN.md §4): K / V for every token, Q / O-projection / FFN for the [CLS] row, and the [CLS]
+# attention kernel's 32 query rows (it runs the full kernel's instruction sequence for queries 0..31)
+_BERT_LAYER_MAC = 128 * 768 * 2304 + 2 * 128 * 128 * 768 + 128 * 768 * 768 + 2 * 128 * 768 * 3072
+_BERT_CLS_LAYER_MAC = 128 * 768 * 1536 + 768 * 768 + 2 * 32 * 128 * 768 + 768 * 768 + 2 * 768 * 3072
+EXEC_FLOP_PER_SAMPLE = dict(FLOP_PER_SAMPLE, text=FLOP_PER_SAMPLE['text'] - 2 * (_BERT_LAYER_MAC - _BERT_CLS_LAYER_MAC))
+
+
+def _oracle_chain(w, x, ids, mask, gray, sel, times=None):
+    """The oracle chain on rows `sel`: per modality (feat, logits, probs) and the fused chain
+    o_f(o_s, o_t, o_i) (inference/multimodal_fusion.py:271-278); `times` collects per-modality
+    seconds."""
+    from oracle import fusion as o_f, image as o_i, speech as o_s, text as o_t
+    t = [time.perf_counter()]
+    rs = o_s.forward(w['speech'], x[sel])
+    t.append(time.perf_counter())
+    rt = o_t.forward(w['text'], ids[sel], mask[sel])
+    t.append(time.perf_counter())
+    ri = o_i.forward(w['image'], gray[sel])
+    t.append(time.perf_counter())
+    rf = o_f.forward(w['fusion'], rs[0], rt[0], ri[0], rs[2], rt[2], ri[2])
+    t.append(time.perf_counter())
+    if times is not None:
+        for k, (a, b) in zip(('speech', 'text', 'image', 'fusion'), zip(t, t[1:])):
+            times.setdefault(k, []).append(b - a)
+        times.setdefault('fused', []).append(t[-1] - t[0])
+    return {'speech': rs, 'text': rt, 'image': ri, 'fusion': rf}
+
+
+CPU_SAMPLE_ROWS, CPU_PASSES = 32, 3
 
 
 def oracle_run(x, ids, mask, gray, rows, timed: bool):
     """The CPU oracle (fp32 torch-CPU / numpy restatement of the reference arithmetic) on `rows`
-    of the batch: per modality (feat, logits, probs) and the fused chain o_f(o_s, o_t, o_i)
-    (inference/multimodal_fusion.py:271-278). timed=True also returns the cpu_baseline record:
-    one warm-up pass on 2 rows, then ONE timed pass over all `rows`."""
+    of the batch: the parity reference (one pass). timed=True also returns the cpu_baseline record
+    (BASELINE.md): the oracle chain on a bounded sample (the first CPU_SAMPLE_ROWS
+    rows of the timed batch), after a 2-row warm-up, CPU_PASSES timed passes -> median, at
+    torch threads = OMP_NUM_THREADS (the box's CPU share for one GPU: `value`) and again at the
+    physical cores in the affinity mask; per-modality rates at both."""
     sys.path.insert(0, ROOT)
     from mec import synthetic as syn
-    from oracle import fusion as o_f, image as o_i, speech as o_s, text as o_t
-    threads, phys, avail = host_cpus()
+    threads, phys, avail, phys_mask = host_cpus()
     prev = torch.get_num_threads()
-    torch.set_num_threads(threads)
     w = {k: syn.weights(k) for k in ('speech', 'text', 'image', 'fusion')}
     r = np.asarray(rows)
-
-    def chain(sel):
-        rs = o_s.forward(w['speech'], x[sel])
-        rt = o_t.forward(w['text'], ids[sel], mask[sel])
-        ri = o_i.forward(w['image'], gray[sel])
-        rf = o_f.forward(w['fusion'], rs[0], rt[0], ri[0], rs[2], rt[2], ri[2])
-        return {'speech': rs, 'text': rt, 'image': ri, 'fusion': rf}
-
+    torch.set_num_threads(threads)
+    t0 = time.perf_counter()
+    ref = _oracle_chain(w, x, ids, mask, gray, r)
+    ref_s = time.perf_counter() - t0
     cb = None
     if timed:
-        chain(r[:2])
-        t0 = time.perf_counter()
-    ref = chain(r)
-    if timed:
-        el = time.perf_counter() - t0
-        cb = {'value': len(r) / el, 'unit': 'fused samples/s', 'cores': threads, 'kind': 'port',
-              'sample': f'one fused batch of {len(r)} samples (L=128 full rows, 48x48 u8) through oracle/ '
-                        f'fp32 torch-CPU, after a 2-sample warm-up ({el:.1f} s)',
-              'threads_note': 'torch threads = OMP_NUM_THREADS, the CPU share the GPU box gives one GPU '
-                              '(the host itself has more cores: host_physical_cores)',
-              'host_physical_cores': phys, 'host_logical_cpus_in_affinity': avail}
+        sample = np.arange(min(CPU_SAMPLE_ROWS, len(x)))
+        runs = {}
+        counts = [threads] + ([phys_mask] if phys_mask and phys_mask != threads else [])
+        for nt in counts:
+            torch.set_num_threads(nt)
+            _oracle_chain(w, x, ids, mask, gray, sample[:2])  # warm-up
+            times = {}
+            for _ in range(CPU_PASSES):
+                _oracle_chain(w, x, ids, mask, gray, sample, times)
+            med = {k: float(np.median(v)) for k, v in times.items()}
+            runs[nt] = {'fused_samples_per_s': len(sample) / med['fused'],
+                        'per_modality_samples_per_s': {k: len(sample) / med[k] for k in ('speech', 'text', 'image', 'fusion')},
+                        'median_pass_s': med['fused'], 'passes_s': [round(v, 3) for v in times['fused']]}
+        head = runs[threads]
+        cb = {'value': head['fused_samples_per_s'], 'unit': 'fused samples/s', 'cores': threads, 'kind': 'port',
+              'sample': f'the first {len(sample)} samples of the timed batch (L=128 full rows, 48x48 u8) through '
+                        f'oracle/ (fp32 torch-CPU restatement: speech DNN, BERT, ResNet50, fusion), 2-sample warm-up, '
+                        f'median of {CPU_PASSES} passes',
+              'per_modality_samples_per_s': head['per_modality_samples_per_s'],
+              'median_pass_s': head['median_pass_s'], 'passes_s': head['passes_s'],
+              'threads_note': 'cores = torch threads = OMP_NUM_THREADS, the CPU share the GPU box gives one GPU; '
+                              '`at_physical_cores_in_affinity_mask` repeats the sample on every physical core '
+                              'this process may run on',
+              'at_physical_cores_in_affinity_mask': ({'cores': phys_mask, **runs[phys_mask]}
+                                                     if phys_mask in runs and phys_mask != threads else None),
+              'parity_pass': {'rows': len(r), 'seconds': ref_s, 'fused_samples_per_s': len(r) / ref_s,
+                              'cores': threads},
+              'host_physical_cores': phys, 'host_logical_cpus_in_affinity': avail,
+              'host_physical_cores_in_affinity': phys_mask}
     torch.set_num_threads(prev)
     return ref, cb
 
@@ -446,6 +500,7 @@ def run(a, precision, B, world, rank, dev, inputs):
                                    'vs_f16_peak_over_3': fp32_eq / (peak / mf)}
     total = world * B * a.steps
     flop = sum(FLOP_PER_SAMPLE.values()) * total
+    flop_exec = sum(EXEC_FLOP_PER_SAMPLE.values()) * total
     res = {
         'metric': METRIC,
         'value': total / el, 'unit': 'samples/s', 'n_gpus': world, 'steps': a.steps, 'warmup': a.warmup,
@@ -462,6 +517,14 @@ def run(a, precision, B, world, rank, dev, inputs):
                    'parallelism': f'dp{world} (sample-sharded, all-gather of 34-float rows)'},
         'achieved_tflops_whole_step': flop / el / 1e12,
         'whole_step_frac_of_peak': flop * mf / el / 1e12 / peak,
+        # the same step counted by what the GPU executes: BERT's last layer on the [CLS] rows only
+        'achieved_tflops_whole_step_executed': flop_exec / el / 1e12,
+        'whole_step_frac_of_peak_executed': flop_exec * mf / el / 1e12 / peak,
+        'flop_per_sample': {'reference_count': sum(FLOP_PER_SAMPLE.values()),
+                            'executed': sum(EXEC_FLOP_PER_SAMPLE.values()),
+                            'note': 'reference_count: the reference forward per sample (BERT 12 full layers, '
+                                    'ResNet50, speech, fusion); executed: BERT last layer [CLS]-only '
+                                    '(bert_cls_last), other encoders as counted'},
         'roofline': roof,
     }
     if world > 1:
@@ -512,6 +575,7 @@ def main_gpu(a, world, rank, local):
                 f = lines[p]
                 head[key] = {k: f[k] for k in ('value', 'unit', 'ms_per_step', 'dtype',
                                                'achieved_tflops_whole_step', 'whole_step_frac_of_peak',
+                                               'achieved_tflops_whole_step_executed',
                                                'roofline', 'parity', 'per_config', 'distributed') if k in f}
         print(json.dumps(head), flush=True)
         if a.json_out:

@@ -152,6 +152,7 @@ int mec_create_ex(int kind, const float* host_blob, size_t n, int device, int pr
     impl->kind = kind;
     impl->device = device;
     impl->prec = (kind == KIND_SPEECH || kind == KIND_FUSION || kind == KIND_AUDIO) ? MEC_PREC_FP32 : precision;
+    if (impl->prec == PREC_FP32X3 && impl->alloc_range_flag() != 0) { delete impl; return -1; }
     *out = new mec_model{impl};
     return 0;
   })
@@ -169,7 +170,7 @@ int mec_speech_fwd(mec_model* m, const float* x, int B, float* feat, float* logi
   API_GUARD({
     auto* p = as<SpeechModel>(m, KIND_SPEECH);
     if (!p) return -1;
-    OptScope sc(&p->opts, &p->tune);
+    OptScope sc(&p->opts, &p->tune, p->range_dev);
     return p->forward(x, B, feat, logits, probs, S(stream));
   })
 }
@@ -179,7 +180,7 @@ int mec_text_fwd(mec_model* m, const int32_t* ids, const int32_t* mask, int B, i
   API_GUARD({
     auto* p = as<TextModel>(m, KIND_TEXT);
     if (!p) return -1;
-    OptScope sc(&p->opts, &p->tune);
+    OptScope sc(&p->opts, &p->tune, p->range_dev);
     return p->forward(ids, mask, B, L, cls, logits, probs, S(stream));
   })
 }
@@ -189,7 +190,7 @@ int mec_image_fwd(mec_model* m, const uint8_t* gray, int B, float* feat, float* 
   API_GUARD({
     auto* p = image_net(m);
     if (!p) return -1;
-    OptScope sc(&p->opts, &p->tune);
+    OptScope sc(&p->opts, &p->tune, p->range_dev);
     return p->forward(gray, B, feat, logits, probs, S(stream));
   })
 }
@@ -199,7 +200,7 @@ int mec_image_fwd_u8(mec_model* m, const uint8_t* img, int B, int H, int W, int 
   API_GUARD({
     auto* p = image_net(m);
     if (!p) return -1;
-    OptScope sc(&p->opts, &p->tune);
+    OptScope sc(&p->opts, &p->tune, p->range_dev);
     return p->forward_u8(img, B, H, W, C, feat, logits, probs, S(stream));
   })
 }
@@ -210,7 +211,7 @@ int mec_fusion_fwd(mec_model* m, const float* s_feat, const float* t_feat, const
   API_GUARD({
     auto* p = as<FusionModel>(m, KIND_FUSION);
     if (!p) return -1;
-    OptScope sc(&p->opts, &p->tune);
+    OptScope sc(&p->opts, &p->tune, p->range_dev);
     return p->forward(s_feat, t_feat, i_feat, s_pred, t_pred, i_pred, B, logits, probs, attn_w, dec_w, S(stream));
   })
 }
@@ -219,7 +220,7 @@ int mec_audio_fwd(mec_model* m, const float* wave, int B, int n_samples, float* 
   API_GUARD({
     auto* p = as<AudioModel>(m, KIND_AUDIO);
     if (!p) return -1;
-    OptScope sc(&p->opts, &p->tune);
+    OptScope sc(&p->opts, &p->tune, p->range_dev);
     return p->forward(wave, B, n_samples, feat, tuning, S(stream));
   })
 }

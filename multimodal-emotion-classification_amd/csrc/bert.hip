@@ -32,8 +32,9 @@ __global__ __launch_bounds__(256) void bert_embed_ln_kernel(const int32_t* __res
                                                             const float* __restrict__ type,
                                                             const float* __restrict__ g,
                                                             const float* __restrict__ b, float* h32,
-                                                            f16* h16, long long lo) {
-  // lo != 0 (the fp32x3 path): h16 is a hi plane and h16 + lo the lo plane, f16(y - hi)
+                                                            f16* h16, long long lo, unsigned* flag) {
+  // lo != 0 (the fp32x3 path): h16 is a hi plane and h16 + lo the lo plane, f16(y - hi); a value
+  // outside the f16 range raises `flag` (x3_raise)
   const int lane = threadIdx.x & 63;
   const int row = blockIdx.x * 4 + (threadIdx.x >> 6);
   if (row >= M) return;
@@ -77,6 +78,7 @@ __global__ __launch_bounds__(256) void bert_embed_ln_kernel(const int32_t* __res
         half4 hl = {(f16)(o.x - (float)hh[0]), (f16)(o.y - (float)hh[1]), (f16)(o.z - (float)hh[2]),
                     (f16)(o.w - (float)hh[3])};
         *reinterpret_cast<half4*>(h16 + lo + (size_t)row * BH + c) = hl;
+        x3_raise(flag, x3_out_of_range4(o));
       }
     }
   }
@@ -89,7 +91,8 @@ template <int RW>
 __global__ __launch_bounds__(256) void bert_layernorm_kernel(const float* x, int M,
                                                              const float* __restrict__ g,
                                                              const float* __restrict__ b, float* h32,
-                                                             f16* h16, float2* stats, long long lo) {
+                                                             f16* h16, float2* stats, long long lo,
+                                                             unsigned* flag) {
   // h32 may be null: the consumer of the f32 output (the next residual add) then
   // re-derives it from x and `stats` in its GEMM epilogue (GemmParams::r_stats)
   const int lane = threadIdx.x & 63;
@@ -138,10 +141,11 @@ __global__ __launch_bounds__(256) void bert_layernorm_kernel(const float* x, int
       if (h16) {  // null on the fp32 path
         half4 hh = {(f16)o.x, (f16)o.y, (f16)o.z, (f16)o.w};
         *reinterpret_cast<half4*>(h16 + (size_t)row * BH + c) = hh;
-        if (lo) {  // fp32x3 path: the lo plane
+        if (lo) {  // fp32x3 path: the lo plane (and the range guard)
           half4 hl = {(f16)(o.x - (float)hh[0]), (f16)(o.y - (float)hh[1]), (f16)(o.z - (float)hh[2]),
                       (f16)(o.w - (float)hh[3])};
           *reinterpret_cast<half4*>(h16 + lo + (size_t)row * BH + c) = hl;
+          x3_raise(flag, x3_out_of_range4(o));
         }
       }
     }
@@ -150,12 +154,13 @@ __global__ __launch_bounds__(256) void bert_layernorm_kernel(const float* x, int
 
 static void launch_ln_rows(const float* x, int M, const float* g, const float* b, float* h32, f16* h16, float2* st,
                            hipStream_t s, long long lo = 0) {
+  unsigned* fl = lo ? range_flag() : nullptr;
   if (opt().bert_ln_rows == 4)
-    hipLaunchKernelGGL(bert_layernorm_kernel<4>, dim3((M + 15) / 16), dim3(256), 0, s, x, M, g, b, h32, h16, st, lo);
+    hipLaunchKernelGGL(bert_layernorm_kernel<4>, dim3((M + 15) / 16), dim3(256), 0, s, x, M, g, b, h32, h16, st, lo, fl);
   else if (opt().bert_ln_rows == 2)
-    hipLaunchKernelGGL(bert_layernorm_kernel<2>, dim3((M + 7) / 8), dim3(256), 0, s, x, M, g, b, h32, h16, st, lo);
+    hipLaunchKernelGGL(bert_layernorm_kernel<2>, dim3((M + 7) / 8), dim3(256), 0, s, x, M, g, b, h32, h16, st, lo, fl);
   else
-    hipLaunchKernelGGL(bert_layernorm_kernel<1>, dim3((M + 3) / 4), dim3(256), 0, s, x, M, g, b, h32, h16, st, lo);
+    hipLaunchKernelGGL(bert_layernorm_kernel<1>, dim3((M + 3) / 4), dim3(256), 0, s, x, M, g, b, h32, h16, st, lo, fl);
 }
 
 // Host launchers (also used by the fp32 path, bert_f32.hip). One wave per token row.
@@ -167,7 +172,7 @@ int launch_bert_embed_ln(const int32_t* ids, int M, int L, const float* emb, flo
   const float* lng = type + 2 * BH;
   const float* lnb = lng + BH;
   hipLaunchKernelGGL(bert_embed_ln_kernel, dim3((M + 3) / 4), dim3(256), 0, s, ids, M, L, word, pos, type, lng, lnb,
-                     h32, h16, lo);
+                     h32, h16, lo, lo ? range_flag() : nullptr);
   MEC_LAUNCH_CHECK();
   return 0;
 }
@@ -851,7 +856,7 @@ int TextModel::forward(const int32_t* ids, const int32_t* mask, int B, int L, fl
   const float* lnb = lng + BH;
   const dim3 rows_grid((M + 3) / 4);
   hipLaunchKernelGGL(bert_embed_ln_kernel, rows_grid, dim3(256), 0, s, ids, M, L, word, pos, type, lng, lnb, h32,
-                     h16, 0LL);
+                     h16, 0LL, nullptr);
   MEC_LAUNCH_CHECK();
   const f16* W = wts.as<f16>();
   const float* P = prm.as<float>();

@@ -19,7 +19,9 @@ constexpr int GBK = 64;
 // inside the encoder 128 x 128 is the fastest (text 8.22 ms vs 8.43 with 256 x 128 / 4 waves;
 // fused step 11.40 vs 11.48 ms).
 
-int launch_gemm(const GemmParams& p, hipStream_t s, Prof* prof, int tag) {
+int launch_gemm(const GemmParams& p0, hipStream_t s, Prof* prof, int tag) {
+  GemmParams p = p0;
+  if (p.c_lo && !p.ovf) p.ovf = range_flag();  // split output: the calling handle's range flag
   MEC_REQUIRE(p.M > 0 && p.N > 0 && p.K > 0, "gemm: empty shape");
   MEC_REQUIRE(p.N % 64 == 0, "gemm: N % 64 != 0");
   MEC_REQUIRE(p.K % GBK == 0, "gemm: K % 64 != 0");

@@ -141,6 +141,7 @@ __device__ __forceinline__ void gemm_epilogue(const GemmParams& p, accv (&acc)[T
     for (int q = 0; q < 8; ++q) { lng[q] = p.r_g[col0 + q]; lnb[q] = p.r_b[col0 + q]; }
   }
   constexpr int SLABS = TM / 32;
+  bool x3bad = false;  // split output left the f16 range (raised once, after the slabs)
 #pragma unroll
   for (int i = 0; i < SLABS; ++i) {
     if constexpr (MF == 32) {
@@ -266,7 +267,10 @@ __device__ __forceinline__ void gemm_epilogue(const GemmParams& p, accv (&acc)[T
           if (p.c_lo) {  // split output: the lo plane carries v - hi
             half8 l;
 #pragma unroll
-            for (int q = 0; q < 8; ++q) l[q] = (f16)(v[q] - (float)h[q]);
+            for (int q = 0; q < 8; ++q) {
+              l[q] = (f16)(v[q] - (float)h[q]);
+              x3bad |= x3_out_of_range(v[q]);
+            }
             *reinterpret_cast<half8*>(p.C16 + p.c_lo + base) = l;
           }
         }
@@ -278,6 +282,7 @@ __device__ __forceinline__ void gemm_epilogue(const GemmParams& p, accv (&acc)[T
     }
     asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
   }
+  if (p.c_lo) x3_raise(p.ovf, x3bad);
 }
 
 }  // namespace mec

@@ -337,12 +337,13 @@ int launch_gemm_f32(const GemmParams& p, hipStream_t s, Prof* prof, int tag) {
   }
   if (!id) {
     hipStreamCaptureStatus cs = hipStreamCaptureStatusNone;
-    if (opt().gemm_autotune && hipStreamIsCapturing(s, &cs) == hipSuccess && cs == hipStreamCaptureStatusNone) {
+    const bool capturing = !(hipStreamIsCapturing(s, &cs) == hipSuccess && cs == hipStreamCaptureStatusNone);
+    if (opt().gemm_autotune && !capturing) {
       MEC_TRY(tune_tile(p, s, &id));
     } else {
       id = heuristic_tile(p);
     }
-    tune_cache().put(key, id);
+    if (!capturing) tune_cache().put(key, id);  // inside capture: untimed, so not cached
     if (getenv("MEC_GEMM_TRACE"))
       fprintf(stderr, "MEC_GEMM_F32 amode=%d M=%d N=%d K=%d H=%d C=%d ks=%d stride=%d act=%d R=%d tile=%d\n", p.amode,
               p.M, p.N, p.K, p.H, p.C, p.ks, p.stride, p.act, p.R != nullptr, id);

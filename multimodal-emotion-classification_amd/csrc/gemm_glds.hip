@@ -429,6 +429,7 @@ __device__ __forceinline__ void pp_epilogue(const GemmParams& p, floatx4 (&acc)[
   }
   // f32 slabs: lane -> row (lane >> 4) of each 4-row group, 16-B chunk (lane & 15) = 4 features
   const int sc = lane & 15, col = cw0 + sc * 4;
+  bool x3bad = false;  // split output left the f16 range (raised once, after the slabs)
   float4 g4 = make_float4(0.f, 0.f, 0.f, 0.f), b4 = g4;
   if (p.r_stats) {
     g4 = *reinterpret_cast<const float4*>(p.r_g + col);
@@ -496,7 +497,10 @@ __device__ __forceinline__ void pp_epilogue(const GemmParams& p, floatx4 (&acc)[
           if (p.c_lo) {  // split output: the lo plane carries v - hi
             half4 l;
 #pragma unroll
-            for (int e = 0; e < 4; ++e) l[e] = (f16)(v[e] - (float)h[e]);
+            for (int e = 0; e < 4; ++e) {
+              l[e] = (f16)(v[e] - (float)h[e]);
+              x3bad |= x3_out_of_range(v[e]);
+            }
             *reinterpret_cast<half4*>(p.C16 + p.c_lo + base) = l;
           }
         }
@@ -505,6 +509,7 @@ __device__ __forceinline__ void pp_epilogue(const GemmParams& p, floatx4 (&acc)[
     }
     asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
   }
+  if (p.c_lo) x3_raise(p.ovf, x3bad);
 }
 
 // ---- 256x256x64 ping-pong GEMM (A_PLAIN), v_mfma_f32_16x16x32_f16, 8 waves (2 x 4).
@@ -911,8 +916,16 @@ static int launch_bn(const GemmParams& p, hipStream_t s, int id) {
   }
 }
 
+// Untuned tile (gemm_autotune 0, or a first launch inside graph capture). K-interleaved split
+// operands take only the 7xxxx tiles: every one of them sums in the same k order, so this choice,
+// like the autotuner's, changes speed only.
 static int heuristic_bn(const GemmParams& p) {
   const long nbm = (p.M + 255) / 256;
+  if (p.split == 2) {
+    if (p.N % 256 == 0 && nbm * (p.N / 256) >= 256) return 70256;
+    if (p.N % 128 == 0) return 71128;
+    return 71064;
+  }
   if (p.N % 256 == 0 && nbm * (p.N / 256) >= 4 * 256 && p.K >= 768) return 256;
   if (p.N % 128 == 0 && p.K >= 1024) return 128;
   if (p.N % 128 == 0 && p.K <= 64) return 128;
@@ -929,7 +942,7 @@ static int tune_bn(const GemmParams& p, hipStream_t s, int* out_bn) {
   hipEvent_t ev[REPS + 1];
   for (auto& e : ev) MEC_HIP(hipEventCreate(&e));
   float best = 1e30f;
-  int best_bn = p.split == 2 ? 71064 : heuristic_bn(p);
+  int best_bn = heuristic_bn(p);
   const int* cb = p.split == 2 ? cands_x3i : cands;
   const int nc = p.split == 2 ? (int)(sizeof(cands_x3i) / sizeof(int)) : (int)(sizeof(cands) / sizeof(int));
   for (int ci = 0; ci < nc; ++ci) {
@@ -971,12 +984,16 @@ int launch_gemm_glds(const GemmParams& p0, hipStream_t s, int force_bn) {
   int bn = tune_cache().find(key);
   if (!bn) {
     hipStreamCaptureStatus cs = hipStreamCaptureStatusNone;
-    if (opt().gemm_autotune && hipStreamIsCapturing(s, &cs) == hipSuccess && cs == hipStreamCaptureStatusNone) {
+    const bool capturing = !(hipStreamIsCapturing(s, &cs) == hipSuccess && cs == hipStreamCaptureStatusNone);
+    if (opt().gemm_autotune && !capturing) {
       MEC_TRY(tune_bn(p, s, &bn));
+      tune_cache().put(key, bn);
     } else {
       bn = heuristic_bn(p);
+      // a launch inside graph capture cannot time tiles: it runs the heuristic tile without caching
+      // it, so the first launch outside capture still tunes the shape (same bits either way)
+      if (!capturing) tune_cache().put(key, bn);
     }
-    tune_cache().put(key, bn);
     if (getenv("MEC_GEMM_TRACE"))  // one line per distinct shape, at its first launch
       fprintf(stderr, "MEC_GEMM amode=%d M=%d N=%d K=%d H=%d C=%d ks=%d stride=%d act=%d R=%d r_f32=%d split=%d tile=%d\n",
               p.amode, p.M, p.N, p.K, p.H, p.C, p.ks, p.stride, p.act, p.R != nullptr, p.r_f32, p.split, bn);

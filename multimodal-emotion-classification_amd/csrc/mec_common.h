@@ -156,12 +156,29 @@ Options& default_options();      // process defaults (mec_set_option), copied in
 TuneCache& default_tune_cache(); // for the handle-less kernel entry points
 const Options& opt();            // options of the handle the calling thread is serving
 TuneCache& tune_cache();         // its autotune cache
+// its fp32x3 range flag (device view of a host-mapped word; null on other precisions): raised by
+// every kernel that writes an activation as f16 hi / lo planes when a value leaves the f16 range,
+// reported by mec_model_check
+unsigned* range_flag();
 struct OptScope {                // set for the duration of one C-ABI call on a handle
   const Options* po;
   TuneCache* pt;
-  OptScope(const Options* o, TuneCache* t);
+  unsigned* pf;
+  OptScope(const Options* o, TuneCache* t, unsigned* flag = nullptr);
   ~OptScope();
 };
+
+// fp32x3 range guard. An activation x is carried as hi = f16(x), lo = f16(x - hi): |x| >= 65520
+// rounds hi to inf (hi + lo = NaN downstream), and a NaN / inf input is no fp32 value either. Any
+// such value raises the handle's flag (a vector store of 1; only on that rare path), so the
+// forward fails loudly at mec_model_check instead of returning NaN probabilities.
+__device__ __forceinline__ bool x3_out_of_range(float v) { return !(__builtin_fabsf(v) < 65520.f); }
+__device__ __forceinline__ bool x3_out_of_range4(float4 v) {
+  return x3_out_of_range(v.x) || x3_out_of_range(v.y) || x3_out_of_range(v.z) || x3_out_of_range(v.w);
+}
+__device__ __forceinline__ void x3_raise(unsigned* flag, bool bad) {
+  if (bad && flag) __hip_atomic_store(flag, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+}
 int set_option(Options& o, const std::string& key, int value);  // 0 = ok, -1 = unknown key / bad value
 constexpr bool kProbes =
 #ifdef MEC_PROBES
@@ -250,6 +267,7 @@ struct GemmParams {
   long long a_lo = 0, b_lo = 0;
   float oscale = 1.f;
   long long c_lo = 0;  // != 0: C16 is written as a hi plane and a lo plane (C16 + c_lo): f16(v), f16(v - hi)
+  unsigned* ovf = nullptr;  // split output's range flag (x3_raise); launch_gemm fills in range_flag()
   long long r_lo = 0;  // != 0: the f16 residual R is a hi plane + a lo plane at R + r_lo (R = hi + lo)
 };
 

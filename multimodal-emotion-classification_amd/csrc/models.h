@@ -27,10 +27,15 @@ struct Model {
   Options opts = default_options();  // this handle's knobs (mec_model_set_option)
   TuneCache tune;                    // this handle's GEMM autotune results
   Prof prof;
-  virtual ~Model() {}
+  // fp32x3 handles: host-mapped pinned word (range_host) and its device view (range_dev), raised by
+  // the kernels that write activation planes when a value leaves the f16 range (x3_raise)
+  unsigned* range_host = nullptr;
+  unsigned* range_dev = nullptr;
+  int alloc_range_flag();
+  virtual ~Model();
   // errors a kernel could only report after the fact (mec_model_check): 0 = none since the last
   // check. Call after the stream that ran the handle's forwards has been synchronized.
-  virtual int check() { return 0; }
+  virtual int check();
 };
 
 // ---------------------------------------------------------------- speech DNN
@@ -196,13 +201,6 @@ struct MobileNetModel : ImageNet {
                  hipStream_t s) override;
   int forward_f32(const uint8_t* img, int B, int H, int W, int C, float* feat, float* logits, float* probs,
                   hipStream_t s);
-  // fp32x3 path (resnet_f32.hip): wts holds every bottleneck conv's f16 hi planes, then the lo
-  // planes at x3_lo halfs (w_off indexes both); the stem, pooling and head run as on the fp32 path
-  size_t x3_lo = 0;
-  float stem_x3_up = 1.f;  // 2^e: the gray stem's weight pre-scale (stem.x3_scale = 2^-e)
-  DevBuf wts_dual;  // fp32x3: block 0's [conv3 | downsample] hi / lo planes (c3ds_w_off, c3ds_x3_lo)
-  int forward_x3(const uint8_t* img, int B, int H, int W, int C, float* feat, float* logits, float* probs,
-                 hipStream_t s);
 };
 
 int resize_u8(const uint8_t* in, int B, int H, int W, uint8_t* out, int OH, int OW, hipStream_t s);

@@ -218,7 +218,8 @@ typedef _Float16 hpair __attribute__((ext_vector_type(2)));
 __global__ __launch_bounds__(512, 1) void stem_pool_gray_x3_kernel(const uint8_t* __restrict__ img, int ntiles,
                                                                   const float* __restrict__ wg, float wsc_up,
                                                                   float wscale, const float* __restrict__ bias,
-                                                                  f16* __restrict__ y, long long lo) {
+                                                                  f16* __restrict__ y, long long lo,
+                                                                  unsigned* flag) {
   __shared__ __attribute__((aligned(16))) f16 swh[52 * 2 * 64];  // [tap][channel][co], taps 49..51 zero
   __shared__ __attribute__((aligned(16))) f16 swl[52 * 2 * 64];
   __shared__ __attribute__((aligned(16))) hpair patch[SGF_P * SGF_P];  // (pixel, inside)
@@ -353,6 +354,7 @@ __global__ __launch_bounds__(512, 1) void stem_pool_gray_x3_kernel(const uint8_t
                        (f16)(m.w - (float)h[3])};
       *reinterpret_cast<half4*>(y + o) = h;
       *reinterpret_cast<half4*>(y + lo + o) = l;
+      x3_raise(flag, x3_out_of_range4(m));
     }
   }
 }
@@ -511,7 +513,7 @@ int ImageModel::create_f32(const float* blob, size_t n) {
 
 // fp32 tensor -> f16 hi / lo planes (the fp32x3 path's stem output): hi = f16(x), lo = f16(x - hi)
 __global__ __launch_bounds__(256) void split_f32_kernel(const float* __restrict__ x, size_t n4, f16* __restrict__ hi,
-                                                        long long lo) {
+                                                        long long lo, unsigned* flag) {
   const size_t i = (size_t)blockIdx.x * 256 + threadIdx.x;
   if (i >= n4) return;
   const float4 v = reinterpret_cast<const float4*>(x)[i];
@@ -520,6 +522,7 @@ __global__ __launch_bounds__(256) void split_f32_kernel(const float* __restrict_
                    (f16)(v.w - (float)h[3])};
   reinterpret_cast<half4*>(hi)[i] = h;
   reinterpret_cast<half4*>(hi + lo)[i] = l;
+  x3_raise(flag, x3_out_of_range4(v));
 }
 
 // global average pool of an NHWC tensor held as f16 hi / lo planes (x = hi + lo exactly), the
@@ -688,7 +691,8 @@ int ImageModel::forward_x3(const uint8_t* img, int B, int H, int W, int C, float
     }
     const int ntiles = B * 49;
     hipLaunchKernelGGL(stem_pool_gray_x3_kernel, dim3(std::min(ntiles, ncu)), dim3(512), 0, s, stem_in, ntiles,
-                       Wt32 + stem_gray32_off, stem_x3_up, stem.x3_scale, P + stem.b_off, X, L);
+                       Wt32 + stem_gray32_off, stem_x3_up, stem.x3_scale, P + stem.b_off, X, L,
+                       range_flag());
     MEC_LAUNCH_CHECK();
   } else {
     const size_t total = (size_t)B * 112 * 112 * (STEM_K / 4);
@@ -704,7 +708,7 @@ int ImageModel::forward_x3(const uint8_t* img, int B, int H, int W, int C, float
     hipLaunchKernelGGL(maxpool_f32_kernel, dim3((unsigned)((tp + 255) / 256)), dim3(256), 0, s, Y32, B, 112, 64, 56, S32);
     MEC_LAUNCH_CHECK();
     const size_t n4 = (size_t)B * 56 * 56 * 64 / 4;
-    hipLaunchKernelGGL(split_f32_kernel, dim3((unsigned)((n4 + 255) / 256)), dim3(256), 0, s, S32, n4, X, L);
+    hipLaunchKernelGGL(split_f32_kernel, dim3((unsigned)((n4 + 255) / 256)), dim3(256), 0, s, S32, n4, X, L, range_flag());
     MEC_LAUNCH_CHECK();
   }
   MEC_TRY(prof.end(TAG_RESNET_STEM, s));

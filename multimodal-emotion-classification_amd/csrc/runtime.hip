@@ -2,7 +2,7 @@
 #include <algorithm>
 #include <cmath>
 
-#include "mec_common.h"
+#include "models.h"
 
 namespace mec {
 
@@ -23,15 +23,19 @@ TuneCache& default_tune_cache() {
 }
 static thread_local const Options* t_opts = nullptr;
 static thread_local TuneCache* t_tune = nullptr;
+static thread_local unsigned* t_flag = nullptr;
 const Options& opt() { return t_opts ? *t_opts : default_options(); }
 TuneCache& tune_cache() { return t_tune ? *t_tune : default_tune_cache(); }
-OptScope::OptScope(const Options* o, TuneCache* t) : po(t_opts), pt(t_tune) {
+unsigned* range_flag() { return t_flag; }
+OptScope::OptScope(const Options* o, TuneCache* t, unsigned* flag) : po(t_opts), pt(t_tune), pf(t_flag) {
   t_opts = o;
   t_tune = t;
+  t_flag = flag;
 }
 OptScope::~OptScope() {
   t_opts = po;
   t_tune = pt;
+  t_flag = pf;
 }
 
 int DevBuf::ensure(size_t n) {
@@ -87,6 +91,26 @@ int Prof::read(double* total_ms, int* count) {
 
 Prof::~Prof() {
   for (auto e : ev) (void)hipEventDestroy(e);
+}
+
+int Model::alloc_range_flag() {
+  if (range_host) return 0;
+  MEC_HIP(hipHostMalloc(reinterpret_cast<void**>(&range_host), sizeof(unsigned), hipHostMallocMapped));
+  *range_host = 0;
+  MEC_HIP(hipHostGetDevicePointer(reinterpret_cast<void**>(&range_dev), range_host, 0));
+  return 0;
+}
+
+Model::~Model() {
+  if (range_host) (void)hipHostFree(range_host);
+}
+
+int Model::check() {
+  if (!range_host || !*reinterpret_cast<volatile unsigned*>(range_host)) return 0;
+  *range_host = 0;
+  set_error("fp32x3: an activation left the f16 hi / lo range (|x| >= 65520, or NaN / inf) in a forward since "
+            "the last check; its outputs are invalid (use MEC_PREC_FP32 for such inputs)");
+  return -1;
 }
 
 float split_planes(const float* w, size_t n, f16* hi, f16* lo) {

@@ -283,3 +283,133 @@ def _plane_output(dev, lib, tile):
     hi, lo = C16[0].cpu().numpy(), C16[1].cpu().numpy()
     assert np.array_equal(hi, v.astype(np.float16))
     assert np.array_equal(lo, (v - hi.astype(np.float32)).astype(np.float16))
+
+
+# ------------------------------------------------------------------ the fp32x3 range envelope
+# Weights are split after a per-matrix power-of-two pre-scale (csrc/runtime.hip split_planes).
+# Activations are split as they are produced: hi = f16(x), lo = f16(x - hi), which holds 22
+# significant bits for 2^-3 <= |x| < 65520 (lo a normal f16). Below 2^-3, lo is an f16 subnormal:
+# each operand then carries an absolute error <= 2^-25 instead. At |x| >= 65520 hi is inf: every
+# producer of activation planes raises the handle's range flag and mec_model_check fails the
+# forward (INTEGRATION.md "fp32x3 envelope").
+
+
+def _gemm_pair(dev, A, W):
+    """(exact-f32 engine, split engine) outputs of A . W^T, and the float64 reference."""
+    import ctypes
+    from mec import _lib
+    lib = _lib.load()
+    M, K = A.shape
+    N = W.shape[0]
+    st = ctypes.c_void_p(torch.cuda.current_stream(dev).cuda_stream)
+    p = lambda t: ctypes.c_void_p(t.data_ptr())  # noqa: E731
+    Ad, Wd = torch.from_numpy(A).to(dev), torch.from_numpy(W).to(dev)
+    e = float(np.ceil(np.log2(16384 / np.abs(W).max())) - 1)
+    Axd, Wxd = torch.from_numpy(_split(A)).to(dev), torch.from_numpy(_split(W, 2.0 ** e)).to(dev)
+    C32, Cx = torch.empty((M, N), device=dev), torch.empty((M, N), device=dev)
+    _lib.check(lib.mec_gemm_f32(p(Ad), p(Wd), None, None, p(C32), M, N, K, 0, st), 'mec_gemm_f32')
+    _lib.check(lib.mec_gemm_f16x3(p(Axd), M * K, p(Wxd), N * K, ctypes.c_float(2.0 ** -e), None, None, None, 0,
+                                  p(Cx), M, N, K, 0, st), 'mec_gemm_f16x3')
+    torch.cuda.synchronize()
+    return C32.cpu().numpy(), Cx.cpu().numpy(), A.astype(np.float64) @ W.astype(np.float64).T
+
+
+def test_split_gemm_mixed_magnitude_activations_1e6_to_1e4(dev):
+    """Activations whose magnitudes span 1e-6 .. 1e4 inside every row (log-uniform, random signs):
+    the split engine stays within the fp32 GEMM bar (2e-6 x sum |a w|) of float64, as the exact-f32
+    engine does; tiny entries lose relative bits to the subnormal lo plane, but the bar is relative
+    to the row's sum and both engines are held to it."""
+    rng = np.random.default_rng(11)
+    M, N, K = 1024, 768, 768
+    A = (np.sign(rng.standard_normal((M, K))) * 10.0 ** rng.uniform(-6, 4, (M, K))).astype(np.float32)
+    W = (rng.standard_normal((N, K)) * 0.02).astype(np.float32)
+    c32, cx, ref = _gemm_pair(dev, A, W)
+    bound = 2e-6 * (np.abs(A).astype(np.float64) @ np.abs(W).astype(np.float64).T + 1)
+    e32, ex3 = np.abs(c32 - ref), np.abs(cx - ref)
+    print(f'mixed 1e-6..1e4: exact-f32 max err/bound {(e32 / bound).max():.3g}, split {(ex3 / bound).max():.3g}')
+    assert (e32 <= bound).all() and (ex3 <= bound).all()
+
+
+@pytest.mark.parametrize('scale', [1e-1, 1e-3])
+def test_split_gemm_small_activations_absolute_floor(dev, scale):
+    """Activations uniformly small (N(0,1) x scale): below 2^-3 the lo plane is an f16 subnormal, so
+    each operand carries an absolute error <= 2^-25. The split engine stays within the fp32 bar plus
+    that floor, 2e-6 x sum |a w| + 2^-25 x sum |w|, and its error against the exact-f32 engine's is
+    printed (the envelope INTEGRATION.md states; MEC_PREC_FP32 has no such floor)."""
+    rng = np.random.default_rng(12)
+    M, N, K = 1024, 768, 768
+    A = (rng.standard_normal((M, K)) * scale).astype(np.float32)
+    W = (rng.standard_normal((N, K)) * 0.02).astype(np.float32)
+    c32, cx, ref = _gemm_pair(dev, A, W)
+    aw = np.abs(A).astype(np.float64) @ np.abs(W).astype(np.float64).T
+    e32, ex3 = np.abs(c32 - ref), np.abs(cx - ref)
+    bound = 2e-6 * (aw + 1e-30) + 2.0 ** -25 * np.abs(W).astype(np.float64).sum(1)[None, :]
+    print(f'A ~ N(0,1) x {scale:g}: max err / sum|a w|: exact-f32 {(e32 / aw).max():.3g}, split {(ex3 / aw).max():.3g}')
+    assert (e32 <= 2e-6 * aw + 1e-30).all()
+    assert (ex3 <= bound).all()
+
+
+def _force_overflow(kind, name, factor):
+    w = syn.weights(kind)
+    w[name] = (w[name] * np.float32(factor)).astype(np.float32)
+    return w
+
+
+@pytest.mark.parametrize('name', ['bert.encoder.layer.0.intermediate.dense.weight',
+                                  'bert.embeddings.LayerNorm.weight'])
+def test_text_fp32x3_overflow_raises_at_check(dev, name):
+    """A weight scaled so one activation plane leaves the f16 range (FFN1's GEMM epilogue output,
+    or the embedding LayerNorm's output): the forward completes, and check() raises MecError
+    (mec_model_check) instead of the probabilities silently going NaN. The flag is cleared by the
+    check: a second check passes. The exact-fp32 path runs the same weights without complaint."""
+    from mec._lib import MecError
+    w = _force_overflow('text', name, 1e5)
+    ids, mask = syn.text_inputs(4, 128, seed=3, ragged=True)
+    args = (engine.to_device(ids, dev), engine.to_device(mask, dev))
+    enc = engine.TextEncoder(w, device=dev, precision='fp32x3')
+    enc.check()  # clean handle
+    enc.forward(*args)
+    torch.cuda.synchronize()
+    with pytest.raises(MecError, match='f16 hi / lo range'):
+        enc.check()
+    enc.check()
+    e32 = engine.TextEncoder(w, device=dev, precision='fp32')
+    _, _, p32 = _np(e32.forward(*args))
+    e32.check()
+    assert np.isfinite(p32).all()
+
+
+def test_resnet_fp32x3_overflow_raises_at_check(dev):
+    """The stem's output planes (stem_pool_gray_x3_kernel) out of the f16 range -> check() raises;
+    the same handle with in-range inputs afterwards checks clean."""
+    from mec._lib import MecError
+    w = _force_overflow('image', 'base.bn1.weight', 1e6)
+    enc = engine.ImageEncoder(w, device=dev, precision='fp32x3')
+    enc.forward(engine.to_device(syn.image_inputs(2, seed=5), dev))
+    torch.cuda.synchronize()
+    with pytest.raises(MecError, match='f16 hi / lo range'):
+        enc.check()
+    ok = engine.ImageEncoder(device=dev, precision='fp32x3')
+    ok.forward(engine.to_device(syn.image_inputs(2, seed=5), dev))
+    torch.cuda.synchronize()
+    ok.check()
+
+
+def test_fp32x3_untuned_tiles_match_autotuned(dev):
+    """gemm_autotune 0 (the untuned fallback, also what a first launch inside graph capture runs):
+    K-interleaved split GEMMs take an interleaved tile (heuristic_bn), so the fp32x3 text and image
+    forwards run and give the autotuned handle's bits (every interleaved tile sums in one k order)."""
+    ids, mask = syn.text_inputs(8, 128, seed=9, ragged=True)
+    targs = (engine.to_device(ids, dev), engine.to_device(mask, dev))
+    g = engine.to_device(syn.image_inputs(8, seed=9), dev)
+    outs = []
+    for autotune in (1, 0):
+        t = engine.TextEncoder(device=dev, precision='fp32x3')
+        i = engine.ImageEncoder(device=dev, precision='fp32x3')
+        t.set_option('gemm_autotune', autotune)
+        i.set_option('gemm_autotune', autotune)
+        outs.append(_np(t.forward(*targs)) + _np(i.forward(g)))
+        t.check()
+        i.check()
+    for k, (a, b) in enumerate(zip(*outs)):
+        assert np.array_equal(a, b), f'output {k}'

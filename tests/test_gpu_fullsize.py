@@ -134,7 +134,7 @@ def test_fused_b256_fp32_vs_oracle_all_rows(fused_run32, oracle_all, mod):
         assert ferr <= 1e-4
 
 
-@pytest.mark.parametrize('precision', ['f16', 'fp32'])
+@pytest.mark.parametrize('precision', ['f16', 'fp32', 'fp32x3'])
 def test_fused_b1024_shard_rows_from_every_quarter(dev, precision):
     """BASELINE configs[4]'s per-rank work (1024 samples per GPU): the pipeline at B=1024 with
     the bench's input seeds, rows from every quarter of the batch (bench.parity_rows, rows
@@ -150,6 +150,7 @@ def test_fused_b1024_shard_rows_from_every_quarter(dev, precision):
     pipe.forward(*args)
     out = pipe.forward(*args)
     pipe.wait()
+    pipe.check()
     got = {k: _np(v) for k, v in out.items()}
     for m in pipe.models():
         m.close()
