@@ -365,75 +365,17 @@ __global__ __launch_bounds__(256) void bert_attention_cls_kernel(const f16* __re
 }
 
 // ----------------------------------------------------------------------------- fp32x3 attention
-// The fp32 attention of one (sequence, head) on split-f16 operands (the MEC_PREC_FP32X3 path):
-// Q, K, V arrive as f16 hi / lo planes (qkv, qkv + lo; the split QKV GEMM's output) and every
-// product is hi.hi + hi.lo + lo.hi into an fp32 accumulator, as in the split GEMM:
-//   S^T = K Q^T      3 v_mfma_f32_32x32x16_f16 per 16-deep k step (K_lo Q_hi, K_hi Q_lo, K_hi Q_hi)
-//   P   = softmax(S / 8 + mask_bias) in fp32 with libm expf (the fp32 path's arithmetic)
-//   O^T = V^T P^T    P (x 2^12, exact, so its small entries stay out of the f16 subnormals) split
-//                    into hi / lo in registers, 3 MFMAs per step; O scaled back by 2^-12
-// Layout and lane roles are attn_head's (keys in registers, one cross-half shuffle per row,
-// transposed V reads); Q goes straight to registers (each wave reads only its own 32 query
-// rows), so 64 KB of LDS (K, V planes) lets two workgroups share a CU and one's loads overlap
-// the other's MFMAs. The output is staged per wave in K's rows (free after the score loop) and
-// written as hi / lo planes (ctx, ctx + clo) for the split O-projection.
-// CLS = 1 (BERT's last layer with bert_cls_last: only the [CLS] query's context is read): qkv holds
-// K | V only ([B*128, 1536] planes, the K / V GEMM's output), the [CLS] query comes from qc ([B, 768]
-// planes, lo at qc + qclo) and the context is written compact ([B, 768] planes). All four waves
-// stage K and V; wave 0 then runs the full kernel's instruction sequence for queries 0..31 with Q
-// zero for all but query 0 (an MFMA output column depends only on its own B column), so the [CLS]
-// context has the full kernel's bits; waves 1-3 leave after staging.
-template <int CLS = 0>
-__global__ __launch_bounds__(256, 2) void bert_attention_x3_kernel(const f16* __restrict__ qkv, long long lo,
-                                                                   const int32_t* __restrict__ mask,
-                                                                   f16* __restrict__ ctx, long long clo,
-                                                                   const f16* __restrict__ qc, long long qclo) {
-  constexpr int LD = CLS ? 2 * BH : 3 * BH;  // row stride of qkv
-  constexpr int KO = CLS ? 0 : BH;           // K column offset (V at KO + BH)
-  __shared__ __attribute__((aligned(16))) f16 sK[2][ATT_L * BDH];
-  __shared__ __attribute__((aligned(16))) f16 sV[2][ATT_L * BDH];
-  __shared__ float sBias[ATT_L];
-  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
-  const int b = blockIdx.x / BHEADS, h = blockIdx.x - (blockIdx.x / BHEADS) * BHEADS;
+// The attention of one (sequence, head) on split operands, after K / V (aswz / vswz rows, hi and lo
+// planes) and the mask bias are in LDS and this lane's Q fragments (row 32 wave + lr, k chunks
+// 2 kk + lh; hi and lo) are in registers: S^T = K Q^T (three f16 products per fp32 product), fp32
+// softmax, O^T = V^T P^T on split P / V, O -> hi / lo planes staged through this wave's own rows of
+// sK and stored to ctx (row stride BH; lo plane at + clo; CLS: query 0 only). `wave` is the wave's
+// index among the four serving this head; every wave of the workgroup reaches the barrier.
+template <int CLS>
+__device__ __forceinline__ void attn_head_x3(f16* const (&sK)[2], const f16* const (&sV)[2], const float* sBias,
+                                             const half8 (&qh)[4], const half8 (&ql)[4], int wave, int lane, f16* ctx,
+                                             long long clo, int b, int h) {
   const int lr = lane & 31, lh = lane >> 5;
-  half8 qh[4], ql[4];  // this lane's Q row 32 wave + lr, k chunks 2 kk + lh (the MFMA B operand)
-  if constexpr (CLS) {
-    const bool own = wave == 0 && lr == 0;
-    const f16* qrow = qc + (size_t)b * BH + h * BDH;
-#pragma unroll
-    for (int kk = 0; kk < 4; ++kk) {
-#pragma unroll
-      for (int j = 0; j < 8; ++j) { qh[kk][j] = (f16)0.f; ql[kk][j] = (f16)0.f; }
-      if (own) {
-        qh[kk] = *reinterpret_cast<const half8*>(qrow + (2 * kk + lh) * 8);
-        ql[kk] = *reinterpret_cast<const half8*>(qrow + qclo + (2 * kk + lh) * 8);
-      }
-    }
-  } else {
-    const f16* qrow = qkv + (size_t)b * ATT_L * LD + h * BDH + (size_t)(32 * wave + lr) * LD;
-#pragma unroll
-    for (int kk = 0; kk < 4; ++kk) {
-      qh[kk] = *reinterpret_cast<const half8*>(qrow + (2 * kk + lh) * 8);
-      ql[kk] = *reinterpret_cast<const half8*>(qrow + lo + (2 * kk + lh) * 8);
-    }
-  }
-#pragma unroll
-  for (int pl = 0; pl < 2; ++pl) {
-    const f16* base = qkv + (pl ? lo : 0) + (size_t)b * ATT_L * LD + h * BDH;
-#pragma unroll
-    for (int i = 0; i < 4; ++i) {
-      const int c = tid + 256 * i;
-      const int row = c >> 3, kc = c & 7;
-      const f16* src = base + (size_t)row * LD + kc * 8;
-      const uint4 k = *reinterpret_cast<const uint4*>(src + KO);
-      const uint4 v = *reinterpret_cast<const uint4*>(src + KO + BH);
-      *reinterpret_cast<uint4*>(sK[pl] + row * BDH + aswz(row, kc) * 8) = k;
-      *reinterpret_cast<uint4*>(sV[pl] + row * BDH + vswz(row, kc) * 8) = v;
-    }
-  }
-  if (tid < ATT_L) sBias[tid] = mask[(size_t)b * ATT_L + tid] ? 0.f : -3.4028234663852886e38f;  // finfo(f32).min
-  __syncthreads();
-  if (CLS && wave != 0) return;
   floatx16 s[4];
 #pragma unroll
   for (int t = 0; t < 4; ++t) {
@@ -537,6 +479,80 @@ __global__ __launch_bounds__(256, 2) void bert_attention_x3_kernel(const f16* __
       const uint4 v = *reinterpret_cast<const uint4*>(sK[pl] + r * BDH + aswz(r, kc) * 8);
       if (!CLS || r == 0) *reinterpret_cast<uint4*>(out + (pl ? clo : 0) + (size_t)r * BH + kc * 8) = v;
     }
+}
+
+// The fp32 attention of one (sequence, head) on split-f16 operands (the MEC_PREC_FP32X3 path):
+// Q, K, V arrive as f16 hi / lo planes (qkv, qkv + lo; the split QKV GEMM's output) and every
+// product is hi.hi + hi.lo + lo.hi into an fp32 accumulator, as in the split GEMM:
+//   S^T = K Q^T      3 v_mfma_f32_32x32x16_f16 per 16-deep k step (K_lo Q_hi, K_hi Q_lo, K_hi Q_hi)
+//   P   = softmax(S / 8 + mask_bias) in fp32 with libm expf (the fp32 path's arithmetic)
+//   O^T = V^T P^T    P (x 2^12, exact, so its small entries stay out of the f16 subnormals) split
+//                    into hi / lo in registers, 3 MFMAs per step; O scaled back by 2^-12
+// Layout and lane roles are attn_head's (keys in registers, one cross-half shuffle per row,
+// transposed V reads); Q goes straight to registers (each wave reads only its own 32 query
+// rows), so 64 KB of LDS (K, V planes) lets two workgroups share a CU and one's loads overlap
+// the other's MFMAs. The output is staged per wave in K's rows (free after the score loop) and
+// written as hi / lo planes (ctx, ctx + clo) for the split O-projection.
+// CLS = 1 (BERT's last layer with bert_cls_last: only the [CLS] query's context is read): qkv holds
+// K | V only ([B*128, 1536] planes, the K / V GEMM's output), the [CLS] query comes from qc ([B, 768]
+// planes, lo at qc + qclo) and the context is written compact ([B, 768] planes). All four waves
+// stage K and V; wave 0 then runs the full kernel's instruction sequence for queries 0..31 with Q
+// zero for all but query 0 (an MFMA output column depends only on its own B column), so the [CLS]
+// context has the full kernel's bits; waves 1-3 leave after staging.
+template <int CLS = 0>
+__global__ __launch_bounds__(256, 2) void bert_attention_x3_kernel(const f16* __restrict__ qkv, long long lo,
+                                                                   const int32_t* __restrict__ mask,
+                                                                   f16* __restrict__ ctx, long long clo,
+                                                                   const f16* __restrict__ qc, long long qclo) {
+  constexpr int LD = CLS ? 2 * BH : 3 * BH;  // row stride of qkv
+  constexpr int KO = CLS ? 0 : BH;           // K column offset (V at KO + BH)
+  __shared__ __attribute__((aligned(16))) f16 sK[2][ATT_L * BDH];
+  __shared__ __attribute__((aligned(16))) f16 sV[2][ATT_L * BDH];
+  __shared__ float sBias[ATT_L];
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int b = blockIdx.x / BHEADS, h = blockIdx.x - (blockIdx.x / BHEADS) * BHEADS;
+  const int lr = lane & 31, lh = lane >> 5;
+  half8 qh[4], ql[4];  // this lane's Q row 32 wave + lr, k chunks 2 kk + lh (the MFMA B operand)
+  if constexpr (CLS) {
+    const bool own = wave == 0 && lr == 0;
+    const f16* qrow = qc + (size_t)b * BH + h * BDH;
+#pragma unroll
+    for (int kk = 0; kk < 4; ++kk) {
+#pragma unroll
+      for (int j = 0; j < 8; ++j) { qh[kk][j] = (f16)0.f; ql[kk][j] = (f16)0.f; }
+      if (own) {
+        qh[kk] = *reinterpret_cast<const half8*>(qrow + (2 * kk + lh) * 8);
+        ql[kk] = *reinterpret_cast<const half8*>(qrow + qclo + (2 * kk + lh) * 8);
+      }
+    }
+  } else {
+    const f16* qrow = qkv + (size_t)b * ATT_L * LD + h * BDH + (size_t)(32 * wave + lr) * LD;
+#pragma unroll
+    for (int kk = 0; kk < 4; ++kk) {
+      qh[kk] = *reinterpret_cast<const half8*>(qrow + (2 * kk + lh) * 8);
+      ql[kk] = *reinterpret_cast<const half8*>(qrow + lo + (2 * kk + lh) * 8);
+    }
+  }
+#pragma unroll
+  for (int pl = 0; pl < 2; ++pl) {
+    const f16* base = qkv + (pl ? lo : 0) + (size_t)b * ATT_L * LD + h * BDH;
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+      const int c = tid + 256 * i;
+      const int row = c >> 3, kc = c & 7;
+      const f16* src = base + (size_t)row * LD + kc * 8;
+      const uint4 k = *reinterpret_cast<const uint4*>(src + KO);
+      const uint4 v = *reinterpret_cast<const uint4*>(src + KO + BH);
+      *reinterpret_cast<uint4*>(sK[pl] + row * BDH + aswz(row, kc) * 8) = k;
+      *reinterpret_cast<uint4*>(sV[pl] + row * BDH + vswz(row, kc) * 8) = v;
+    }
+  }
+  if (tid < ATT_L) sBias[tid] = mask[(size_t)b * ATT_L + tid] ? 0.f : -3.4028234663852886e38f;  // finfo(f32).min
+  __syncthreads();
+  if (CLS && wave != 0) return;
+  f16* const sKp[2] = {sK[0], sK[1]};
+  const f16* const sVp[2] = {sV[0], sV[1]};
+  attn_head_x3<CLS>(sKp, sVp, sBias, qh, ql, wave, lane, ctx, clo, b, h);
 }
 
 int launch_bert_attention_x3(const f16* qkv, long long lo, const int32_t* mask, f16* ctx, long long clo, int B,
@@ -708,6 +724,197 @@ __global__ __launch_bounds__(512, 1) void bert_qkv_attn_kernel(const f16* __rest
             wave & 3, lane, ctx + (size_t)b * ATT_L * BH + (2 * hp + hh) * BDH);
 }
 
+
+// ----------------------------------------------------------------------------- fp32x3 QKV + attention
+// The fp32x3 path's QKV projection and attention of one (sequence, head pair) in one workgroup, as
+// bert_qkv_attn_kernel does on the f16 path, so the Q / K / V hi / lo planes (302 MB per layer at
+// B = 256 written by the split QKV GEMM and read back by bert_attention_x3_kernel) never reach HBM:
+//   * the 128 (tokens) x 384 (Q | K | V of heads 2 hp, 2 hp + 1) x 768 split GEMM tile: 8 waves
+//     (2 x 4, wave tile 64 x 96) on v_mfma_f32_16x16x32_f16 computed transposed (out^T = W . X^T),
+//     32-deep K stages holding the hi AND lo tiles of the token rows and the weight rows (64 KB;
+//     two stages, restaged for k + 2 as soon as every wave holds its fragments), and per k chunk the
+//     K-interleaved split engine's three terms in its order (X_lo W_hi, X_hi W_lo, X_hi W_hi);
+//   * the epilogue computes (acc 2^-e + b) + 0 and its hi / lo planes exactly as the split GEMM's
+//     epilogue, in two phases through the freed stages: the Q planes first, from which every
+//     attention wave loads its query fragments into registers, then the K / V planes (aswz / vswz
+//     rows: 128 KB for both heads);
+//   * each 4-wave half runs attn_head_x3 (bert_attention_x3_kernel's body) on one head.
+// Same products, term order and k order as the split QKV GEMM, the same attention code: the context
+// planes are bit-identical to the unfused pair (tests/test_gpu_fp32x3.py).
+constexpr int QX_BK = 32, QX_NK = BH / QX_BK;       // 24 K steps of 32
+constexpr int QX_PLANE = (QA_BM + QA_BN) * QX_BK;  // halfs per plane of a stage (32 KB)
+constexpr int QX_STAGE = 2 * QX_PLANE;             // hi + lo planes (64 KB)
+
+__device__ __forceinline__ int qx_sw(int row, int kc) { return kc ^ ((4 - ((row >> 2) & 3)) & 3); }  // sw<32>
+
+__global__ __launch_bounds__(512, 1) void bert_qkv_attn_x3_kernel(const f16* __restrict__ hs, long long hlo,
+                                                                  const f16* __restrict__ wqkv, long long wlo,
+                                                                  float oscale, const float* __restrict__ bqkv,
+                                                                  const int32_t* __restrict__ mask,
+                                                                  f16* __restrict__ ctx, long long clo, int nseq,
+                                                                  unsigned* flag) {
+  __shared__ __attribute__((aligned(16))) f16 smem[2 * QX_STAGE];  // 2 GEMM stages, then Q, then K / V images
+  __shared__ float sBias[ATT_L];
+  typedef __attribute__((address_space(3))) void* lds_p;
+  const int tid = threadIdx.x, lane = tid & 63;
+  const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int wm = wave >> 2, wn = wave & 3;
+  const int l16 = lane & 15, lq = lane >> 4;
+  // XCD-aware bijective remap: the 6 head pairs of a sequence (which share its token rows) on one XCD
+  const int nwg = nseq * 6;
+  int bid = blockIdx.x;
+  {
+    const int xcd = bid & 7, q = nwg >> 3, r = nwg & 7;
+    bid = (xcd < r ? xcd * (q + 1) : r * (q + 1) + (xcd - r) * q) + (bid >> 3);
+  }
+  const int b = bid / 6, hp = bid - (bid / 6) * 6;
+
+  // stage loader: LDS row R < 128 = token row R of the sequence; R >= 128 = weight row
+  // (R-128)/128 * 768 + hp*128 + (R-128)%128; 16 rows of 64 B per wave-instruction, 4 per plane per wave
+  const int lrow = lane >> 2, pch = lane & 3;
+  const f16* src[4];
+  long long lo_off[4];
+#pragma unroll
+  for (int it = 0; it < 4; ++it) {
+    const int R = (it * 8 + wave) * 16 + lrow;
+    const int c = qx_sw(R, pch);
+    if (R < QA_BM) {
+      src[it] = hs + ((size_t)b * ATT_L + R) * BH + c * 8;
+      lo_off[it] = hlo;
+    } else {
+      const int n = R - QA_BM, seg = n >> 7, j = n & 127;
+      src[it] = wqkv + ((size_t)seg * BH + hp * 128 + j) * BH + c * 8;
+      lo_off[it] = wlo;
+    }
+  }
+  auto issue = [&](int kt, int st) {
+    f16* base = smem + st * QX_STAGE;
+#pragma unroll
+    for (int pl = 0; pl < 2; ++pl)
+#pragma unroll
+      for (int it = 0; it < 4; ++it)
+        __builtin_amdgcn_global_load_lds((const void*)(src[it] + (pl ? lo_off[it] : 0) + kt * QX_BK),
+                                         (lds_p)(base + pl * QX_PLANE + (it * 8 + wave) * 16 * QX_BK), 16, 0, 0);
+  };
+
+  floatx4 acc[4][6];
+#pragma unroll
+  for (int i = 0; i < 4; ++i)
+#pragma unroll
+    for (int j = 0; j < 6; ++j) acc[i][j] = floatx4{0.f, 0.f, 0.f, 0.f};
+  issue(0, 0);
+  issue(1, 1);
+#pragma unroll 1
+  for (int kt = 0; kt < QX_NK; ++kt) {
+    if (kt + 1 < QX_NK)
+      asm volatile("s_waitcnt vmcnt(8)" ::: "memory");
+    else
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    __builtin_amdgcn_s_barrier();  // stage kt landed for every wave
+    const f16* sA = smem + (kt & 1) * QX_STAGE;
+    half8 af[2][4], bf[2][6];  // [plane: 0 hi, 1 lo]
+#pragma unroll
+    for (int pl = 0; pl < 2; ++pl) {
+#pragma unroll
+      for (int i = 0; i < 4; ++i) {
+        const int r = 64 * wm + 16 * i + l16;
+        af[pl][i] = *reinterpret_cast<const half8*>(sA + pl * QX_PLANE + r * QX_BK + qx_sw(r, lq) * 8);
+      }
+#pragma unroll
+      for (int j = 0; j < 6; ++j) {
+        const int rr = QA_BM + 96 * wn + 16 * j + l16;
+        bf[pl][j] = *reinterpret_cast<const half8*>(sA + pl * QX_PLANE + rr * QX_BK + qx_sw(rr, lq) * 8);
+      }
+    }
+    // the stage is free once every wave holds its fragments: restage it for kt + 2 before the MFMAs
+    __builtin_amdgcn_sched_barrier(0);
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+    __builtin_amdgcn_s_barrier();
+    if (kt + 2 < QX_NK) issue(kt + 2, kt & 1);
+    __builtin_amdgcn_sched_barrier(0);
+#pragma unroll
+    for (int i = 0; i < 4; ++i)
+#pragma unroll
+      for (int j = 0; j < 6; ++j) acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_f16(bf[0][j], af[1][i], acc[i][j], 0, 0, 0);
+#pragma unroll
+    for (int i = 0; i < 4; ++i)
+#pragma unroll
+      for (int j = 0; j < 6; ++j) acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_f16(bf[1][j], af[0][i], acc[i][j], 0, 0, 0);
+#pragma unroll
+    for (int i = 0; i < 4; ++i)
+#pragma unroll
+      for (int j = 0; j < 6; ++j) acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_f16(bf[0][j], af[0][i], acc[i][j], 0, 0, 0);
+  }
+  asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)" ::: "memory");
+  __syncthreads();  // every wave is past its last stage read: the stages become the Q / K / V images
+
+  // ---- epilogue: v = (acc 2^-e + b) + 0 (the split GEMM epilogue's expression), hi = f16(v),
+  // lo = f16(v - hi). Images: [seg][head][plane] = [128][64] halfs, seg 0 Q / 1 K / 2 V
+  if (tid < ATT_L) sBias[tid] = mask[(size_t)b * ATT_L + tid] ? 0.f : -3.4028234663852886e38f;  // finfo(f32).min
+  bool bad = false;
+  auto write_seg = [&](int want, f16* img) {
+#pragma unroll
+    for (int j = 0; j < 6; ++j) {
+      const int n = 96 * wn + 16 * j + 4 * lq;  // features n .. n+3 (one 128-block, one head)
+      const int seg = n >> 7, hh = (n >> 6) & 1, d = n & 63;
+      if (seg != want) continue;
+      const float4 bv = *reinterpret_cast<const float4*>(bqkv + seg * BH + hp * 128 + (n & 127));
+      const float bb[4] = {bv.x, bv.y, bv.z, bv.w};
+      // hi plane of this (segment, head); its lo plane follows (Q: [head][plane]; K / V: [seg-1][head][plane])
+      f16* dst = img + (want == 0 ? 2 * hh : 2 * (2 * (seg - 1) + hh)) * (ATT_L * BDH);
+#pragma unroll
+      for (int i = 0; i < 4; ++i) {
+        const int m = 64 * wm + 16 * i + l16;  // token
+        half4 hv, lv;
+#pragma unroll
+        for (int e = 0; e < 4; ++e) {
+          float v = __builtin_fmaf(acc[i][j][e], oscale, bb[e]);
+          v += 0.f;
+          hv[e] = (f16)v;
+          lv[e] = (f16)(v - (float)hv[e]);
+          bad |= x3_out_of_range(v);
+        }
+        const int ch = seg == 2 ? vswz(m, d >> 3) : aswz(m, d >> 3);
+        *reinterpret_cast<half4*>(dst + m * BDH + ch * 8 + (d & 7)) = hv;
+        *reinterpret_cast<half4*>(dst + ATT_L * BDH + m * BDH + ch * 8 + (d & 7)) = lv;
+      }
+    }
+  };
+  // phase 1: Q planes of both heads ([head][plane] at smem), then every wave's query fragments
+  write_seg(0, smem);
+  __syncthreads();
+  const int hh = wave >> 2, aw = wave & 3;  // this wave's head (of the pair) and its index among that head's 4
+  const int lr = lane & 31, lh = lane >> 5;
+  half8 qh[4], ql[4];
+  {
+    const f16* qi = smem + hh * 2 * (ATT_L * BDH);
+    const int rq = 32 * aw + lr;
+#pragma unroll
+    for (int kk = 0; kk < 4; ++kk) {
+      const int kc = 2 * kk + lh;
+      qh[kk] = *reinterpret_cast<const half8*>(qi + rq * BDH + aswz(rq, kc) * 8);
+      ql[kk] = *reinterpret_cast<const half8*>(qi + ATT_L * BDH + rq * BDH + aswz(rq, kc) * 8);
+    }
+  }
+  asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+  __syncthreads();
+  // phase 2: K and V planes ([K h0 hi, K h0 lo, K h1 hi, K h1 lo, V h0 hi, ..] at smem)
+  write_seg(1, smem);
+  write_seg(2, smem);
+  x3_raise(flag, bad);
+  __syncthreads();
+  f16* const sK[2] = {smem + (0 * 2 + hh) * 2 * (ATT_L * BDH), smem + ((0 * 2 + hh) * 2 + 1) * (ATT_L * BDH)};
+  const f16* const sV[2] = {smem + (1 * 2 + hh) * 2 * (ATT_L * BDH), smem + ((1 * 2 + hh) * 2 + 1) * (ATT_L * BDH)};
+  attn_head_x3<0>(sK, sV, sBias, qh, ql, aw, lane, ctx, clo, b, 2 * hp + hh);
+}
+
+int launch_bert_qkv_attn_x3(const f16* hs, long long hlo, const f16* wqkv, long long wlo, float oscale,
+                            const float* bqkv, const int32_t* mask, f16* ctx, long long clo, int B, hipStream_t s) {
+  hipLaunchKernelGGL(bert_qkv_attn_x3_kernel, dim3(B * 6), dim3(512), 0, s, hs, hlo, wqkv, wlo, oscale, bqkv, mask, ctx,
+                     clo, B, range_flag());
+  MEC_LAUNCH_CHECK();
+  return 0;
+}
 
 // ----------------------------------------------------------------------------- model
 // prm layout per layer (floats): bqkv 2304 | bo 768 | ln1g 768 | ln1b 768 | bi 3072 | bo2 768 |

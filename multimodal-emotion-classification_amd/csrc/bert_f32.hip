@@ -346,12 +346,18 @@ int TextModel::forward_x3(const int32_t* ids, const int32_t* mask, int B, int L,
       MEC_TRY(launch_bert_layernorm(t32c, B, g2, b2, h32c, hsc, nullptr, s, BHc));
       break;
     }
-    g.split = 1; g.A = hs; g.a_lo = MH; g.B = wqkv; g.b_lo = wlo; g.oscale = sc[0];
-    g.bias = bqkv; g.C16 = bigs; g.c_lo = (long long)M * 2304; g.M = M; g.N = 2304; g.K = H;
-    MEC_TRY(launch_gemm(g, s, &prof, TAG_BERT_QKV));
-    MEC_TRY(prof.begin(TAG_BERT_ATTN, s));
-    MEC_TRY(launch_bert_attention_x3(bigs, (long long)M * 2304, mask, cs, MH, B, s));
-    MEC_TRY(prof.end(TAG_BERT_ATTN, s));
+    if (opt().bert_qkv_attn == 1 && L == 128) {  // QKV projection + attention fused: Q / K / V stay on chip
+      MEC_TRY(prof.begin(TAG_BERT_QKV, s));
+      MEC_TRY(launch_bert_qkv_attn_x3(hs, MH, wqkv, wlo, sc[0], bqkv, mask, cs, MH, B, s));
+      MEC_TRY(prof.end(TAG_BERT_QKV, s));
+    } else {
+      g.split = 1; g.A = hs; g.a_lo = MH; g.B = wqkv; g.b_lo = wlo; g.oscale = sc[0];
+      g.bias = bqkv; g.C16 = bigs; g.c_lo = (long long)M * 2304; g.M = M; g.N = 2304; g.K = H;
+      MEC_TRY(launch_gemm(g, s, &prof, TAG_BERT_QKV));
+      MEC_TRY(prof.begin(TAG_BERT_ATTN, s));
+      MEC_TRY(launch_bert_attention_x3(bigs, (long long)M * 2304, mask, cs, MH, B, s));
+      MEC_TRY(prof.end(TAG_BERT_ATTN, s));
+    }
     // deferred LayerNorm (as on the f16 path): the LN kernels write the GEMM operand planes and the
     // row (mean, rstd) only; the f32 LN output is needed only as the next residual, which the
     // O-proj / FFN2 epilogue re-derives from the pre-LN sum with the LN kernel's own expression

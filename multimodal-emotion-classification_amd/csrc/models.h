@@ -116,6 +116,12 @@ int launch_bert_attention_x3(const f16* qkv, long long lo, const int32_t* mask, 
 int launch_bert_attention_x3_cls(const f16* kv, long long lo, const int32_t* mask, const f16* qc, long long qclo,
                                  f16* ctx, long long clo, int B, hipStream_t s);
 
+// fp32x3 QKV projection + attention of one (sequence, head pair) per workgroup (bert.hip, L = 128):
+// h planes [B*128, 768] (lo at hs + hlo), Wqkv planes (lo at wqkv + wlo, epilogue scale oscale) ->
+// ctx planes [B*128, 768] (lo at ctx + clo); Q / K / V never reach HBM
+int launch_bert_qkv_attn_x3(const f16* hs, long long hlo, const f16* wqkv, long long wlo, float oscale,
+                            const float* bqkv, const int32_t* mask, f16* ctx, long long clo, int B, hipStream_t s);
+
 // Split n fp32 weights into f16 planes for the fp32x3 path: hi = f16(w 2^e), lo = f16(w 2^e - hi)
 // with e the largest power of two keeping max |w| 2^e <= 2^14 (so hi never overflows and lo
 // stays out of the f16 subnormals for all but the smallest weights); returns 2^-e, the GEMM

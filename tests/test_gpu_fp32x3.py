@@ -413,3 +413,21 @@ def test_fp32x3_untuned_tiles_match_autotuned(dev):
         i.check()
     for k, (a, b) in enumerate(zip(*outs)):
         assert np.array_equal(a, b), f'output {k}'
+
+
+@pytest.mark.parametrize('B,ragged', [(3, True), (64, True), (256, False)])
+def test_text_fp32x3_fused_qkv_attention_bit_identical(dev, B, ragged):
+    """bert_qkv_attn 1 (the default: bert_qkv_attn_x3_kernel, Q / K / V planes kept in LDS) against
+    0 (the split QKV GEMM, then bert_attention_x3_kernel): the same products in the same term and k
+    order and the same attention code, so CLS feature, logits and probs are equal bit for bit."""
+    ids, mask = syn.text_inputs(B, 128, seed=800 + B, ragged=ragged)
+    args = (engine.to_device(ids, dev), engine.to_device(mask, dev))
+    outs = []
+    for fused in (1, 0):
+        enc = engine.TextEncoder(device=dev, precision='fp32x3')
+        enc.set_option('bert_qkv_attn', fused)
+        outs.append(_np(enc.forward(*args)))
+        enc.check()
+        enc.close()
+    for k, (a, b) in enumerate(zip(*outs)):
+        assert np.array_equal(a, b), f'output {k}: max |d| {np.abs(a - b).max()}'
