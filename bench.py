@@ -339,7 +339,7 @@ def per_config(pipe, dev, precision, iters=10):
     af = engine.AudioFeaturizer(device=dev)
     wv = torch.from_numpy(np.random.default_rng(7).standard_normal((32, 66150)).astype(np.float32)).to(dev)
     runs['speech_waveform_b32'] = (32, lambda: pipe.speech.forward(af.forward(wv)))
-    mb = engine.MobileNetImageEncoder(device=dev, precision='fp32' if precision == 'fp32x3' else precision)
+    mb = engine.MobileNetImageEncoder(device=dev, precision=precision)
     runs['image_mobilenet_v2_b256'] = (256, lambda: mb.forward(g))
     out = {}
     for name, (b, fn) in runs.items():

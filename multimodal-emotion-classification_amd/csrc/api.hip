@@ -124,11 +124,6 @@ int mec_create_ex(int kind, const float* host_blob, size_t n, int device, int pr
       set_error("mec_create: precision must be MEC_PREC_F16, MEC_PREC_FP32 or MEC_PREC_FP32X3");
       return -1;
     }
-    if (precision == MEC_PREC_FP32X3 && kind != KIND_TEXT && kind != KIND_IMAGE && kind != KIND_SPEECH &&
-        kind != KIND_FUSION && kind != KIND_AUDIO) {
-      set_error("mec_create: MEC_PREC_FP32X3 is implemented for BERT and ResNet50 (MobileNetV2: f16 / fp32)");
-      return -1;
-    }
     *out = nullptr;
     const size_t want = blob_floats(kind);
     if (!want) { set_error("mec_create: unknown kind"); return -1; }

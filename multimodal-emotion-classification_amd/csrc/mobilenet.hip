@@ -608,6 +608,7 @@ static int pad_to(int v, int m) { return (v + m - 1) / m * m; }
 
 int MobileNetModel::create(const float* blob, size_t n) {
   if (prec == PREC_FP32) return create_f32(blob, n);  // mobilenet_f32.hip
+  if (prec == PREC_FP32X3) return create_x3(blob, n);  // mobilenet_x3.hip
   BlobReader rd(blob, n);
   std::vector<f16> w;
   std::vector<float> pr;
@@ -866,6 +867,7 @@ int MobileNetModel::forward_u8(const uint8_t* img, int B, int H, int W, int C, f
   MEC_REQUIRE(fer || (H == 224 && W == 224 && (C == 1 || C == 3)),
               "image: input must be u8 [B,48,48,1] (GPU resize) or [B,224,224,{1,3}] (already resized)");
   if (prec == PREC_FP32) return forward_f32(img, B, H, W, C, feat, logits, probs, s);
+  if (prec == PREC_FP32X3) return forward_x3(img, B, H, W, C, feat, logits, probs, s);
   const size_t per_big = (size_t)112 * 112 * 16;  // largest block output (features[1]), elements
   const size_t per_last = (size_t)49 * 1280;
   const size_t per_img = 224 * 224 + (2 * per_big + per_last) * sizeof(f16) + 1280 * sizeof(float);

@@ -1,0 +1,627 @@
+// MobileNetV2 image path on the fp32x3 engine (mec_create_ex(MEC_IMAGE_MBV2, ..., MEC_PREC_FP32X3)):
+// the fp32 arithmetic of mobilenet_f32.hip (torchvision mobilenet_v2 features, README.md:13, restated
+// by oracle/image_mbv2.py, with the reference's transform and head: inference/image_inference.py:28-32,
+// :59-65) in the fused one-kernel-per-block form of mobilenet.hip, with every 1x1 product on the f16
+// MFMA as hi.hi + hi.lo + lo.hi of exact f16 hi / lo pairs (the split GEMM engine's arithmetic,
+// gemm_glds.hip) into one fp32 accumulator:
+//   expand   E = ReLU6(We X 2^-e + be): X (the block input, f32 in HBM) split into hi / lo planes as the
+//            tile is staged in LDS, We pre-split on the host (per-matrix power-of-two scale); E in fp32
+//   dw       D = ReLU6(bd + sum_taps E w) in fp32 (torch's (kh, kw) tap order), split into planes
+//   project  Y = Wp D 2^-e + bp (+ the block input, read back from HBM in f32: an exact residual)
+// Block outputs are f32 NHWC in HBM (the same bytes as two f16 planes); the expanded (6x wider)
+// tensors never leave the CU. Block 1 (t = 1) also computes the stem (3x3/2 on the u8 image,
+// ToTensor / Normalize / BN folded into fp32 weights with a border-class bias) for its tile, kept in
+// fp32 for its depthwise conv. features[18] (1x1 320 -> 1280 + BN + ReLU6) runs on the split GEMM.
+#include <algorithm>
+#include <cmath>
+
+#include "block_ops.h"
+#include "models.h"
+
+namespace mec {
+
+namespace {
+
+constexpr int MX_HC = 32;  // hidden channels per chunk
+
+struct MbX3Args {
+  const void* x;        // block input f32 NHWC [B,H,H,cin] (STEM == 0) or the u8 image [B,224,224,STEM]
+  float* y;             // block output f32 NHWC [B,OH,OH,cout]
+  int H, OH, cin, cout;
+  const f16* We;        // expand hi plane [HIDP][CINP]; lo plane at We + we_lo
+  long long we_lo;
+  float we_scale;       // 2^-e of the expand planes
+  const float* be;      // [HIDP]
+  const float* Wd;      // [HIDP/8][9][8]
+  const float* bd;      // [HIDP]
+  const f16* Wp;        // project hi plane [COUTP][HIDP]; lo plane at Wp + wp_lo
+  long long wp_lo;
+  float wp_scale;
+  const float* bp;      // [COUTP]
+  const float* stem_w;     // [C*9][32] folded stem weights (STEM > 0)
+  const float* stem_corr;  // [4][32] bias per border class (STEM > 0)
+  unsigned* flag;          // range flag (x3_raise): a block input outside the f16 range
+};
+
+__device__ __forceinline__ float relu6x(float v) { return fminf(fmaxf(v, 0.f), 6.f); }
+
+template <int S, int TO, int CINP, int HIDP, int COUTP, bool EXPAND, bool RES, int STEM>
+struct MxGeom {
+  static constexpr int IR = (TO - 1) * S + 3, NP = IR * IR, MP = (NP + 15) / 16 * 16;
+  static constexpr int XLD = CINP + 8;   // f16 plane row (halfs)
+  static constexpr int XF = CINP + 4;    // f32 row of the non-expand (stem) input tile
+  static constexpr int EF = MX_HC + 4;   // f32 row of the expanded chunk
+  static constexpr int ELD = MX_HC + 8;  // f16 plane row of the depthwise output
+  static constexpr int NQ = TO * TO;
+  static constexpr int OT = COUTP / 16, KX = CINP / 32;
+  static constexpr size_t LDS_FIXED = (size_t)(EXPAND ? 2 * MP * XLD * 2 + MP * EF * 4 : MP * XF * 4) +
+                                      2 * 64 * ELD * 2 + (HIDP * (EXPAND ? 2 : 1) + COUTP) * 4;
+  // depthwise weights staged in LDS when they fit beside the tile (else read through L1 / L2)
+  static constexpr bool DWL = LDS_FIXED + HIDP * 9 * 4 <= 128 * 1024;
+};
+
+template <int S, int TO, int CINP, int HIDP, int COUTP, bool EXPAND, bool RES, int STEM>
+__global__ __launch_bounds__(256) void mbv2_x3_kernel(const MbX3Args a) {
+  using G = MxGeom<S, TO, CINP, HIDP, COUTP, EXPAND, RES, STEM>;
+  constexpr int IR = G::IR, NP = G::NP, MP = G::MP, XLD = G::XLD, XF = G::XF, EF = G::EF, ELD = G::ELD;
+  constexpr int NQ = G::NQ, OT = G::OT, KX = G::KX;
+  static_assert(NQ <= 64, "tile");
+  static_assert(!STEM || (CINP == 32 && HIDP == 32 && !EXPAND && S == 1), "stem fuses into block 1 only");
+  static_assert(STEM || EXPAND, "t = 1 blocks only as block 1 (with the stem)");
+  __shared__ __attribute__((aligned(16))) f16 sXh[EXPAND ? MP * XLD : 8];
+  __shared__ __attribute__((aligned(16))) f16 sXl[EXPAND ? MP * XLD : 8];
+  __shared__ __attribute__((aligned(16))) float sXf[EXPAND ? 4 : MP * XF];
+  __shared__ __attribute__((aligned(16))) float sE[EXPAND ? MP * EF : 4];
+  __shared__ __attribute__((aligned(16))) f16 sDh[64 * ELD];
+  __shared__ __attribute__((aligned(16))) f16 sDl[64 * ELD];
+  __shared__ __attribute__((aligned(16))) float sWd[G::DWL ? HIDP * 9 : 4];
+  __shared__ __attribute__((aligned(16))) float sBd[HIDP];
+  __shared__ __attribute__((aligned(16))) float sBe[EXPAND ? HIDP : 4];
+  __shared__ __attribute__((aligned(16))) float sBp[COUTP];
+  constexpr int PR = 2 * (TO + 2) + 1;  // stem: u8 patch side
+  __shared__ __attribute__((aligned(16))) float sSW[STEM ? STEM * 9 * 32 : 4];
+  __shared__ uint8_t sPatch[STEM ? PR * PR * STEM : 4];
+
+  const int tid = threadIdx.x, lane = tid & 63;
+  const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int tpr = a.OH / TO;
+  const int n = blockIdx.x / (tpr * tpr);
+  const int tt = blockIdx.x - n * tpr * tpr;
+  const int oy0 = (tt / tpr) * TO, ox0 = (tt - (tt / tpr) * tpr) * TO;
+  const int iy0 = oy0 * S - 1, ix0 = ox0 * S - 1;  // input tile origin (pad 1)
+  const int H = a.H;
+  const int l16 = lane & 15, lq = lane >> 4;
+
+  // ---- per-block constants -> LDS
+  if constexpr (G::DWL)
+    for (int i = tid; i < HIDP * 9 / 4; i += 256) reinterpret_cast<float4*>(sWd)[i] = reinterpret_cast<const float4*>(a.Wd)[i];
+  for (int i = tid; i < HIDP / 4; i += 256) {
+    reinterpret_cast<float4*>(sBd)[i] = reinterpret_cast<const float4*>(a.bd)[i];
+    if constexpr (EXPAND) reinterpret_cast<float4*>(sBe)[i] = reinterpret_cast<const float4*>(a.be)[i];
+  }
+  if (tid < COUTP / 4) reinterpret_cast<float4*>(sBp)[tid] = reinterpret_cast<const float4*>(a.bp)[tid];
+
+  // expand weights of the first chunk (A fragments, rows = hidden channels), hi and lo planes
+  half8 afh[2][KX], afl[2][KX];
+  auto load_af = [&](int h0) {
+#pragma unroll
+    for (int ht = 0; ht < 2; ++ht)
+#pragma unroll
+      for (int k = 0; k < KX; ++k) {
+        const size_t o = (size_t)(h0 + 16 * ht + l16) * CINP + 32 * k + 8 * lq;
+        afh[ht][k] = *reinterpret_cast<const half8*>(a.We + o);
+        afl[ht][k] = *reinterpret_cast<const half8*>(a.We + a.we_lo + o);
+      }
+  };
+  if constexpr (EXPAND) load_af(0);
+
+  // ---- stage the block input tile (zeros outside the image and past cin)
+  if constexpr (STEM == 0) {
+    // f32 -> hi / lo planes: x - hi is exact in f32, lo = f16(x - hi)
+    constexpr int C4 = CINP / 4;
+    constexpr int NIT = (MP * C4 + 255) / 256;
+    const float* xin = reinterpret_cast<const float*>(a.x) + (size_t)n * H * H * a.cin;
+    float4 v[NIT];
+#pragma unroll
+    for (int j = 0; j < NIT; ++j) {  // all loads first ...
+      const int i = tid + 256 * j;
+      const int p = i / C4, c4 = i - (i / C4) * C4;
+      const int py = p / IR, px = p - (p / IR) * IR;
+      const int iy = iy0 + py, ix = ix0 + px;
+      v[j] = make_float4(0.f, 0.f, 0.f, 0.f);
+      if (i < MP * C4 && p < NP && iy >= 0 && iy < H && ix >= 0 && ix < H && c4 * 4 < a.cin)
+        v[j] = *reinterpret_cast<const float4*>(xin + ((size_t)iy * H + ix) * a.cin + c4 * 4);
+    }
+    bool bad = false;
+#pragma unroll
+    for (int j = 0; j < NIT; ++j) {  // ... then the split and the LDS stores
+      const int i = tid + 256 * j;
+      const int p = i / C4, c4 = i - (i / C4) * C4;
+      if (i < MP * C4) {
+        const half4 h = {(f16)v[j].x, (f16)v[j].y, (f16)v[j].z, (f16)v[j].w};
+        const half4 l = {(f16)(v[j].x - (float)h[0]), (f16)(v[j].y - (float)h[1]), (f16)(v[j].z - (float)h[2]),
+                         (f16)(v[j].w - (float)h[3])};
+        *reinterpret_cast<half4*>(sXh + p * XLD + c4 * 4) = h;
+        *reinterpret_cast<half4*>(sXl + p * XLD + c4 * 4) = l;
+        bad |= x3_out_of_range4(v[j]);
+      }
+    }
+    x3_raise(a.flag, bad);
+  } else {
+    // stem conv 3x3/2 pad 1 on the u8 image for stem pixel (iy, ix) of the 112x112 grid, in fp32
+    const uint8_t* img = reinterpret_cast<const uint8_t*>(a.x) + (size_t)n * 224 * 224 * STEM;
+    const int ry0 = 2 * iy0 - 1, rx0 = 2 * ix0 - 1;
+    for (int i = tid; i < PR * PR * STEM; i += 256) {
+      const int c = i % STEM, pix = i / STEM;
+      const int yy = ry0 + pix / PR, xx = rx0 + pix % PR;
+      sPatch[i] = (yy >= 0 && yy < 224 && xx >= 0 && xx < 224) ? img[((size_t)yy * 224 + xx) * STEM + c] : 0;
+    }
+    for (int i = tid; i < STEM * 9 * 8; i += 256)
+      reinterpret_cast<float4*>(sSW)[i] = reinterpret_cast<const float4*>(a.stem_w)[i];
+    __syncthreads();
+    for (int i = tid; i < MP * 4; i += 256) {
+      const int p = i >> 2, cg = i & 3;
+      const int py = p / IR, px = p - (p / IR) * IR;
+      const int iy = iy0 + py, ix = ix0 + px;
+      float acc[8] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
+      if (p < NP && iy >= 0 && iy < 112 && ix >= 0 && ix < 112) {
+        const int cls = (iy == 0 ? 2 : 0) + (ix == 0 ? 1 : 0);
+        const float4 c0 = *reinterpret_cast<const float4*>(a.stem_corr + cls * 32 + cg * 8);
+        const float4 c1 = *reinterpret_cast<const float4*>(a.stem_corr + cls * 32 + cg * 8 + 4);
+        acc[0] = c0.x; acc[1] = c0.y; acc[2] = c0.z; acc[3] = c0.w;
+        acc[4] = c1.x; acc[5] = c1.y; acc[6] = c1.z; acc[7] = c1.w;
+#pragma unroll
+        for (int ky = 0; ky < 3; ++ky)
+#pragma unroll
+          for (int kx = 0; kx < 3; ++kx)
+#pragma unroll
+            for (int c = 0; c < STEM; ++c) {
+              const float u = (float)sPatch[((2 * py + ky) * PR + 2 * px + kx) * STEM + c];
+              const float* w = sSW + ((c * 3 + ky) * 3 + kx) * 32 + cg * 8;
+              const float4 w0 = *reinterpret_cast<const float4*>(w);
+              const float4 w1 = *reinterpret_cast<const float4*>(w + 4);
+              acc[0] = __builtin_fmaf(u, w0.x, acc[0]); acc[1] = __builtin_fmaf(u, w0.y, acc[1]);
+              acc[2] = __builtin_fmaf(u, w0.z, acc[2]); acc[3] = __builtin_fmaf(u, w0.w, acc[3]);
+              acc[4] = __builtin_fmaf(u, w1.x, acc[4]); acc[5] = __builtin_fmaf(u, w1.y, acc[5]);
+              acc[6] = __builtin_fmaf(u, w1.z, acc[6]); acc[7] = __builtin_fmaf(u, w1.w, acc[7]);
+            }
+#pragma unroll
+        for (int j = 0; j < 8; ++j) acc[j] = relu6x(acc[j]);
+      }
+      *reinterpret_cast<float4*>(sXf + p * XF + cg * 8) = make_float4(acc[0], acc[1], acc[2], acc[3]);
+      *reinterpret_cast<float4*>(sXf + p * XF + cg * 8 + 4) = make_float4(acc[4], acc[5], acc[6], acc[7]);
+    }
+  }
+  __syncthreads();
+
+  floatx4 acc[OT];
+#pragma unroll
+  for (int o = 0; o < OT; ++o) acc[o] = floatx4{0.f, 0.f, 0.f, 0.f};
+
+  // depthwise item of this thread: output pixel dq, channels 8 dcg .. 8 dcg + 7 of the chunk
+  const int dq = tid >> 2, dcg = tid & 3;
+  const int dqy = dq / TO, dqx = dq - (dq / TO) * TO;
+  const int dp0 = (dqy * S) * IR + dqx * S;  // top-left tap of the 3x3 window
+  const float* wdsrc = G::DWL ? sWd : a.Wd;
+
+#pragma unroll 1
+  for (int h0 = 0; h0 < HIDP; h0 += MX_HC) {
+    // project weights of this chunk (hi and lo): in flight during expand + depthwise
+    half8 pfh[OT], pfl[OT];
+#pragma unroll
+    for (int o = 0; o < OT; ++o) {
+      const size_t off = (size_t)(16 * o + l16) * HIDP + h0 + 8 * lq;
+      pfh[o] = *reinterpret_cast<const half8*>(a.Wp + off);
+      pfl[o] = *reinterpret_cast<const half8*>(a.Wp + a.wp_lo + off);
+    }
+    const float* src;  // fp32 depthwise input for this chunk: row p at src + p * sld
+    int sld;
+    if constexpr (EXPAND) {
+      // E^T[h][p] = sum_c We[h0+h][c] X[p][c] (A = weights, B = X^T: a lane ends with 4 consecutive
+      // hidden channels of one pixel); per 32-deep k chunk the split engine's terms lo.hi, hi.lo, hi.hi
+      float eb[2][4];
+#pragma unroll
+      for (int ht = 0; ht < 2; ++ht)
+#pragma unroll
+        for (int e = 0; e < 4; ++e) eb[ht][e] = sBe[h0 + 16 * ht + 4 * lq + e];
+      for (int pt = wave; pt < MP / 16; pt += 4) {
+        const int p = pt * 16 + l16;
+        const int py = p / IR, px = p - (p / IR) * IR;
+        const int iy = iy0 + py, ix = ix0 + px;
+        const bool valid = p < NP && iy >= 0 && iy < H && ix >= 0 && ix < H;
+        floatx4 e2[2] = {floatx4{0.f, 0.f, 0.f, 0.f}, floatx4{0.f, 0.f, 0.f, 0.f}};
+#pragma unroll
+        for (int k = 0; k < KX; ++k) {
+          const half8 bh = *reinterpret_cast<const half8*>(sXh + p * XLD + 32 * k + 8 * lq);
+          const half8 bl = *reinterpret_cast<const half8*>(sXl + p * XLD + 32 * k + 8 * lq);
+#pragma unroll
+          for (int ht = 0; ht < 2; ++ht) {
+            e2[ht] = __builtin_amdgcn_mfma_f32_16x16x32_f16(afl[ht][k], bh, e2[ht], 0, 0, 0);
+            e2[ht] = __builtin_amdgcn_mfma_f32_16x16x32_f16(afh[ht][k], bl, e2[ht], 0, 0, 0);
+            e2[ht] = __builtin_amdgcn_mfma_f32_16x16x32_f16(afh[ht][k], bh, e2[ht], 0, 0, 0);
+          }
+        }
+#pragma unroll
+        for (int ht = 0; ht < 2; ++ht) {
+          float4 ev;
+          ev.x = valid ? relu6x(__builtin_fmaf(e2[ht][0], a.we_scale, eb[ht][0])) : 0.f;  // dw zero pad
+          ev.y = valid ? relu6x(__builtin_fmaf(e2[ht][1], a.we_scale, eb[ht][1])) : 0.f;
+          ev.z = valid ? relu6x(__builtin_fmaf(e2[ht][2], a.we_scale, eb[ht][2])) : 0.f;
+          ev.w = valid ? relu6x(__builtin_fmaf(e2[ht][3], a.we_scale, eb[ht][3])) : 0.f;
+          *reinterpret_cast<float4*>(sE + p * EF + 16 * ht + 4 * lq) = ev;
+        }
+      }
+      if (h0 + MX_HC < HIDP) load_af(h0 + MX_HC);  // next chunk's expand weights: in flight during dw + project
+      __syncthreads();
+      src = sE;
+      sld = EF;
+    } else {
+      src = sXf + h0;
+      sld = XF;
+    }
+
+    // ---- depthwise 3x3/S + BN + ReLU6 (fp32) -> sDh / sDl planes [q][h]
+    {
+      half8 oh = {0, 0, 0, 0, 0, 0, 0, 0}, ol = {0, 0, 0, 0, 0, 0, 0, 0};
+      if (dq < NQ) {
+        const int hc = h0 + 8 * dcg;
+        float d[8];
+        {
+          const float4 b0 = *reinterpret_cast<const float4*>(sBd + hc);
+          const float4 b1 = *reinterpret_cast<const float4*>(sBd + hc + 4);
+          d[0] = b0.x; d[1] = b0.y; d[2] = b0.z; d[3] = b0.w; d[4] = b1.x; d[5] = b1.y; d[6] = b1.z; d[7] = b1.w;
+        }
+        const float* wd = wdsrc + (size_t)(hc / 8) * 72;
+#pragma unroll
+        for (int ky = 0; ky < 3; ++ky)
+#pragma unroll
+          for (int kx = 0; kx < 3; ++kx) {
+            const float* ep = src + (dp0 + ky * IR + kx) * sld + 8 * dcg;
+            const float4 e0 = *reinterpret_cast<const float4*>(ep);
+            const float4 e1 = *reinterpret_cast<const float4*>(ep + 4);
+            const float4 w0 = *reinterpret_cast<const float4*>(wd + (ky * 3 + kx) * 8);
+            const float4 w1 = *reinterpret_cast<const float4*>(wd + (ky * 3 + kx) * 8 + 4);
+            d[0] = __builtin_fmaf(e0.x, w0.x, d[0]); d[1] = __builtin_fmaf(e0.y, w0.y, d[1]);
+            d[2] = __builtin_fmaf(e0.z, w0.z, d[2]); d[3] = __builtin_fmaf(e0.w, w0.w, d[3]);
+            d[4] = __builtin_fmaf(e1.x, w1.x, d[4]); d[5] = __builtin_fmaf(e1.y, w1.y, d[5]);
+            d[6] = __builtin_fmaf(e1.z, w1.z, d[6]); d[7] = __builtin_fmaf(e1.w, w1.w, d[7]);
+          }
+#pragma unroll
+        for (int j = 0; j < 8; ++j) {
+          const float v = relu6x(d[j]);  // in [0, 6]: always inside the f16 range
+          oh[j] = (f16)v;
+          ol[j] = (f16)(v - (float)oh[j]);
+        }
+      }
+      *reinterpret_cast<half8*>(sDh + dq * ELD + 8 * dcg) = oh;
+      *reinterpret_cast<half8*>(sDl + dq * ELD + 8 * dcg) = ol;
+    }
+    __syncthreads();
+
+    // ---- project: out^T[o][q] += Wp[o][h0..h0+31] . D[q][:]; wave w owns pixels 16w..16w+15
+    {
+      const half8 bh = *reinterpret_cast<const half8*>(sDh + (16 * wave + l16) * ELD + 8 * lq);
+      const half8 bl = *reinterpret_cast<const half8*>(sDl + (16 * wave + l16) * ELD + 8 * lq);
+#pragma unroll
+      for (int o = 0; o < OT; ++o) {
+        acc[o] = __builtin_amdgcn_mfma_f32_16x16x32_f16(pfl[o], bh, acc[o], 0, 0, 0);
+        acc[o] = __builtin_amdgcn_mfma_f32_16x16x32_f16(pfh[o], bl, acc[o], 0, 0, 0);
+        acc[o] = __builtin_amdgcn_mfma_f32_16x16x32_f16(pfh[o], bh, acc[o], 0, 0, 0);
+      }
+    }
+    if constexpr (!EXPAND) __syncthreads();  // next chunk's dw rewrites sD
+  }
+
+  // ---- epilogue: acc 2^-e + BN shift (+ the exact f32 block input) -> f32 NHWC
+  {
+    const int q = 16 * wave + l16;
+    if (q < NQ) {
+      const int qy = q / TO, qx = q - (q / TO) * TO;
+      const size_t pix = (size_t)n * a.OH * a.OH + (size_t)(oy0 + qy) * a.OH + ox0 + qx;
+      float4 r[OT];
+      if constexpr (RES) {  // stride 1 and cin == cout: the same pixel of the block input
+#pragma unroll
+        for (int o = 0; o < OT; ++o) {
+          const int c = 16 * o + 4 * lq;
+          r[o] = c < a.cout ? *reinterpret_cast<const float4*>(reinterpret_cast<const float*>(a.x) + pix * a.cin + c)
+                            : make_float4(0.f, 0.f, 0.f, 0.f);
+        }
+      }
+#pragma unroll
+      for (int o = 0; o < OT; ++o) {
+        const int c = 16 * o + 4 * lq;
+        if (c >= a.cout) continue;
+        const float4 bv = *reinterpret_cast<const float4*>(sBp + c);
+        float4 v = make_float4(__builtin_fmaf(acc[o][0], a.wp_scale, bv.x), __builtin_fmaf(acc[o][1], a.wp_scale, bv.y),
+                               __builtin_fmaf(acc[o][2], a.wp_scale, bv.z), __builtin_fmaf(acc[o][3], a.wp_scale, bv.w));
+        if constexpr (RES) {
+          v.x += r[o].x; v.y += r[o].y; v.z += r[o].z; v.w += r[o].w;
+        }
+        *reinterpret_cast<float4*>(a.y + pix * a.cout + c) = v;
+      }
+    }
+  }
+}
+
+// f32 [n4 * 4] -> f16 hi / lo planes (the features[18] GEMM's A operand)
+__global__ __launch_bounds__(256) void mbv2_split_kernel(const float* __restrict__ x, size_t n4, f16* __restrict__ hi,
+                                                         long long lo, unsigned* flag) {
+  const size_t i = (size_t)blockIdx.x * 256 + threadIdx.x;
+  if (i >= n4) return;
+  const float4 v = reinterpret_cast<const float4*>(x)[i];
+  const half4 h = {(f16)v.x, (f16)v.y, (f16)v.z, (f16)v.w};
+  const half4 l = {(f16)(v.x - (float)h[0]), (f16)(v.y - (float)h[1]), (f16)(v.z - (float)h[2]),
+                   (f16)(v.w - (float)h[3])};
+  reinterpret_cast<half4*>(hi)[i] = h;
+  reinterpret_cast<half4*>(hi + lo)[i] = l;
+  x3_raise(flag, x3_out_of_range4(v));
+}
+
+template <int S, int TO, int CINP, int HIDP, int COUTP, bool EXPAND, bool RES, int STEM>
+int launch_x3_block(const MbX3Args& a, int B, hipStream_t s) {
+  const int tpr = a.OH / TO;
+  hipLaunchKernelGGL((mbv2_x3_kernel<S, TO, CINP, HIDP, COUTP, EXPAND, RES, STEM>), dim3(B * tpr * tpr), dim3(256),
+                     0, s, a);
+  MEC_LAUNCH_CHECK();
+  return 0;
+}
+
+// The 17 block shapes of mobilenet_v2 at 224x224 (as mobilenet.hip dispatch_block)
+int dispatch_x3_block(const MbBlock& b, const MbX3Args& a, int B, int stem_c, hipStream_t s) {
+  const bool res = b.stride == 1 && b.cin == b.cout;
+  const int TO = (a.OH % 8 == 0) ? 8 : 7;
+#define MX_CASE(S_, TO_, CI_, HI_, CO_, RS_)                                                                      \
+  if (b.stride == S_ && TO == TO_ && b.cinp == CI_ && b.hidp == HI_ && b.coutp == CO_ && b.t != 1 && res == RS_) \
+    return launch_x3_block<S_, TO_, CI_, HI_, CO_, true, RS_, 0>(a, B, s);
+  if (b.t == 1) {
+    MEC_REQUIRE(b.stride == 1 && b.cinp == 32 && b.hidp == 32 && b.coutp == 16 && !res && TO == 8 && stem_c,
+                "mbv2 x3: block 1 shape");
+    if (stem_c == 3) return launch_x3_block<1, 8, 32, 32, 16, false, false, 3>(a, B, s);
+    return launch_x3_block<1, 8, 32, 32, 16, false, false, 1>(a, B, s);
+  }
+  MX_CASE(2, 8, 32, 96, 32, false)     // 16 -> 24, 112 -> 56
+  MX_CASE(1, 8, 32, 160, 32, true)     // 24 -> 24 @ 56
+  MX_CASE(2, 7, 32, 160, 32, false)    // 24 -> 32, 56 -> 28
+  MX_CASE(1, 7, 32, 192, 32, true)     // 32 -> 32 @ 28
+  MX_CASE(2, 7, 32, 192, 64, false)    // 32 -> 64, 28 -> 14
+  MX_CASE(1, 7, 64, 384, 64, true)     // 64 -> 64 @ 14
+  MX_CASE(1, 7, 64, 384, 96, false)    // 64 -> 96 @ 14
+  MX_CASE(1, 7, 96, 576, 96, true)     // 96 -> 96 @ 14
+  MX_CASE(2, 7, 96, 576, 160, false)   // 96 -> 160, 14 -> 7
+  MX_CASE(1, 7, 160, 960, 160, true)   // 160 -> 160 @ 7
+  MX_CASE(1, 7, 160, 960, 320, false)  // 160 -> 320 @ 7
+#undef MX_CASE
+  set_error("mbv2 x3: no kernel instance for this block shape");
+  return -1;
+}
+
+}  // namespace
+
+// fp32x3 weights: the f16 path's layouts (channels padded to 32 / 32 / 16, depthwise [hidp/8][9][8],
+// stem folded per pixel with a border-class bias) built in fp32, then every 1x1 matrix split into
+// hi / lo planes after a per-matrix power-of-two pre-scale (split_planes)
+int MobileNetModel::create_x3(const float* blob, size_t n) {
+  BlobReader rd(blob, n);
+  std::vector<float> w, pr;
+  auto align4 = [&]() { while (pr.size() % 4) pr.push_back(0.f); };
+  auto pad_to = [](int v, int m) { return (v + m - 1) / m * m; };
+  auto bn_scale_shift = [&](int c, std::vector<double>& scale, std::vector<double>& shift) {
+    const float* g = rd.take(c);
+    const float* b = rd.take(c);
+    const float* rm = rd.take(c);
+    const float* rv = rd.take(c);
+    scale.assign(c, 0.0);
+    shift.assign(c, 0.0);
+    if (!rd.ok) return;
+    for (int i = 0; i < c; ++i) {
+      scale[i] = (double)g[i] / std::sqrt((double)rv[i] + 1e-5);
+      shift[i] = (double)b[i] - (double)rm[i] * scale[i];
+    }
+  };
+  std::vector<double> sc, sh;
+  {  // stem, as MobileNetModel::create (mobilenet.hip)
+    const float* src = rd.take((size_t)32 * 3 * 9);
+    bn_scale_shift(32, sc, sh);
+    align4();
+    stem_w_off = pr.size();
+    pr.resize(pr.size() + 9 * 32, 0.f);
+    stem_rgb_off = pr.size();
+    pr.resize(pr.size() + 27 * 32, 0.f);
+    stem_corr_off = pr.size();
+    pr.resize(pr.size() + 4 * 32, 0.f);
+    const double mean[3] = {0.485, 0.456, 0.406}, stdv[3] = {0.229, 0.224, 0.225};
+    if (rd.ok)
+      for (int o = 0; o < 32; ++o) {
+        double cterm[9] = {};
+        for (int t = 0; t < 9; ++t) {
+          double gsum = 0.0;
+          for (int c = 0; c < 3; ++c) {
+            const double wv = src[((size_t)o * 3 + c) * 9 + t];
+            const double mf = (double)(float)mean[c], sf = (double)(float)stdv[c];
+            gsum += wv / (255.0 * sf);
+            cterm[t] -= wv * mf / sf;
+            pr[stem_rgb_off + (size_t)(c * 9 + t) * 32 + o] = (float)(wv / (255.0 * sf) * sc[o]);
+          }
+          pr[stem_w_off + (size_t)t * 32 + o] = (float)(gsum * sc[o]);
+        }
+        for (int cls = 0; cls < 4; ++cls) {
+          double sum = sh[o];
+          for (int t = 0; t < 9; ++t) {
+            const int ky = t / 3, kx = t % 3;
+            if (((cls & 2) && ky == 0) || ((cls & 1) && kx == 0)) continue;
+            sum += cterm[t] * sc[o];
+          }
+          pr[stem_corr_off + (size_t)cls * 32 + o] = (float)sum;
+        }
+      }
+  }
+  static const int kSet[7][4] = {{1, 16, 1, 1}, {6, 24, 2, 2}, {6, 32, 3, 2}, {6, 64, 4, 2},
+                                 {6, 96, 3, 1}, {6, 160, 3, 2}, {6, 320, 1, 1}};
+  blocks.clear();
+  x3_scale.clear();
+  int cin = 32;
+  for (int si = 0; si < 7; ++si)
+    for (int r = 0; r < kSet[si][2]; ++r) {
+      MbBlock b;
+      b.t = kSet[si][0]; b.cin = cin; b.hid = cin * b.t; b.cout = kSet[si][1]; b.stride = r == 0 ? kSet[si][3] : 1;
+      b.cinp = pad_to(cin, 32); b.hidp = pad_to(b.hid, 32); b.coutp = pad_to(b.cout, 16);
+      if (b.t != 1) {
+        const float* we = rd.take((size_t)b.hid * cin);
+        bn_scale_shift(b.hid, sc, sh);
+        b.we_off = w.size();
+        w.resize(w.size() + (size_t)b.hidp * b.cinp, 0.f);
+        align4();
+        b.be_off = pr.size();
+        pr.resize(pr.size() + b.hidp, 0.f);
+        if (rd.ok)
+          for (int h = 0; h < b.hid; ++h) {
+            for (int c = 0; c < cin; ++c) w[b.we_off + (size_t)h * b.cinp + c] = (float)((double)we[(size_t)h * cin + c] * sc[h]);
+            pr[b.be_off + h] = (float)sh[h];
+          }
+      }
+      {
+        const float* wd = rd.take((size_t)b.hid * 9);
+        bn_scale_shift(b.hid, sc, sh);
+        align4();
+        b.wd_off = pr.size();
+        pr.resize(pr.size() + (size_t)b.hidp * 9, 0.f);
+        b.bd_off = pr.size();
+        pr.resize(pr.size() + b.hidp, 0.f);
+        if (rd.ok)
+          for (int h = 0; h < b.hid; ++h) {
+            for (int t = 0; t < 9; ++t)
+              pr[b.wd_off + (size_t)(h / 8) * 72 + t * 8 + (h % 8)] = (float)((double)wd[(size_t)h * 9 + t] * sc[h]);
+            pr[b.bd_off + h] = (float)sh[h];
+          }
+      }
+      {
+        const float* wp = rd.take((size_t)b.cout * b.hid);
+        bn_scale_shift(b.cout, sc, sh);
+        b.wp_off = w.size();
+        w.resize(w.size() + (size_t)b.coutp * b.hidp, 0.f);
+        align4();
+        b.bp_off = pr.size();
+        pr.resize(pr.size() + b.coutp, 0.f);
+        if (rd.ok)
+          for (int o = 0; o < b.cout; ++o) {
+            for (int h = 0; h < b.hid; ++h) w[b.wp_off + (size_t)o * b.hidp + h] = (float)((double)wp[(size_t)o * b.hid + h] * sc[o]);
+            pr[b.bp_off + o] = (float)sh[o];
+          }
+      }
+      blocks.push_back(b);
+      cin = b.cout;
+    }
+  {  // features[18]: [1280][320]
+    const float* wl = rd.take((size_t)1280 * 320);
+    bn_scale_shift(1280, sc, sh);
+    last_w_off = w.size();
+    w.resize(w.size() + (size_t)1280 * 320, 0.f);
+    align4();
+    last_b_off = pr.size();
+    pr.resize(pr.size() + 1280, 0.f);
+    if (rd.ok)
+      for (int o = 0; o < 1280; ++o) {
+        for (int c = 0; c < 320; ++c) w[last_w_off + (size_t)o * 320 + c] = (float)((double)wl[(size_t)o * 320 + c] * sc[o]);
+        pr[last_b_off + o] = (float)sh[o];
+      }
+  }
+  const float* f1w = rd.take((size_t)512 * 1280);
+  const float* f1b = rd.take(512);
+  const float* f2w = rd.take((size_t)7 * 512);
+  const float* f2b = rd.take(7);
+  MEC_REQUIRE(rd.ok && rd.off == n, "image_mbv2 blob size mismatch");
+  align4();
+  fc1_off = pr.size();
+  pr.resize(pr.size() + (size_t)1280 * 512);
+  for (int i = 0; i < 1280; ++i)
+    for (int j = 0; j < 512; ++j) pr[fc1_off + (size_t)i * 512 + j] = f1w[(size_t)j * 1280 + i];
+  fc1b_off = pr.size();
+  pr.insert(pr.end(), f1b, f1b + 512);
+  fc2_off = pr.size();
+  pr.resize(pr.size() + 512 * 7);
+  for (int i = 0; i < 512; ++i)
+    for (int j = 0; j < 7; ++j) pr[fc2_off + (size_t)i * 7 + j] = f2w[(size_t)j * 512 + i];
+  fc2b_off = pr.size();
+  pr.insert(pr.end(), f2b, f2b + 7);
+  // split every 1x1 matrix: hi planes at the f32 offsets, lo planes x3_lo halfs later
+  x3_lo = w.size();
+  std::vector<f16> hl(2 * w.size(), (f16)0.f);
+  auto split = [&](size_t off, size_t cnt) { return split_planes(w.data() + off, cnt, hl.data() + off, hl.data() + x3_lo + off); };
+  for (MbBlock& b : blocks) {
+    x3_scale.push_back(b.t != 1 ? split(b.we_off, (size_t)b.hidp * b.cinp) : 1.f);
+    x3_scale.push_back(split(b.wp_off, (size_t)b.coutp * b.hidp));
+  }
+  x3_scale.push_back(split(last_w_off, (size_t)1280 * 320));
+  MEC_TRY(upload(wts, hl.data(), hl.size() * sizeof(f16)));
+  MEC_TRY(upload(prm, pr.data(), pr.size() * sizeof(float)));
+  return 0;
+}
+
+int MobileNetModel::forward_x3(const uint8_t* img, int B, int H, int W, int C, float* feat, float* logits,
+                               float* probs, hipStream_t s) {
+  MEC_REQUIRE(wts.p && x3_lo && x3_scale.size() == 2 * blocks.size() + 1, "image_mbv2: fp32x3 weights missing");
+  const bool fer = (H == 48 && W == 48 && C == 1);
+  const size_t per_big = (size_t)112 * 112 * 16;  // largest block output (features[1]), floats
+  const size_t per_last = (size_t)49 * 1280, per_in = (size_t)49 * 320;
+  const size_t per_img = 224 * 224 + (2 * per_big + per_last + 1280) * sizeof(float) + per_in * 2 * sizeof(f16);
+  const size_t need = per_img * (size_t)B + 8192;
+  if (ws.bytes < need) MEC_TRY(ws.ensure(need));
+  char* p = ws.as<char>();
+  uint8_t* resized = reinterpret_cast<uint8_t*>(p);
+  p += ((size_t)B * 224 * 224 + 255) / 256 * 256;
+  float* X = reinterpret_cast<float*>(p); p += (size_t)B * per_big * sizeof(float);
+  float* Y = reinterpret_cast<float*>(p); p += (size_t)B * per_big * sizeof(float);
+  float* Lst = reinterpret_cast<float*>(p); p += (size_t)B * per_last * sizeof(float);
+  float* pooled = reinterpret_cast<float*>(p); p += (size_t)B * 1280 * sizeof(float);
+  f16* Lin = reinterpret_cast<f16*>(p);  // features[18]'s A planes [B*49, 320] (lo at + B*49*320)
+
+  const f16* Wt = wts.as<f16>();
+  const long long wlo = (long long)x3_lo;
+  const float* P = prm.as<float>();
+  const uint8_t* stem_in = img;
+  if (fer) {
+    MEC_TRY(resize_u8(img, B, 48, 48, resized, 224, 224, s));
+    stem_in = resized;
+  }
+  MEC_TRY(prof.begin(TAG_MBV2_BLOCK, s));
+  const void* cur = stem_in;
+  float* out = X;
+  int h = 112;
+  for (size_t i = 0; i < blocks.size(); ++i) {
+    const MbBlock& b = blocks[i];
+    MbX3Args a;
+    a.x = cur; a.y = out; a.H = h; a.OH = b.stride == 2 ? h / 2 : h;
+    a.cin = b.cin; a.cout = b.cout;
+    a.We = Wt + b.we_off; a.we_lo = wlo; a.we_scale = x3_scale[2 * i];
+    a.be = P + b.be_off; a.Wd = P + b.wd_off; a.bd = P + b.bd_off;
+    a.Wp = Wt + b.wp_off; a.wp_lo = wlo; a.wp_scale = x3_scale[2 * i + 1];
+    a.bp = P + b.bp_off;
+    a.stem_w = P + (C == 3 ? stem_rgb_off : stem_w_off);
+    a.stem_corr = P + stem_corr_off;
+    a.flag = range_flag();
+    MEC_TRY(dispatch_x3_block(b, a, B, i == 0 ? (C == 3 ? 3 : 1) : 0, s));
+    cur = out;
+    out = (out == X) ? Y : X;
+    h = a.OH;
+  }
+  MEC_TRY(prof.end(TAG_MBV2_BLOCK, s));
+  {  // features[18] 1x1 320 -> 1280 + BN + ReLU6 on the split GEMM engine
+    const size_t n4 = (size_t)B * h * h * 320 / 4;
+    const long long llo = (long long)B * h * h * 320;
+    hipLaunchKernelGGL(mbv2_split_kernel, dim3((unsigned)((n4 + 255) / 256)), dim3(256), 0, s,
+                       reinterpret_cast<const float*>(cur), n4, Lin, llo, range_flag());
+    MEC_LAUNCH_CHECK();
+    GemmParams g;
+    g.split = 1; g.A = Lin; g.a_lo = llo; g.B = Wt + last_w_off; g.b_lo = wlo; g.oscale = x3_scale.back();
+    g.bias = P + last_b_off; g.act = ACT_RELU6; g.C32 = Lst;
+    g.M = B * h * h; g.N = 1280; g.K = 320;
+    MEC_TRY(launch_gemm(g, s, &prof, TAG_MBV2_LAST));
+  }
+  hipLaunchKernelGGL(avgpool_f32_kernel, dim3(B, 1280 / 256), dim3(256), 0, s, Lst, h * h, 1280, pooled);
+  MEC_LAUNCH_CHECK();
+  MEC_TRY(launch_linear_mfma<BACT_RELU>(pooled, 1280, B, 1280, P + fc1_off, P + fc1b_off, 512, feat, 512, nullptr, 0, s));
+  MEC_TRY(launch_head7(feat, B, 512, P + fc2_off, P + fc2b_off, logits, probs, s));
+  return 0;
+}
+
+}  // namespace mec

@@ -207,6 +207,13 @@ struct MobileNetModel : ImageNet {
                  hipStream_t s) override;
   int forward_f32(const uint8_t* img, int B, int H, int W, int C, float* feat, float* logits, float* probs,
                   hipStream_t s);
+  // fp32x3 path (mobilenet_x3.hip): wts holds every 1x1 matrix's f16 hi planes (f16 path layouts), then
+  // the lo planes at x3_lo halfs; x3_scale: per block (expand, project) epilogue scales, then features[18]
+  size_t x3_lo = 0;
+  std::vector<float> x3_scale;
+  int create_x3(const float* blob, size_t n);
+  int forward_x3(const uint8_t* img, int B, int H, int W, int C, float* feat, float* logits, float* probs,
+                 hipStream_t s);
 };
 
 int resize_u8(const uint8_t* in, int B, int H, int W, uint8_t* out, int OH, int OW, hipStream_t s);

@@ -431,3 +431,50 @@ def test_text_fp32x3_fused_qkv_attention_bit_identical(dev, B, ragged):
         enc.close()
     for k, (a, b) in enumerate(zip(*outs)):
         assert np.array_equal(a, b), f'output {k}: max |d| {np.abs(a - b).max()}'
+
+
+# ------------------------------------------------------------------ MobileNetV2 on the fp32x3 path
+@pytest.mark.parametrize('B', [3, 64, 256])
+def test_mobilenet_v2_fp32x3_vs_oracle(dev, B):
+    """MobileNetV2 (BASELINE configs[1], parity unpinned: no reference code) on the fp32x3 path
+    (csrc/mobilenet_x3.hip: one fused kernel per block, 1x1 products on split f16 operands, fp32
+    depthwise and block outputs) against the oracle at the fp32 bars: probs within 1e-5, feature
+    within 1e-4 relative, argmax exact; the exact-fp32 path's error printed beside it."""
+    from oracle import image_mbv2 as o_mb
+    gray = syn.image_inputs(B, seed=90 + B)
+    g = engine.to_device(gray, dev)
+    enc = engine.MobileNetImageEncoder(device=dev, precision='fp32x3')
+    feat, logits, probs = _np(enc.forward(g))
+    enc.check()
+    feat32, _, probs32 = _np(engine.MobileNetImageEncoder(device=dev, precision='fp32').forward(g))
+    sub = np.unique(np.r_[0, np.arange(0, B, max(1, B // 16)), B - 1])
+    rf, rl, rp = o_mb.forward(syn.weights('image_mbv2'), gray[sub])
+    err, agree = _report(f'mobilenet_v2 fp32x3 B={B}', probs[sub], rp, probs32[sub])
+    ferr = float(np.abs(feat[sub] - rf).max() / np.abs(rf).max())
+    print(f'  feat rel err {ferr:.3g} (fp32 path {float(np.abs(feat32[sub] - rf).max() / np.abs(rf).max()):.3g}), '
+          f'logits max|d| {np.abs(logits[sub] - rl).max():.3g}')
+    assert agree == len(sub) and err <= PROB_TOL and ferr <= FEAT_RTOL
+
+
+def test_mobilenet_v2_fp32x3_batch_invariance_and_entry_shapes(dev):
+    """Rows of a B=64 batch equal the same rows run as B=8 bit for bit (per-tile kernels, and the
+    features[18] split GEMM's interleaved tiles share one k order); the RGB and already-resized
+    224 gray entry shapes through the fp32x3 stem against the oracle."""
+    from oracle import image_mbv2 as o_mb
+    enc = engine.MobileNetImageEncoder(device=dev, precision='fp32x3')
+    g = engine.to_device(syn.image_inputs(64, seed=99), dev)
+    big = [t[:8].cpu() for t in enc.forward(g)]
+    small = [t.cpu() for t in enc.forward(g[:8])]
+    for i, (a, b) in enumerate(zip(big, small)):
+        assert torch.equal(a, b), f'output {i}'
+    rgb = np.stack([syn.image_inputs(2, seed=170 + c).repeat(4, axis=1).repeat(4, axis=2)[:, :224, :224]
+                    for c in range(3)], -1)
+    rgb = np.ascontiguousarray(np.pad(rgb, ((0, 0), (0, 32), (0, 32), (0, 0)))[:, :224, :224])
+    _, _, probs = _np(enc.forward_u8(engine.to_device(rgb, dev)))
+    _, _, rp = o_mb.forward_resized(syn.weights('image_mbv2'), rgb)
+    assert np.abs(probs - rp).max() <= PROB_TOL and (probs.argmax(1) == rp.argmax(1)).all()
+    g224 = np.ascontiguousarray(rgb[..., 0])
+    _, _, probs = _np(enc.forward_u8(engine.to_device(g224[..., None], dev)))
+    _, _, rp = o_mb.forward_resized(syn.weights('image_mbv2'), g224)
+    assert np.abs(probs - rp).max() <= PROB_TOL
+    enc.check()
