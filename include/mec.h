@@ -52,11 +52,14 @@ int mec_create(int kind, const float* host_blob, size_t n, int device, mec_model
  * residual stream and heads. MEC_PREC_FP32: every operand and product in fp32
  * (v_mfma_f32_32x32x2_f32, an exact fmaf chain), the precision the reference computes in
  * (inference/text_inference.py:91-93, inference/image_inference.py:116-118).
- * MEC_PREC_FP32X3 (BERT, ResNet50): the fp32 path's arithmetic with every GEMM / conv operand
- * carried as an exact pair of f16 planes (x = hi + lo, 22 significant bits against fp32's 24) and
- * each product as hi.hi + hi.lo + lo.hi on the f16 MFMA into one fp32 accumulator; LayerNorm,
- * softmax, attention, GELU, residual stream and heads fp32. Speech, fusion and audio handles
- * are fp32 at every setting. */
+ * MEC_PREC_FP32X3 (BERT, ResNet50, MobileNetV2): the fp32 path's arithmetic with every GEMM / conv
+ * operand carried as a pair of f16 planes (x = hi + lo) and each product as hi.hi + hi.lo + lo.hi
+ * on the f16 MFMA into one fp32 accumulator; LayerNorm, softmax, attention, GELU, depthwise convs,
+ * residual stream and heads fp32. Envelope: weights are split after a per-matrix power-of-two
+ * pre-scale (22 significant bits each); an activation keeps 22 significant bits for
+ * 2^-3 <= |x| < 65520 and an absolute error <= 2^-25 below 2^-3 (the lo plane is then an f16
+ * subnormal); at |x| >= 65520 (or NaN / inf) the producing kernel raises the handle's range flag
+ * and mec_model_check fails. Speech, fusion and audio handles are fp32 at every setting. */
 enum { MEC_PREC_F16 = 0, MEC_PREC_FP32 = 1, MEC_PREC_FP32X3 = 2 };
 int mec_create_ex(int kind, const float* host_blob, size_t n, int device, int precision, mec_model** out);
 /* The handle's precision (MEC_PREC_*), -1 on a null handle. */
@@ -202,9 +205,10 @@ int mec_model_gemm_query(mec_model* m, int amode, int M, int N, int K);
 /* Errors a kernel can only report after the fact, since the handle's last check: 0 = none,
  * -1 = mec_last_error() says what (and the flag is cleared). Call once the stream that ran
  * the handle's forwards has been synchronized. Speech: a stage hand-off wait of
- * speech_flow_kernel expired (that forward's probs are NaN); no such condition exists for the
- * other kinds (always 0). No reference counterpart: the reference's Keras predict has no
- * asynchronous failure (inference/speech_inference.py:69). */
+ * speech_flow_kernel expired (that forward's probs are NaN). MEC_PREC_FP32X3 text / image
+ * handles: an activation left the f16 hi / lo range (|x| >= 65520, NaN or inf; that forward's
+ * outputs are invalid). Always 0 for the other kinds and precisions. No reference counterpart:
+ * the reference's predict calls have no asynchronous failure (inference/speech_inference.py:69). */
 int mec_model_check(mec_model* m);
 
 /* hipEvent timing hook: time every launch of kernel class `tag`. */

@@ -350,7 +350,7 @@ def test_split_gemm_small_activations_absolute_floor(dev, scale):
 
 
 def _force_overflow(kind, name, factor):
-    w = syn.weights(kind)
+    w = dict(syn.weights(kind))  # a copy: syn.weights returns the cached dict every handle shares
     w[name] = (w[name] * np.float32(factor)).astype(np.float32)
     return w
 
