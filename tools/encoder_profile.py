@@ -45,7 +45,7 @@ def main():
         g = engine.to_device(syn.image_inputs(B, seed=0), dev)
         fn = lambda: m.forward(g)  # noqa: E731
     elif a.enc == 'image_mbv2':
-        m = engine.MobileNetImageEncoder(device=dev)
+        m = engine.MobileNetImageEncoder(device=dev, precision=a.precision)
         g = engine.to_device(syn.image_inputs(B, seed=0), dev)
         fn = lambda: m.forward(g)  # noqa: E731
     elif a.enc == 'speech':
