@@ -39,12 +39,11 @@ int launch_gemm(const GemmParams& p0, hipStream_t s, Prof* prof, int tag) {
   if (prof) MEC_TRY(prof->begin(tag, s));
   int rc;
   if (p.split)  // split-f16 operands: the glds engine only (the halo conv kernels read one plane); autotuned,
-    // except BERT FFN1, pinned to the 256 x 256 glds tile: it and the ping-pong tile time within 3-7 %
-    // of each other (tools/bench_split.py), so the autotune flipped between them run to run, and the
-    // bench's roofline kernel (and its PMC traffic file) must be one kernel
+    // except the launch classes gemm_x3_tag pins (BERT FFN1 -> 70256 by default, mec_common.h); the
+    // pass-major order pins FFN1 to 10256 (it and the ping-pong tile time within 3-7 %, tools/bench_split.py)
     rc = launch_gemm_glds(p, s, opt().gemm_bn ? opt().gemm_bn
-                                : tag == TAG_BERT_FFN1 ? (opt().gemm_x3_order ? 70256 : 10256)
-                                : (opt().gemm_x3_order && tag > 0 && tag < TAG_COUNT) ? opt().gemm_x3_tag[tag] : 0);
+                                : !opt().gemm_x3_order ? (tag == TAG_BERT_FFN1 ? 10256 : 0)
+                                : (tag > 0 && tag < TAG_COUNT) ? opt().gemm_x3_tag[tag] : 0);
   else if (opt().conv3x3_direct && !opt().gemm_bn && p.amode == A_CONV && p.ks == 3 && p.stride == 1 && p.pad == 1 && p.H == 56 &&
       p.W == 56 && p.C == 64 && p.N == 64 && p.act == ACT_RELU && !p.R && p.C16 && !p.C32 && p.M % (56 * 56) == 0)
     rc = launch_conv3x3_c64(reinterpret_cast<const f16*>(p.A), p.B, p.bias, p.C16, p.M / (56 * 56), 56, 64, 64, s);

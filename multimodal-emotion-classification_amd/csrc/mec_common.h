@@ -118,9 +118,11 @@ struct Options {
   // MFMA, a higher held clock: text 18.84 -> 17.96 ms, ResNet50 10.06 -> 9.00, fused step 28.05 ->
   // 26.19 ms at B = 256 (profiles/r03_ab_x3order_*.txt)
   int gemm_x3_order = 1;
-  // K-interleaved split engine, per launch class: forced tile (7xxxx), 0 = autotune (BERT FFN1 is
-  // pinned to 70256 separately, gemm.hip)
-  int gemm_x3_tag[TAG_COUNT] = {0};
+  // K-interleaved split engine, per launch class: forced tile (7xxxx), 0 = autotune. BERT FFN1 is
+  // pinned to 70256 by default: it and the other tiles time within a few % of each other alone, so an
+  // autotune would flip between them run to run, and the bench's roofline kernel (and its PMC traffic
+  // file) must be one kernel
+  int gemm_x3_tag[TAG_COUNT] = {0, 0, 0, 0, /*TAG_BERT_FFN1*/ 70256};
   // fp32x3 BERT FFN1 GELU: 1 = ACT_GELU_F32 (branch-free erf, one-instruction exp; max |error| /
   // max(|x|, 1) 1.21e-7 against float64, the correctly rounded erf's 1.06e-7), 0 = libm erff
   int gelu_x3 = 1;

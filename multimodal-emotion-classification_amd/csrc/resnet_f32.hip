@@ -712,38 +712,62 @@ int ImageModel::forward_x3(const uint8_t* img, int B, int H, int W, int C, float
     MEC_LAUNCH_CHECK();
   }
   MEC_TRY(prof.end(TAG_RESNET_STEM, s));
-  GemmParams g;
+  // Bottleneck blocks [b0, b1) over images [i0, i0 + nb) (NHWC planes are image-major: an image range
+  // is a pointer offset; the lo planes stay L elements after their hi planes). cur/other swap per block.
+  auto run_blocks = [&](size_t b0, size_t b1, int i0, int nb, int Hin, f16*& cur, f16*& other) -> int {
+    int Hc = Hin;
+    for (size_t bi = b0; bi < b1; ++bi) {
+      const Bottleneck& bk = blocks[bi];
+      const int wd = bk.c1.cout, cin = bk.c1.cin, st = bk.c2.stride;
+      const int OH = (Hc + 2 - 3) / st + 1;
+      f16* in = cur + (size_t)i0 * Hc * Hc * cin;
+      f16* out = other + (size_t)i0 * OH * OH * 4 * wd;
+      f16* t1 = T1 + (size_t)i0 * Hc * Hc * wd;
+      f16* t2 = T2 + (size_t)i0 * OH * OH * wd;
+      GemmParams g;
+      g.split = 1; g.A = in; g.a_lo = L; g.B = Wt + bk.c1.w_off; g.b_lo = wlo; g.oscale = bk.c1.x3_scale;
+      g.bias = P + bk.c1.b_off; g.act = ACT_RELU; g.C16 = t1; g.c_lo = L;
+      g.M = nb * Hc * Hc; g.N = wd; g.K = cin;
+      MEC_TRY(launch_gemm(g, s, &prof, TAG_RESNET_CONV1X1));
+      g = GemmParams();
+      g.split = 1; g.amode = A_CONV; g.A = t1; g.a_lo = L; g.B = Wt + bk.c2.w_off; g.b_lo = wlo;
+      g.oscale = bk.c2.x3_scale; g.bias = P + bk.c2.b_off; g.act = ACT_RELU; g.C16 = t2; g.c_lo = L;
+      g.M = nb * OH * OH; g.N = wd; g.K = 9 * wd;
+      g.H = Hc; g.W = Hc; g.C = wd; g.OH = OH; g.OW = OH; g.ks = 3; g.stride = st; g.pad = 1;
+      MEC_TRY(launch_gemm(g, s, &prof, TAG_RESNET_CONV3X3));
+      g = GemmParams();
+      g.split = 1; g.a_lo = L; g.act = ACT_RELU; g.C16 = out; g.c_lo = L; g.M = nb * OH * OH; g.N = 4 * wd;
+      if (bk.has_ds) {  // relu(bn3(conv3(t2)) + bn_ds(conv_ds/s(x))) as one GEMM over K = [w | cin]
+        g.amode = A_DUAL; g.A = t2; g.K1 = wd; g.A2 = in; g.B = Wd + bk.c3ds_w_off; g.b_lo = (long long)bk.c3ds_x3_lo;
+        g.oscale = bk.c3ds_x3_scale; g.bias = P + bk.c3ds_b_off; g.K = wd + cin;
+        g.H = Hc; g.W = Hc; g.C = cin; g.OH = OH; g.OW = OH; g.ks = 1; g.stride = st; g.pad = 0;
+      } else {  // relu(bn3(conv3(t2)) + x)
+        g.A = t2; g.B = Wt + bk.c3.w_off; g.b_lo = wlo; g.oscale = bk.c3.x3_scale; g.bias = P + bk.c3.b_off;
+        g.R = in; g.r_lo = L; g.K = wd;
+      }
+      MEC_TRY(launch_gemm(g, s, &prof, TAG_RESNET_CONV1X1));
+      std::swap(cur, other);
+      Hc = OH;
+    }
+    return 0;
+  };
+  // Layers 1-2 over chunks of opt().resnet_chunk images (0 = the whole batch), so that a chunk's hi /
+  // lo activations can stay in the 256-MB Infinity Cache between a block's producer and consumer
+  // kernels. Every GEMM row and conv pixel is computed the same way at any batch split (every
+  // interleaved split tile sums in one k order), so the outputs do not depend on the chunk size.
+  constexpr size_t kL12 = 7;  // layer1 (3 blocks) + layer2 (4 blocks)
   f16* cur = X;
   f16* other = Y;
-  int Hc = 56;
-  for (const Bottleneck& bk : blocks) {
-    const int wd = bk.c1.cout, cin = bk.c1.cin, st = bk.c2.stride;
-    const int OH = (Hc + 2 - 3) / st + 1;
-    g = GemmParams();
-    g.split = 1; g.A = cur; g.a_lo = L; g.B = Wt + bk.c1.w_off; g.b_lo = wlo; g.oscale = bk.c1.x3_scale;
-    g.bias = P + bk.c1.b_off; g.act = ACT_RELU; g.C16 = T1; g.c_lo = L;
-    g.M = B * Hc * Hc; g.N = wd; g.K = cin;
-    MEC_TRY(launch_gemm(g, s, &prof, TAG_RESNET_CONV1X1));
-    g = GemmParams();
-    g.split = 1; g.amode = A_CONV; g.A = T1; g.a_lo = L; g.B = Wt + bk.c2.w_off; g.b_lo = wlo;
-    g.oscale = bk.c2.x3_scale; g.bias = P + bk.c2.b_off; g.act = ACT_RELU; g.C16 = T2; g.c_lo = L;
-    g.M = B * OH * OH; g.N = wd; g.K = 9 * wd;
-    g.H = Hc; g.W = Hc; g.C = wd; g.OH = OH; g.OW = OH; g.ks = 3; g.stride = st; g.pad = 1;
-    MEC_TRY(launch_gemm(g, s, &prof, TAG_RESNET_CONV3X3));
-    g = GemmParams();
-    g.split = 1; g.a_lo = L; g.act = ACT_RELU; g.C16 = other; g.c_lo = L; g.M = B * OH * OH; g.N = 4 * wd;
-    if (bk.has_ds) {  // relu(bn3(conv3(t2)) + bn_ds(conv_ds/s(x))) as one GEMM over K = [w | cin]
-      g.amode = A_DUAL; g.A = T2; g.K1 = wd; g.A2 = cur; g.B = Wd + bk.c3ds_w_off; g.b_lo = (long long)bk.c3ds_x3_lo;
-      g.oscale = bk.c3ds_x3_scale; g.bias = P + bk.c3ds_b_off; g.K = wd + cin;
-      g.H = Hc; g.W = Hc; g.C = cin; g.OH = OH; g.OW = OH; g.ks = 1; g.stride = st; g.pad = 0;
-    } else {  // relu(bn3(conv3(t2)) + x)
-      g.A = T2; g.B = Wt + bk.c3.w_off; g.b_lo = wlo; g.oscale = bk.c3.x3_scale; g.bias = P + bk.c3.b_off;
-      g.R = cur; g.r_lo = L; g.K = wd;
-    }
-    MEC_TRY(launch_gemm(g, s, &prof, TAG_RESNET_CONV1X1));
-    std::swap(cur, other);
-    Hc = OH;
+  const int chunk = opt().resnet_chunk > 0 ? std::min(opt().resnet_chunk, B) : B;
+  for (int i0 = 0; i0 < B; i0 += chunk) {
+    f16* c = X;
+    f16* o = Y;
+    MEC_TRY(run_blocks(0, kL12, i0, std::min(chunk, B - i0), 56, c, o));
+    cur = c;
+    other = o;
   }
+  MEC_TRY(run_blocks(kL12, blocks.size(), 0, B, 28, cur, other));
+  const int Hc = 7;
   hipLaunchKernelGGL(avgpool_split_kernel, dim3(B, 2048 / 256), dim3(256), 0, s, cur, L, Hc * Hc, 2048, pooled);
   MEC_LAUNCH_CHECK();
   MEC_TRY(launch_linear_mfma<BACT_RELU>(pooled, 2048, B, 2048, P + fc1_off, P + fc1b_off, 512, feat, 512, nullptr, 0, s));

@@ -478,3 +478,18 @@ def test_mobilenet_v2_fp32x3_batch_invariance_and_entry_shapes(dev):
     _, _, rp = o_mb.forward_resized(syn.weights('image_mbv2'), g224)
     assert np.abs(probs - rp).max() <= PROB_TOL
     enc.check()
+
+
+def test_resnet_fp32x3_chunked_layers_bit_identical(dev):
+    """resnet_chunk n (layers 1-2 over chunks of n images, the rest over the batch) gives the
+    unchunked forward's bits: every split GEMM / conv row is computed the same way at any M."""
+    g = engine.to_device(syn.image_inputs(40, seed=44), dev)
+    outs = []
+    for chunk in (0, 16):
+        enc = engine.ImageEncoder(device=dev, precision='fp32x3')
+        enc.set_option('resnet_chunk', chunk)
+        outs.append(_np(enc.forward(g)))
+        enc.check()
+        enc.close()
+    for k, (a, b) in enumerate(zip(*outs)):
+        assert np.array_equal(a, b), f'output {k}'
