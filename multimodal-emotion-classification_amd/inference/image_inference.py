@@ -61,7 +61,9 @@ class ImageInference:
     def _forward(self, arr: np.ndarray):
         x = engine.to_device(np.asarray(arr, np.uint8)[None], self.device)
         feat, logits, probs = self.model.forward_u8(x)
-        return feat.cpu().numpy()[0], probs.cpu().numpy()[0]
+        feat, probs = feat.cpu().numpy()[0], probs.cpu().numpy()[0]  # synchronizes the stream
+        self.model.check()  # fp32x3: an activation outside the f16 range raises MecError, not NaN probs
+        return feat, probs
 
     @staticmethod
     def _as_dict(emotions, probs: np.ndarray) -> Dict:

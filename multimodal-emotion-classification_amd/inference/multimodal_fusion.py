@@ -129,3 +129,12 @@ class MultimodalFusion:
         imf, il, ip = self.image_inference.model.forward(gray)
         fl, fp, aw, dw = self.fusion_model.forward(sf, tf, imf, sp, tp, ip)
         return {'speech': (sf, sl, sp), 'text': (tf, tl, tp), 'image': (imf, il, ip), 'fusion': (fl, fp, aw, dw)}
+
+    def check(self):
+        """After predict_batch: synchronize the device and raise MecError if a kernel flagged an
+        after-the-fact error (the speech DNN's expired wait; an fp32x3 activation outside the f16 range)."""
+        torch.cuda.synchronize(self.device)
+        for obj in (self.speech_inference.model, self.text_inference.model, self.image_inference.model,
+                    self.fusion_model):
+            if obj is not None:
+                obj.check()

@@ -105,7 +105,9 @@ class TextInference:
             # the reference's nn.Embedding raises IndexError for such ids
             raise ValueError(f'token id out of range [0, {engine.TextEncoder.VOCAB})')
         cls, logits, probs = self.model.forward(engine.to_device(ids, self.device), engine.to_device(mask, self.device))
-        return cls.cpu().numpy()[0], probs.cpu().numpy()[0]
+        cls, probs = cls.cpu().numpy()[0], probs.cpu().numpy()[0]  # synchronizes the stream
+        self.model.check()  # fp32x3: an activation outside the f16 range raises MecError, not NaN probs
+        return cls, probs
 
     @staticmethod
     def _as_dict(emotions, probs: np.ndarray) -> Dict:
@@ -149,7 +151,9 @@ class TextInference:
             return []
         ids, mask = self.encode_batch(texts)
         _, _, probs = self.model.forward(engine.to_device(ids, self.device), engine.to_device(mask, self.device))
-        return [self._as_dict(self.emotions, p) for p in probs.cpu().numpy()]
+        probs = probs.cpu().numpy()
+        self.model.check()
+        return [self._as_dict(self.emotions, p) for p in probs]
 
     def predict_batch(self, ids, mask):
         """ids/mask: device int32 [B,128] -> (cls [B,768], logits [B,7], probs [B,7])."""
