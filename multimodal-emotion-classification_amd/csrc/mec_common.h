@@ -102,6 +102,8 @@ struct Options {
   // computes the [CLS] query with the full kernel's instruction sequence). 0 = the full layer
   int bert_cls_last = 1;
   int mbv2_impl = 0;
+  // fp32x3 MobileNetV2, stride-2 blocks at 56 / 28 outputs: 4 = 4x4 output tiles, 0 = 8x8 / 7x7
+  int mbv2_x3_tile = 0;
   // ping-pong GEMM tile order inside each XCD's contiguous tile range: 0 = row-major (all N
   // panels of one M panel in turn), G = groups of G M panels walked M-fastest, so the 32
   // tiles an XCD runs at once share G A panels and 32/G weight panels

@@ -369,7 +369,9 @@ int launch_x3_block(const MbX3Args& a, int B, hipStream_t s) {
 // The 17 block shapes of mobilenet_v2 at 224x224 (as mobilenet.hip dispatch_block)
 int dispatch_x3_block(const MbBlock& b, const MbX3Args& a, int B, int stem_c, hipStream_t s) {
   const bool res = b.stride == 1 && b.cin == b.cout;
-  const int TO = (a.OH % 8 == 0) ? 8 : 7;
+  // stride-2 blocks at 56 / 28 outputs: 4x4 output tiles (9x9 inputs, 40 KB of LDS, four workgroups
+  // per CU) when opt().mbv2_x3_tile == 4, else 8x8 / 7x7 tiles (17x17 / 15x15 inputs, one per CU)
+  const int TO = (opt().mbv2_x3_tile == 4 && b.stride == 2 && a.OH % 4 == 0) ? 4 : (a.OH % 8 == 0) ? 8 : 7;
 #define MX_CASE(S_, TO_, CI_, HI_, CO_, RS_)                                                                      \
   if (b.stride == S_ && TO == TO_ && b.cinp == CI_ && b.hidp == HI_ && b.coutp == CO_ && b.t != 1 && res == RS_) \
     return launch_x3_block<S_, TO_, CI_, HI_, CO_, true, RS_, 0>(a, B, s);
@@ -379,6 +381,8 @@ int dispatch_x3_block(const MbBlock& b, const MbX3Args& a, int B, int stem_c, hi
     if (stem_c == 3) return launch_x3_block<1, 8, 32, 32, 16, false, false, 3>(a, B, s);
     return launch_x3_block<1, 8, 32, 32, 16, false, false, 1>(a, B, s);
   }
+  MX_CASE(2, 4, 32, 96, 32, false)     // 16 -> 24, 112 -> 56 (4x4 tiles)
+  MX_CASE(2, 4, 32, 160, 32, false)    // 24 -> 32, 56 -> 28 (4x4 tiles)
   MX_CASE(2, 8, 32, 96, 32, false)     // 16 -> 24, 112 -> 56
   MX_CASE(1, 8, 32, 160, 32, true)     // 24 -> 24 @ 56
   MX_CASE(2, 7, 32, 160, 32, false)    // 24 -> 32, 56 -> 28

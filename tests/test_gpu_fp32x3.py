@@ -493,3 +493,17 @@ def test_resnet_fp32x3_chunked_layers_bit_identical(dev):
         enc.close()
     for k, (a, b) in enumerate(zip(*outs)):
         assert np.array_equal(a, b), f'output {k}'
+
+
+def test_mobilenet_v2_fp32x3_tile_forms_bit_identical(dev):
+    """mbv2_x3_tile 4 (4x4 output tiles for the stride-2 blocks at 56 / 28 outputs) computes every
+    output pixel with the same arithmetic as the 8x8 / 7x7 tiles: the same bits."""
+    g = engine.to_device(syn.image_inputs(6, seed=46), dev)
+    outs = []
+    for t in (0, 4):
+        enc = engine.MobileNetImageEncoder(device=dev, precision='fp32x3')
+        enc.set_option('mbv2_x3_tile', t)
+        outs.append(_np(enc.forward(g)))
+        enc.close()
+    for k, (a, b) in enumerate(zip(*outs)):
+        assert np.array_equal(a, b), f'output {k}'

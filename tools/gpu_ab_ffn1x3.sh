@@ -16,3 +16,6 @@ tail -4 gpurun_out/r04_ab_chunk_x3_image.txt
 timeout -k 10 400 python3 -u tools/ab_option.py --enc pipeline --opt resnet_chunk --values 0 32 64 \
   --precision fp32x3 > gpurun_out/r04_ab_chunk_x3_pipeline.txt 2>&1 || exit 1
 tail -3 gpurun_out/r04_ab_chunk_x3_pipeline.txt
+timeout -k 10 300 python3 -u tools/ab_option.py --enc image_mbv2 --opt mbv2_x3_tile --values 0 4 \
+  --precision fp32x3 > gpurun_out/r04_ab_mbv2x3_tile.txt 2>&1 || exit 1
+tail -2 gpurun_out/r04_ab_mbv2x3_tile.txt
