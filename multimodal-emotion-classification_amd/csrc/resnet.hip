@@ -519,6 +519,9 @@ int ImageModel::forward_u8(const uint8_t* img, int B, int H, int W, int C, float
   p += ((size_t)B * 224 * 224 + 255) / 256 * 256;
   f16* X = reinterpret_cast<f16*>(p); p += (size_t)B * per_img_big * sizeof(f16);
   f16* Y = reinterpret_cast<f16*>(p); p += (size_t)B * per_img_big * sizeof(f16);
+  // the stem output [B,56,56,64] sits in the last quarter of X: a chunk's layer-1 outputs (4x the
+  // per-image stride) then never reach the stem output of a later chunk's images (resnet_chunk)
+  f16* Xs = X + (size_t)3 * B * 56 * 56 * 64;
   f16* T1 = reinterpret_cast<f16*>(p); p += (size_t)B * per_t1 * sizeof(f16);
   f16* T2 = reinterpret_cast<f16*>(p);
   p += (size_t)B * per_t2 * sizeof(f16);
@@ -545,19 +548,19 @@ int ImageModel::forward_u8(const uint8_t* img, int B, int H, int W, int C, float
     const f16* sw = Wt + st.w_off;
     const float *sbias = P + st.b_off, *scorr = P + stem_corr_off;
     if (C == 3)
-      hipLaunchKernelGGL(stem_pool_kernel<3>, sg, sb, 0, s, stem_in, ntiles, sw, sbias, scorr, X);
+      hipLaunchKernelGGL(stem_pool_kernel<3>, sg, sb, 0, s, stem_in, ntiles, sw, sbias, scorr, Xs);
 #ifdef MEC_PROBES
     else if (opt().stem_debug == 1)  // probe builds (wrong results): no MFMA / no pool / no prefetch
-      hipLaunchKernelGGL((stem_pool_kernel<1, 1>), sg, sb, 0, s, stem_in, ntiles, sw, sbias, scorr, X);
+      hipLaunchKernelGGL((stem_pool_kernel<1, 1>), sg, sb, 0, s, stem_in, ntiles, sw, sbias, scorr, Xs);
     else if (opt().stem_debug == 2)
-      hipLaunchKernelGGL((stem_pool_kernel<1, 2>), sg, sb, 0, s, stem_in, ntiles, sw, sbias, scorr, X);
+      hipLaunchKernelGGL((stem_pool_kernel<1, 2>), sg, sb, 0, s, stem_in, ntiles, sw, sbias, scorr, Xs);
     else if (opt().stem_debug == 4)
-      hipLaunchKernelGGL((stem_pool_kernel<1, 4>), sg, sb, 0, s, stem_in, ntiles, sw, sbias, scorr, X);
+      hipLaunchKernelGGL((stem_pool_kernel<1, 4>), sg, sb, 0, s, stem_in, ntiles, sw, sbias, scorr, Xs);
     else if (opt().stem_debug == 7)
-      hipLaunchKernelGGL((stem_pool_kernel<1, 7>), sg, sb, 0, s, stem_in, ntiles, sw, sbias, scorr, X);
+      hipLaunchKernelGGL((stem_pool_kernel<1, 7>), sg, sb, 0, s, stem_in, ntiles, sw, sbias, scorr, Xs);
 #endif
     else
-      hipLaunchKernelGGL(stem_pool_kernel<1>, sg, sb, 0, s, stem_in, ntiles, sw, sbias, scorr, X);
+      hipLaunchKernelGGL(stem_pool_kernel<1>, sg, sb, 0, s, stem_in, ntiles, sw, sbias, scorr, Xs);
     MEC_LAUNCH_CHECK();
     MEC_TRY(prof.end(TAG_RESNET_STEM, s));
   }
@@ -570,7 +573,7 @@ int ImageModel::forward_u8(const uint8_t* img, int B, int H, int W, int C, float
       const Bottleneck& bk = blocks[bi];
       const int wd = bk.c1.cout, cin = bk.c1.cin, st = bk.c2.stride;
       const int OH = (H + 2 - 3) / st + 1;
-      f16* in = cur + (size_t)i0 * H * H * cin;
+      f16* in = (bi == 0 ? Xs : cur) + (size_t)i0 * H * H * cin;
       f16* out = other + (size_t)i0 * OH * OH * 4 * wd;
       f16* t1 = T1 + (size_t)i0 * H * H * wd;
       f16* t2 = T2 + (size_t)i0 * OH * OH * wd;

@@ -665,6 +665,9 @@ int ImageModel::forward_x3(const uint8_t* img, int B, int H, int W, int C, float
   const long long L = (long long)B * arena_img;  // lo plane = hi plane + L, for every activation
   f16* X = arena;
   f16* Y = X + (size_t)B * big;
+  // the stem output [B,56,56,64] sits in the last quarter of X: a chunk's layer-1 outputs (4x the
+  // per-image stride) then never reach the stem output of a later chunk's images (resnet_chunk)
+  f16* Xs = X + (size_t)3 * B * 56 * 56 * 64;
   f16* T1 = Y + (size_t)B * big;
   f16* T2 = T1 + (size_t)B * t1n;
 
@@ -691,7 +694,7 @@ int ImageModel::forward_x3(const uint8_t* img, int B, int H, int W, int C, float
     }
     const int ntiles = B * 49;
     hipLaunchKernelGGL(stem_pool_gray_x3_kernel, dim3(std::min(ntiles, ncu)), dim3(512), 0, s, stem_in, ntiles,
-                       Wt32 + stem_gray32_off, stem_x3_up, stem.x3_scale, P + stem.b_off, X, L,
+                       Wt32 + stem_gray32_off, stem_x3_up, stem.x3_scale, P + stem.b_off, Xs, L,
                        range_flag());
     MEC_LAUNCH_CHECK();
   } else {
@@ -708,7 +711,7 @@ int ImageModel::forward_x3(const uint8_t* img, int B, int H, int W, int C, float
     hipLaunchKernelGGL(maxpool_f32_kernel, dim3((unsigned)((tp + 255) / 256)), dim3(256), 0, s, Y32, B, 112, 64, 56, S32);
     MEC_LAUNCH_CHECK();
     const size_t n4 = (size_t)B * 56 * 56 * 64 / 4;
-    hipLaunchKernelGGL(split_f32_kernel, dim3((unsigned)((n4 + 255) / 256)), dim3(256), 0, s, S32, n4, X, L, range_flag());
+    hipLaunchKernelGGL(split_f32_kernel, dim3((unsigned)((n4 + 255) / 256)), dim3(256), 0, s, S32, n4, Xs, L, range_flag());
     MEC_LAUNCH_CHECK();
   }
   MEC_TRY(prof.end(TAG_RESNET_STEM, s));
@@ -720,7 +723,7 @@ int ImageModel::forward_x3(const uint8_t* img, int B, int H, int W, int C, float
       const Bottleneck& bk = blocks[bi];
       const int wd = bk.c1.cout, cin = bk.c1.cin, st = bk.c2.stride;
       const int OH = (Hc + 2 - 3) / st + 1;
-      f16* in = cur + (size_t)i0 * Hc * Hc * cin;
+      f16* in = (bi == 0 ? Xs : cur) + (size_t)i0 * Hc * Hc * cin;
       f16* out = other + (size_t)i0 * OH * OH * 4 * wd;
       f16* t1 = T1 + (size_t)i0 * Hc * Hc * wd;
       f16* t2 = T2 + (size_t)i0 * OH * OH * wd;
