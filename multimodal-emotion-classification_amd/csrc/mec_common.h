@@ -102,11 +102,10 @@ struct Options {
   // computes the [CLS] query with the full kernel's instruction sequence). 0 = the full layer
   int bert_cls_last = 1;
   int mbv2_impl = 0;
-  // MobileNetV2 f16 path: features[8..17] (the 14x14 and 7x7 stages) as one kernel per image with the
-  // activation map resident in LDS (mobilenet_tail.hip); bit-identical to the per-block kernels
-  int mbv2_tail = 0;
-  // fp32x3 MobileNetV2, stride-2 blocks at 56 / 28 outputs: 4 = 4x4 output tiles, 0 = 8x8 / 7x7
-  int mbv2_x3_tile = 0;
+  // fp32x3 MobileNetV2, stride-2 blocks at 56 / 28 outputs: 4 = 4x4 output tiles (9x9 inputs, four
+  // workgroups per CU), 0 = 8x8 / 7x7 (17x17 / 15x15 inputs, one per CU); same bits. 4: 2.99 -> 2.92 ms
+  // at B = 256 (profiles/r04_ab_mbv2x3_tile.txt)
+  int mbv2_x3_tile = 4;
   // ping-pong GEMM tile order inside each XCD's contiguous tile range: 0 = row-major (all N
   // panels of one M panel in turn), G = groups of G M panels walked M-fastest, so the 32
   // tiles an XCD runs at once share G A panels and 32/G weight panels

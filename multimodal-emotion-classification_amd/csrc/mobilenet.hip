@@ -761,7 +761,7 @@ int MobileNetModel::create(const float* blob, size_t n) {
   pr.insert(pr.end(), f2b, f2b + 7);
   MEC_TRY(upload(wts, w.data(), w.size() * sizeof(f16)));
   MEC_TRY(upload(prm, pr.data(), pr.size() * sizeof(float)));
-  return build_mbv2_tail_table(*this);
+  return 0;
 }
 
 // mec_set_option("mbv2_impl"): 1 = workgroup tiles, 2 = wave-autonomous tiles, 0 = per block
@@ -895,12 +895,6 @@ int MobileNetModel::forward_u8(const uint8_t* img, int B, int H, int W, int C, f
   f16* out = X;
   int h = 112;
   for (size_t i = 0; i < blocks.size(); ++i) {
-    if (i == 7 && opt().mbv2_tail) {  // features[8..17] as one kernel per image (mobilenet_tail.hip)
-      MEC_TRY(launch_mbv2_tail(*this, cur, out, B, s));
-      cur = out;
-      h = 7;
-      break;
-    }
     const MbBlock& b = blocks[i];
     MbArgs a;
     a.x = cur; a.y = out; a.H = h; a.OH = b.stride == 2 ? h / 2 : h;

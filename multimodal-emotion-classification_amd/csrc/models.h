@@ -201,7 +201,6 @@ struct MobileNetModel : ImageNet {
   size_t last_w_off = 0, last_b_off = 0;  // features[18]: f16 [1280][320], f32 [1280]
   size_t fc1_off = 0, fc1b_off = 0, fc2_off = 0, fc2b_off = 0;
   DevBuf wts32;  // fp32 path (mobilenet_f32.hip): f32 weights, channels padded to 64
-  DevBuf tail_tab;  // f16 path: features[8..17]'s block table for mbv2_tail_kernel (mobilenet_tail.hip)
   int create(const float* blob, size_t n);
   int create_f32(const float* blob, size_t n);
   int forward_u8(const uint8_t* img, int B, int H, int W, int C, float* feat, float* logits, float* probs,
@@ -216,11 +215,6 @@ struct MobileNetModel : ImageNet {
   int forward_x3(const uint8_t* img, int B, int H, int W, int C, float* feat, float* logits, float* probs,
                  hipStream_t s);
 };
-
-// MobileNetV2 features[8..17] as one kernel per image (mobilenet_tail.hip): x = features[7]'s output
-// f16 [B,14,14,64] -> y = features[17]'s output f16 [B,7,7,320]; bit-identical to the per-block kernels
-int launch_mbv2_tail(const MobileNetModel& m, const f16* x, f16* y, int B, hipStream_t s);
-int build_mbv2_tail_table(MobileNetModel& m);
 
 int resize_u8(const uint8_t* in, int B, int H, int W, uint8_t* out, int OH, int OW, hipStream_t s);
 // layer1 seam: conv3 (64 -> 256) + residual + ReLU, then the next block's conv1 (256 -> N2)

@@ -93,18 +93,3 @@ def test_mbv2_wave_and_workgroup_forms_bit_identical(mb, dev, C):
     for a, b in zip(*outs):
         np.testing.assert_array_equal(a, b)
 
-
-@pytest.mark.parametrize('B', [5, 64])
-def test_mbv2_tail_bit_identical(dev, B):
-    """mbv2_tail 1 (features[8..17] as one kernel per image, csrc/mobilenet_tail.hip) against the
-    per-block kernels: the same sums in the same order and the same f16 roundings, so feature,
-    logits and probs are equal bit for bit."""
-    g = engine.to_device(syn.image_inputs(B, seed=60 + B), dev)
-    outs = []
-    for tail in (0, 1):
-        enc = engine.MobileNetImageEncoder(device=dev)
-        enc.set_option('mbv2_tail', tail)
-        outs.append(_np(enc.forward(g)))
-        enc.close()
-    for k, (a, b) in enumerate(zip(*outs)):
-        assert np.array_equal(a, b), f'output {k}: max |d| {np.abs(a - b).max()}'
