@@ -94,6 +94,9 @@ struct Options {
   int resnet_chunk = 0;
   int pw_chain = 2;         // layer1 seam kernels (pw_chain.hip)
   int pw_chain_form = 0;
+  // fp32x3 layer1 seam kernels (pw_chain_x3.hip): 0 off, 1 the 256 -> 64 seams (block 1 -> 2 with
+  // the downsample, 2 -> 3), 2 also the 256 -> 128 seam into layer2
+  int pw_chain_x3 = 2;
   int bert_qkv_attn = 1;    // fused BERT QKV projection + attention
   int bert_ln_rows = 2;     // BERT LayerNorm rows per wave (1 | 2 | 4): 27.0 / 25.7 / 26.3 us at B = 256
   // BERT's last layer on the [CLS] rows only (the outputs -- pooler, logits, CLS feature -- read

@@ -223,6 +223,12 @@ int launch_pw_chain(const f16* t2, const f16* xin, const f16* w3, const float* b
 // layer1 block 1 -> 2 seam: conv3 + downsample (K = [T2 | X0]) + ReLU, then block 2's conv1
 int launch_pw_chain_dual(const f16* t2, const f16* x0, const f16* w3ds, const float* b3ds, const f16* w1,
                          const float* b1, f16* xout, f16* t1, int M, hipStream_t s);
+// fp32x3 layer1 seam (pw_chain_x3.hip): the same two products on hi / lo planes (lo planes L
+// elements after their hi planes; weight lo planes at w*_lo, pre-scales undone by os*); dual =
+// conv3 + downsample over K = [T2 | X0] (xin = X0), else conv3 + identity residual (xin)
+int launch_pw_chain_x3(const f16* t2, const f16* xin, long long L, const f16* w3, long long w3_lo, float os3,
+                       const float* b3, const f16* w1, long long w1_lo, float os1, const float* b1, f16* xout, f16* t1,
+                       int M, int N2, bool dual, hipStream_t s);
 
 
 }  // namespace mec

@@ -719,6 +719,7 @@ int ImageModel::forward_x3(const uint8_t* img, int B, int H, int W, int C, float
   // is a pointer offset; the lo planes stay L elements after their hi planes). cur/other swap per block.
   auto run_blocks = [&](size_t b0, size_t b1, int i0, int nb, int Hin, f16*& cur, f16*& other) -> int {
     int Hc = Hin;
+    bool conv1_done = false;  // this block's conv1 already ran in the previous block's seam kernel
     for (size_t bi = b0; bi < b1; ++bi) {
       const Bottleneck& bk = blocks[bi];
       const int wd = bk.c1.cout, cin = bk.c1.cin, st = bk.c2.stride;
@@ -728,16 +729,42 @@ int ImageModel::forward_x3(const uint8_t* img, int B, int H, int W, int C, float
       f16* t1 = T1 + (size_t)i0 * Hc * Hc * wd;
       f16* t2 = T2 + (size_t)i0 * OH * OH * wd;
       GemmParams g;
-      g.split = 1; g.A = in; g.a_lo = L; g.B = Wt + bk.c1.w_off; g.b_lo = wlo; g.oscale = bk.c1.x3_scale;
-      g.bias = P + bk.c1.b_off; g.act = ACT_RELU; g.C16 = t1; g.c_lo = L;
-      g.M = nb * Hc * Hc; g.N = wd; g.K = cin;
-      MEC_TRY(launch_gemm(g, s, &prof, TAG_RESNET_CONV1X1));
+      if (!conv1_done) {
+        g.split = 1; g.A = in; g.a_lo = L; g.B = Wt + bk.c1.w_off; g.b_lo = wlo; g.oscale = bk.c1.x3_scale;
+        g.bias = P + bk.c1.b_off; g.act = ACT_RELU; g.C16 = t1; g.c_lo = L;
+        g.M = nb * Hc * Hc; g.N = wd; g.K = cin;
+        MEC_TRY(launch_gemm(g, s, &prof, TAG_RESNET_CONV1X1));
+      }
+      conv1_done = false;
       g = GemmParams();
       g.split = 1; g.amode = A_CONV; g.A = t1; g.a_lo = L; g.B = Wt + bk.c2.w_off; g.b_lo = wlo;
       g.oscale = bk.c2.x3_scale; g.bias = P + bk.c2.b_off; g.act = ACT_RELU; g.C16 = t2; g.c_lo = L;
       g.M = nb * OH * OH; g.N = wd; g.K = 9 * wd;
       g.H = Hc; g.W = Hc; g.C = wd; g.OH = OH; g.OW = OH; g.ks = 3; g.stride = st; g.pad = 1;
       MEC_TRY(launch_gemm(g, s, &prof, TAG_RESNET_CONV3X3));
+      // layer1 seams (pw_chain_x3.hip): conv3 (+ downsample or + residual) + ReLU, then the next
+      // block's conv1 on the rows just produced; the block output's planes are not read back
+      const int sx = opt().pw_chain_x3;
+      const Bottleneck* nx = bi + 1 < b1 ? &blocks[bi + 1] : nullptr;
+      const bool seam = sx && nx && wd == 64 && OH == 56 && nx->c1.cin == 256 &&
+                        (nx->c1.cout == 64 || (sx == 2 && nx->c1.cout == 128)) &&
+                        (!bk.has_ds || (st == 1 && cin == 64 && nx->c1.cout == 64));
+      if (seam) {
+        MEC_TRY(prof.begin(TAG_RESNET_CONV1X1, s));
+        if (bk.has_ds)
+          MEC_TRY(launch_pw_chain_x3(t2, in, L, Wd + bk.c3ds_w_off, (long long)bk.c3ds_x3_lo, bk.c3ds_x3_scale,
+                                     P + bk.c3ds_b_off, Wt + nx->c1.w_off, wlo, nx->c1.x3_scale, P + nx->c1.b_off, out,
+                                     T1 + (size_t)i0 * OH * OH * nx->c1.cout, nb * OH * OH, nx->c1.cout, true, s));
+        else
+          MEC_TRY(launch_pw_chain_x3(t2, in, L, Wt + bk.c3.w_off, wlo, bk.c3.x3_scale, P + bk.c3.b_off,
+                                     Wt + nx->c1.w_off, wlo, nx->c1.x3_scale, P + nx->c1.b_off, out,
+                                     T1 + (size_t)i0 * OH * OH * nx->c1.cout, nb * OH * OH, nx->c1.cout, false, s));
+        MEC_TRY(prof.end(TAG_RESNET_CONV1X1, s));
+        conv1_done = true;
+        std::swap(cur, other);
+        Hc = OH;
+        continue;
+      }
       g = GemmParams();
       g.split = 1; g.a_lo = L; g.act = ACT_RELU; g.C16 = out; g.c_lo = L; g.M = nb * OH * OH; g.N = 4 * wd;
       if (bk.has_ds) {  // relu(bn3(conv3(t2)) + bn_ds(conv_ds/s(x))) as one GEMM over K = [w | cin]

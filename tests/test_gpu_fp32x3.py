@@ -495,6 +495,26 @@ def test_resnet_fp32x3_chunked_layers_bit_identical(dev):
         assert np.array_equal(a, b), f'output {k}'
 
 
+@pytest.mark.parametrize('B,chunk', [(3, 0), (40, 0), (40, 16)])
+def test_resnet_fp32x3_seams_bit_identical(dev, B, chunk):
+    """pw_chain_x3 1 / 2 (layer1's conv3 + downsample-or-residual + ReLU and the next block's conv1
+    in one kernel, csrc/pw_chain_x3.hip) against 0 (the two split GEMMs): the same K-interleaved
+    terms in the same k order and the same epilogue, so every output is equal bit for bit, also
+    over image chunks (resnet_chunk)."""
+    g = engine.to_device(syn.image_inputs(B, seed=47 + B), dev)
+    outs = []
+    for seam in (0, 1, 2):
+        enc = engine.ImageEncoder(device=dev, precision='fp32x3')
+        enc.set_option('pw_chain_x3', seam)
+        enc.set_option('resnet_chunk', chunk)
+        outs.append(_np(enc.forward(g)))
+        enc.check()
+        enc.close()
+    for seam, o in zip((1, 2), outs[1:]):
+        for k, (a, b) in enumerate(zip(outs[0], o)):
+            assert np.array_equal(a, b), f'pw_chain_x3 {seam}, output {k}: max |d| {np.abs(a - b).max()}'
+
+
 def test_mobilenet_v2_fp32x3_tile_forms_bit_identical(dev):
     """mbv2_x3_tile 4 (4x4 output tiles for the stride-2 blocks at 56 / 28 outputs) computes every
     output pixel with the same arithmetic as the 8x8 / 7x7 tiles: the same bits."""
