@@ -109,6 +109,9 @@ struct Options {
   // workgroups per CU), 0 = 8x8 / 7x7 (17x17 / 15x15 inputs, one per CU); same bits. 4: 2.99 -> 2.92 ms
   // at B = 256 (profiles/r04_ab_mbv2x3_tile.txt)
   int mbv2_x3_tile = 4;
+  // fp32x3 MobileNetV2: features[k..17] as expand GEMM -> depthwise kernel -> project GEMM on hi / lo
+  // planes (the "layered" form; k = 7..17, 0 = every block fused)
+  int mbv2_layered = 8;
   // ping-pong GEMM tile order inside each XCD's contiguous tile range: 0 = row-major (all N
   // panels of one M panel in turn), G = groups of G M panels walked M-fastest, so the 32
   // tiles an XCD runs at once share G A panels and 32/G weight panels

@@ -357,6 +357,126 @@ __global__ __launch_bounds__(256) void mbv2_split_kernel(const float* __restrict
   x3_raise(flag, x3_out_of_range4(v));
 }
 
+// f32 [rows][cin] -> f16 hi / lo planes [rows][ld] (lo at + lo), channels cin .. ld-1 zero: the first
+// layered block's input
+__global__ __launch_bounds__(256) void mbv2_split_pad_kernel(const float* __restrict__ x, size_t rows, int cin, int ld,
+                                                             f16* __restrict__ hi, long long lo, unsigned* flag) {
+  const size_t i = (size_t)blockIdx.x * 256 + threadIdx.x;  // one 4-channel group of one row
+  const int G = ld / 4;
+  if (i >= rows * G) return;
+  const size_t r = i / G;
+  const int c = (int)(i - r * G) * 4;
+  const float4 v = c < cin ? *reinterpret_cast<const float4*>(x + r * cin + c) : make_float4(0.f, 0.f, 0.f, 0.f);
+  const half4 h = {(f16)v.x, (f16)v.y, (f16)v.z, (f16)v.w};
+  const half4 l = {(f16)(v.x - (float)h[0]), (f16)(v.y - (float)h[1]), (f16)(v.z - (float)h[2]),
+                   (f16)(v.w - (float)h[3])};
+  *reinterpret_cast<half4*>(hi + r * ld + c) = h;
+  *reinterpret_cast<half4*>(hi + lo + r * ld + c) = l;
+  x3_raise(flag, x3_out_of_range4(v));
+}
+
+// Depthwise 3x3/S (pad 1) + BN shift + ReLU6 of a layered block: E f32 NHWC [B,H,H,C] (the expand GEMM's
+// ReLU6 output) -> D hi / lo planes NHWC [B,OH,OH,C] (lo at D + dlo), the project GEMM's A operand. A
+// thread owns one output row of one 8-channel group: its 72 tap weights and a 3-row x 3-column window
+// of input pixels stay in registers while it walks the row, so each input pixel is loaded about 3 / S
+// times instead of 9 (consecutive threads take consecutive channel groups: every load is part of a
+// contiguous run). Per output: fp32 FMAs in torch's (kh, kw) tap order from the shift, as the fused
+// kernel's depthwise (whose zero-padded taps add exact zeros).
+template <int S>
+__global__ __launch_bounds__(256) void mbv2_dw_x3_kernel(const float* __restrict__ E, int H, int OH, int C,
+                                                         const float* __restrict__ Wd, const float* __restrict__ bd,
+                                                         f16* __restrict__ D, long long dlo, size_t items) {
+  const size_t it = (size_t)blockIdx.x * 256 + threadIdx.x;
+  if (it >= items) return;
+  const int G = C / 8;
+  const size_t row = it / G;  // (image, output row)
+  const int g = (int)(it - row * G);
+  const size_t n = row / OH;
+  const int oy = (int)(row - n * OH);
+  float w[9][8], bias[8];
+  {
+    const float* wd = Wd + (size_t)g * 72;
+#pragma unroll
+    for (int t = 0; t < 9; ++t) {
+      const float4 w0 = *reinterpret_cast<const float4*>(wd + t * 8);
+      const float4 w1 = *reinterpret_cast<const float4*>(wd + t * 8 + 4);
+      w[t][0] = w0.x; w[t][1] = w0.y; w[t][2] = w0.z; w[t][3] = w0.w;
+      w[t][4] = w1.x; w[t][5] = w1.y; w[t][6] = w1.z; w[t][7] = w1.w;
+    }
+    const float4 b0 = *reinterpret_cast<const float4*>(bd + 8 * g);
+    const float4 b1 = *reinterpret_cast<const float4*>(bd + 8 * g + 4);
+    bias[0] = b0.x; bias[1] = b0.y; bias[2] = b0.z; bias[3] = b0.w;
+    bias[4] = b1.x; bias[5] = b1.y; bias[6] = b1.z; bias[7] = b1.w;
+  }
+  bool rok[3];
+  const float* rp[3];
+#pragma unroll
+  for (int ky = 0; ky < 3; ++ky) {
+    const int iy = oy * S - 1 + ky;
+    rok[ky] = iy >= 0 && iy < H;
+    rp[ky] = E + ((n * H + (rok[ky] ? iy : 0)) * H) * C + 8 * g;
+  }
+  // input column ix of the three rows -> e[ky][0..7] (zeros outside the image: those taps are skipped)
+  auto load_col = [&](int ix, float (&e)[3][8], bool& ok) {
+    ok = ix >= 0 && ix < H;
+#pragma unroll
+    for (int ky = 0; ky < 3; ++ky) {
+      float4 a = make_float4(0.f, 0.f, 0.f, 0.f), c = a;
+      if (ok && rok[ky]) {
+        a = *reinterpret_cast<const float4*>(rp[ky] + (size_t)ix * C);
+        c = *reinterpret_cast<const float4*>(rp[ky] + (size_t)ix * C + 4);
+      }
+      e[ky][0] = a.x; e[ky][1] = a.y; e[ky][2] = a.z; e[ky][3] = a.w;
+      e[ky][4] = c.x; e[ky][5] = c.y; e[ky][6] = c.z; e[ky][7] = c.w;
+    }
+  };
+  float win[3][3][8];  // [kx][ky][channel]: input columns ox S - 1 + kx
+  bool cok[3];
+  load_col(-1, win[0], cok[0]);
+  load_col(0, win[1], cok[1]);
+  f16* dst = D + (row * OH) * C + 8 * g;
+  for (int ox = 0; ox < OH; ++ox) {
+    if (S == 1) {
+      load_col(ox + 1, win[2], cok[2]);
+    } else {
+      load_col(2 * ox, win[1], cok[1]);
+      load_col(2 * ox + 1, win[2], cok[2]);
+    }
+    float d[8];
+#pragma unroll
+    for (int j = 0; j < 8; ++j) d[j] = bias[j];
+#pragma unroll
+    for (int ky = 0; ky < 3; ++ky) {
+      if (!rok[ky]) continue;
+#pragma unroll
+      for (int kx = 0; kx < 3; ++kx) {
+        if (!cok[kx]) continue;
+#pragma unroll
+        for (int j = 0; j < 8; ++j) d[j] = __builtin_fmaf(win[kx][ky][j], w[ky * 3 + kx][j], d[j]);
+      }
+    }
+    half8 oh, ol;
+#pragma unroll
+    for (int j = 0; j < 8; ++j) {
+      const float v = relu6x(d[j]);  // in [0, 6]: inside the f16 range
+      oh[j] = (f16)v;
+      ol[j] = (f16)(v - (float)oh[j]);
+    }
+    *reinterpret_cast<half8*>(dst + (size_t)ox * C) = oh;
+    *reinterpret_cast<half8*>(dst + dlo + (size_t)ox * C) = ol;
+    // slide: the next output's first column(s)
+#pragma unroll
+    for (int ky = 0; ky < 3; ++ky)
+#pragma unroll
+      for (int j = 0; j < 8; ++j) {
+        win[0][ky][j] = S == 1 ? win[1][ky][j] : win[2][ky][j];
+        if (S == 1) win[1][ky][j] = win[2][ky][j];
+      }
+    cok[0] = S == 1 ? cok[1] : cok[2];
+    if (S == 1) cok[1] = cok[2];
+  }
+}
+
 template <int S, int TO, int CINP, int HIDP, int COUTP, bool EXPAND, bool RES, int STEM>
 int launch_x3_block(const MbX3Args& a, int B, hipStream_t s) {
   const int tpr = a.OH / TO;
@@ -463,7 +583,8 @@ int MobileNetModel::create_x3(const float* blob, size_t n) {
                                  {6, 96, 3, 1}, {6, 160, 3, 2}, {6, 320, 1, 1}};
   blocks.clear();
   x3_scale.clear();
-  int cin = 32;
+  lx3_scale.clear();
+  int cin = 32, prev_lcoutp = 32;
   for (int si = 0; si < 7; ++si)
     for (int r = 0; r < kSet[si][2]; ++r) {
       MbBlock b;
@@ -512,6 +633,22 @@ int MobileNetModel::create_x3(const float* blob, size_t n) {
             pr[b.bp_off + o] = (float)sh[o];
           }
       }
+      b.lcinp = prev_lcoutp;
+      b.lcoutp = pad_to(b.cout, 64);
+      prev_lcoutp = b.lcoutp;
+      if (b.t != 1 && b.hidp % 64 == 0) {  // layered form: the same matrices, K / N padded with zeros
+        b.lwe_off = w.size();
+        w.resize(w.size() + (size_t)b.hidp * b.lcinp, 0.f);
+        for (int h = 0; h < b.hidp; ++h)
+          for (int c = 0; c < b.cinp && c < b.lcinp; ++c)
+            w[b.lwe_off + (size_t)h * b.lcinp + c] = w[b.we_off + (size_t)h * b.cinp + c];
+        b.lwp_off = w.size();
+        w.resize(w.size() + (size_t)b.lcoutp * b.hidp, 0.f);
+        std::copy(w.begin() + b.wp_off, w.begin() + b.wp_off + (size_t)b.coutp * b.hidp, w.begin() + b.lwp_off);
+        b.lbp_off = pr.size();
+        pr.resize(pr.size() + b.lcoutp, 0.f);
+        std::copy(pr.begin() + b.bp_off, pr.begin() + b.bp_off + b.coutp, pr.begin() + b.lbp_off);
+      }
       blocks.push_back(b);
       cin = b.cout;
     }
@@ -554,6 +691,8 @@ int MobileNetModel::create_x3(const float* blob, size_t n) {
   for (MbBlock& b : blocks) {
     x3_scale.push_back(b.t != 1 ? split(b.we_off, (size_t)b.hidp * b.cinp) : 1.f);
     x3_scale.push_back(split(b.wp_off, (size_t)b.coutp * b.hidp));
+    lx3_scale.push_back(b.lwe_off ? split(b.lwe_off, (size_t)b.hidp * b.lcinp) : 1.f);
+    lx3_scale.push_back(b.lwe_off ? split(b.lwp_off, (size_t)b.lcoutp * b.hidp) : 1.f);
   }
   x3_scale.push_back(split(last_w_off, (size_t)1280 * 320));
   MEC_TRY(upload(wts, hl.data(), hl.size() * sizeof(f16)));
@@ -563,11 +702,35 @@ int MobileNetModel::create_x3(const float* blob, size_t n) {
 
 int MobileNetModel::forward_x3(const uint8_t* img, int B, int H, int W, int C, float* feat, float* logits,
                                float* probs, hipStream_t s) {
-  MEC_REQUIRE(wts.p && x3_lo && x3_scale.size() == 2 * blocks.size() + 1, "image_mbv2: fp32x3 weights missing");
+  MEC_REQUIRE(wts.p && x3_lo && x3_scale.size() == 2 * blocks.size() + 1 && lx3_scale.size() == 2 * blocks.size(),
+              "image_mbv2: fp32x3 weights missing");
   const bool fer = (H == 48 && W == 48 && C == 1);
+  // layered tail: blocks[l0 ..] (features[l0 + 1 ..]) as expand GEMM -> depthwise -> project GEMM
+  size_t l0 = blocks.size();
+  if (opt().mbv2_layered) {
+    l0 = (size_t)opt().mbv2_layered - 1;
+    for (size_t i = l0; i < blocks.size(); ++i)
+      MEC_REQUIRE(blocks[i].lwe_off, "mbv2 x3: mbv2_layered names a block without a layered form");
+  }
+  // per-image element counts of the layered buffers: E (f32), D / block-I/O planes (halfs per plane)
+  size_t pe = 0, pd = 0, pp = 0;
+  {
+    int hh = 112;
+    for (size_t i = 0; i < blocks.size(); ++i) {
+      const MbBlock& b = blocks[i];
+      const int oh = b.stride == 2 ? hh / 2 : hh;
+      if (i >= l0) {
+        pe = std::max(pe, (size_t)hh * hh * b.hidp);
+        pd = std::max(pd, (size_t)oh * oh * b.hidp);
+        pp = std::max(pp, std::max((size_t)hh * hh * b.lcinp, (size_t)oh * oh * b.lcoutp));
+      }
+      hh = oh;
+    }
+  }
   const size_t per_big = (size_t)112 * 112 * 16;  // largest block output (features[1]), floats
   const size_t per_last = (size_t)49 * 1280, per_in = (size_t)49 * 320;
-  const size_t per_img = 224 * 224 + (2 * per_big + per_last + 1280) * sizeof(float) + per_in * 2 * sizeof(f16);
+  const size_t per_img = 224 * 224 + (2 * per_big + per_last + 1280) * sizeof(float) + per_in * 2 * sizeof(f16) +
+                         pe * sizeof(float) + (pd + 2 * pp) * 2 * sizeof(f16);
   const size_t need = per_img * (size_t)B + 8192;
   if (ws.bytes < need) MEC_TRY(ws.ensure(need));
   char* p = ws.as<char>();
@@ -577,7 +740,12 @@ int MobileNetModel::forward_x3(const uint8_t* img, int B, int H, int W, int C, f
   float* Y = reinterpret_cast<float*>(p); p += (size_t)B * per_big * sizeof(float);
   float* Lst = reinterpret_cast<float*>(p); p += (size_t)B * per_last * sizeof(float);
   float* pooled = reinterpret_cast<float*>(p); p += (size_t)B * 1280 * sizeof(float);
-  f16* Lin = reinterpret_cast<f16*>(p);  // features[18]'s A planes [B*49, 320] (lo at + B*49*320)
+  f16* Lin = reinterpret_cast<f16*>(p); p += (size_t)B * per_in * 2 * sizeof(f16);  // features[18]'s A planes
+  float* Eb = reinterpret_cast<float*>(p); p += (size_t)B * pe * sizeof(float);
+  const long long dlo = (long long)B * pd, plo = (long long)B * pp;  // plane offsets (halfs)
+  f16* Db = reinterpret_cast<f16*>(p); p += (size_t)B * pd * 2 * sizeof(f16);
+  f16* P0 = reinterpret_cast<f16*>(p); p += (size_t)B * pp * 2 * sizeof(f16);
+  f16* P1 = reinterpret_cast<f16*>(p);
 
   const f16* Wt = wts.as<f16>();
   const long long wlo = (long long)x3_lo;
@@ -591,8 +759,44 @@ int MobileNetModel::forward_x3(const uint8_t* img, int B, int H, int W, int C, f
   const void* cur = stem_in;
   float* out = X;
   int h = 112;
+  f16* pin = P0;  // layered blocks: input / output planes
   for (size_t i = 0; i < blocks.size(); ++i) {
     const MbBlock& b = blocks[i];
+    if (i >= l0) {
+      const int oh = b.stride == 2 ? h / 2 : h;
+      if (i == l0) {  // the fused blocks' f32 output -> planes with the layered row stride
+        const size_t rows = (size_t)B * h * h, items = rows * (b.lcinp / 4);
+        hipLaunchKernelGGL(mbv2_split_pad_kernel, dim3((unsigned)((items + 255) / 256)), dim3(256), 0, s,
+                           reinterpret_cast<const float*>(cur), rows, b.cin, b.lcinp, pin, plo, range_flag());
+        MEC_LAUNCH_CHECK();
+      }
+      f16* pout = pin == P0 ? P1 : P0;
+      GemmParams g;  // expand: E = ReLU6(We X 2^-e + be), f32
+      g.split = 1; g.A = pin; g.a_lo = plo; g.B = Wt + b.lwe_off; g.b_lo = wlo; g.oscale = lx3_scale[2 * i];
+      g.bias = P + b.be_off; g.act = ACT_RELU6; g.C32 = Eb;
+      g.M = B * h * h; g.N = b.hidp; g.K = b.lcinp;
+      MEC_TRY(launch_gemm(g, s, nullptr, 0));  // inside the TAG_MBV2_BLOCK window
+      const size_t items = (size_t)B * oh * (b.hidp / 8);  // one output row of one 8-channel group each
+      if (b.stride == 2)
+        hipLaunchKernelGGL(mbv2_dw_x3_kernel<2>, dim3((unsigned)((items + 255) / 256)), dim3(256), 0, s, Eb, h, oh,
+                           b.hidp, P + b.wd_off, P + b.bd_off, Db, dlo, items);
+      else
+        hipLaunchKernelGGL(mbv2_dw_x3_kernel<1>, dim3((unsigned)((items + 255) / 256)), dim3(256), 0, s, Eb, h, oh,
+                           b.hidp, P + b.wd_off, P + b.bd_off, Db, dlo, items);
+      MEC_LAUNCH_CHECK();
+      g = GemmParams();  // project: Y = Wp D 2^-e + bp (+ the block input's planes), hi / lo planes
+      g.split = 1; g.A = Db; g.a_lo = dlo; g.B = Wt + b.lwp_off; g.b_lo = wlo; g.oscale = lx3_scale[2 * i + 1];
+      g.bias = P + b.lbp_off; g.act = ACT_NONE; g.C16 = pout; g.c_lo = plo;
+      if (b.stride == 1 && b.cin == b.cout) {
+        g.R = pin;
+        g.r_lo = plo;
+      }
+      g.M = B * oh * oh; g.N = b.lcoutp; g.K = b.hidp;
+      MEC_TRY(launch_gemm(g, s, nullptr, 0));  // inside the TAG_MBV2_BLOCK window
+      pin = pout;
+      h = oh;
+      continue;
+    }
     MbX3Args a;
     a.x = cur; a.y = out; a.H = h; a.OH = b.stride == 2 ? h / 2 : h;
     a.cin = b.cin; a.cout = b.cout;
@@ -611,12 +815,18 @@ int MobileNetModel::forward_x3(const uint8_t* img, int B, int H, int W, int C, f
   MEC_TRY(prof.end(TAG_MBV2_BLOCK, s));
   {  // features[18] 1x1 320 -> 1280 + BN + ReLU6 on the split GEMM engine
     const size_t n4 = (size_t)B * h * h * 320 / 4;
-    const long long llo = (long long)B * h * h * 320;
-    hipLaunchKernelGGL(mbv2_split_kernel, dim3((unsigned)((n4 + 255) / 256)), dim3(256), 0, s,
-                       reinterpret_cast<const float*>(cur), n4, Lin, llo, range_flag());
-    MEC_LAUNCH_CHECK();
+    long long llo = (long long)B * h * h * 320;
+    const f16* A = Lin;
+    if (l0 < blocks.size()) {  // the layered tail's planes (320 channels: no padding)
+      A = pin;
+      llo = plo;
+    } else {
+      hipLaunchKernelGGL(mbv2_split_kernel, dim3((unsigned)((n4 + 255) / 256)), dim3(256), 0, s,
+                         reinterpret_cast<const float*>(cur), n4, Lin, llo, range_flag());
+      MEC_LAUNCH_CHECK();
+    }
     GemmParams g;
-    g.split = 1; g.A = Lin; g.a_lo = llo; g.B = Wt + last_w_off; g.b_lo = wlo; g.oscale = x3_scale.back();
+    g.split = 1; g.A = A; g.a_lo = llo; g.B = Wt + last_w_off; g.b_lo = wlo; g.oscale = x3_scale.back();
     g.bias = P + last_b_off; g.act = ACT_RELU6; g.C32 = Lst;
     g.M = B * h * h; g.N = 1280; g.K = 320;
     MEC_TRY(launch_gemm(g, s, &prof, TAG_MBV2_LAST));

@@ -190,6 +190,10 @@ struct MbBlock {
   int cinp = 0, hidp = 0, coutp = 0;
   size_t we_off = 0, wp_off = 0;          // f16: expand [hidp][cinp], project [coutp][hidp]
   size_t be_off = 0, wd_off = 0, bd_off = 0, bp_off = 0;  // f32: expand bias, dw [hidp/8][9][8], dw bias, project bias
+  // fp32x3 layered form (hidp % 64 == 0): expand [hidp][lcinp], project [lcoutp][hidp] (lcoutp = cout padded
+  // to 64, lcinp = the previous block's lcoutp), project bias [lcoutp]
+  int lcinp = 0, lcoutp = 0;
+  size_t lwe_off = 0, lwp_off = 0, lbp_off = 0;
 };
 struct MobileNetModel : ImageNet {
   DevBuf wts;   // f16 1x1 weights
@@ -211,6 +215,7 @@ struct MobileNetModel : ImageNet {
   // the lo planes at x3_lo halfs; x3_scale: per block (expand, project) epilogue scales, then features[18]
   size_t x3_lo = 0;
   std::vector<float> x3_scale;
+  std::vector<float> lx3_scale;  // layered form: per block (expand, project) epilogue scales
   int create_x3(const float* blob, size_t n);
   int forward_x3(const uint8_t* img, int B, int H, int W, int C, float* feat, float* logits, float* probs,
                  hipStream_t s);

@@ -456,6 +456,29 @@ def test_mobilenet_v2_fp32x3_vs_oracle(dev, B):
     assert agree == len(sub) and err <= PROB_TOL and ferr <= FEAT_RTOL
 
 
+@pytest.mark.parametrize('first', [0, 7, 11, 15, 17])
+def test_mobilenet_v2_fp32x3_layered_tail_vs_oracle(dev, first):
+    """mbv2_layered k: features[k..17] as expand GEMM -> depthwise kernel -> project GEMM on split
+    planes (csrc/mobilenet_x3.hip; 0 = every block fused) against the oracle at the fp32 bars, and
+    batch invariance of the layered form (rows of a B=24 batch equal the same rows run as B=5)."""
+    from oracle import image_mbv2 as o_mb
+    gray = syn.image_inputs(24, seed=120 + first)
+    g = engine.to_device(gray, dev)
+    enc = engine.MobileNetImageEncoder(device=dev, precision='fp32x3')
+    enc.set_option('mbv2_layered', first)
+    feat, logits, probs = _np(enc.forward(g))
+    small = _np(enc.forward(g[:5]))
+    enc.check()
+    for i, (a, b) in enumerate(zip((feat, logits, probs), small)):
+        assert np.array_equal(a[:5], b), f'output {i}'
+    sub = np.array([0, 7, 15, 23])
+    rf, rl, rp = o_mb.forward(syn.weights('image_mbv2'), gray[sub])
+    err = float(np.abs(probs[sub] - rp).max())
+    ferr = float(np.abs(feat[sub] - rf).max() / np.abs(rf).max())
+    print(f'mbv2_layered {first}: probs max|d| {err:.3g}, feat rel err {ferr:.3g}')
+    assert err <= PROB_TOL and ferr <= FEAT_RTOL and (probs[sub].argmax(1) == rp.argmax(1)).all()
+
+
 def test_mobilenet_v2_fp32x3_batch_invariance_and_entry_shapes(dev):
     """Rows of a B=64 batch equal the same rows run as B=8 bit for bit (per-tile kernels, and the
     features[18] split GEMM's interleaved tiles share one k order); the RGB and already-resized
