@@ -181,6 +181,7 @@ int mec_conv_f32(const float* x, const float* w, const float* bias, const float*
  *   "resnet_chunk" [0]|n   ResNet layers 1-2 over n-image chunks (f16 and fp32x3; measured slower)
  *   "mbv2_x3_tile" 0|[4]   fp32x3 MobileNetV2: 4x4 output tiles for the stride-2 blocks at 56 / 28 outputs
  *   "mbv2_layered" 0|7..17 [8]  fp32x3 MobileNetV2: features[k..17] as expand GEMM -> depthwise -> project GEMM
+ *   "mbv2_layered16" 0|7..17 [8]  the same on the f16 path
  *   "mbv2_impl" [0]|1|2    MobileNetV2 block form: 0 = time both per block shape, 1 = workgroup, 2 = wave
  *   "fusion_r" 1|2|[4]     samples per fusion workgroup
  *   "fusion_split" 0|[1]   fusion as 3 launches (per-modality projection, cross-attention, head)

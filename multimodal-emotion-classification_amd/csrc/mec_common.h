@@ -112,6 +112,7 @@ struct Options {
   // fp32x3 MobileNetV2: features[k..17] as expand GEMM -> depthwise kernel -> project GEMM on hi / lo
   // planes (the "layered" form; k = 7..17, 0 = every block fused)
   int mbv2_layered = 8;
+  int mbv2_layered16 = 8;  // the same on the f16 path (features[k..17] on f16 GEMMs; 0 = every block fused)
   // ping-pong GEMM tile order inside each XCD's contiguous tile range: 0 = row-major (all N
   // panels of one M panel in turn), G = groups of G M panels walked M-fastest, so the 32
   // tiles an XCD runs at once share G A panels and 32/G weight panels

@@ -672,7 +672,7 @@ int MobileNetModel::create(const float* blob, size_t n) {
   static const int kSet[7][4] = {{1, 16, 1, 1}, {6, 24, 2, 2}, {6, 32, 3, 2}, {6, 64, 4, 2},
                                  {6, 96, 3, 1}, {6, 160, 3, 2}, {6, 320, 1, 1}};
   blocks.clear();
-  int cin = 32;
+  int cin = 32, prev_lcoutp = 32;
   for (int si = 0; si < 7; ++si)
     for (int r = 0; r < kSet[si][2]; ++r) {
       MbBlock b;
@@ -721,6 +721,23 @@ int MobileNetModel::create(const float* blob, size_t n) {
               w[b.wp_off + (size_t)o * b.hidp + h] = (f16)((double)wp[(size_t)o * b.hid + h] * sc[o]);
             pr[b.bp_off + o] = (float)sh[o];
           }
+      }
+      b.lcinp = prev_lcoutp;
+      b.lcoutp = pad_to(b.cout, 64);
+      prev_lcoutp = b.lcoutp;
+      if (b.t != 1 && b.hidp % 64 == 0) {  // layered form: the same matrices, K / N padded with zeros
+        b.lwe_off = w.size();
+        w.resize(w.size() + (size_t)b.hidp * b.lcinp, (f16)0.f);
+        for (int h = 0; h < b.hidp; ++h)
+          for (int c = 0; c < b.cinp && c < b.lcinp; ++c)
+            w[b.lwe_off + (size_t)h * b.lcinp + c] = w[b.we_off + (size_t)h * b.cinp + c];
+        b.lwp_off = w.size();
+        w.resize(w.size() + (size_t)b.lcoutp * b.hidp, (f16)0.f);
+        std::copy(w.begin() + b.wp_off, w.begin() + b.wp_off + (size_t)b.coutp * b.hidp, w.begin() + b.lwp_off);
+        align4();
+        b.lbp_off = pr.size();
+        pr.resize(pr.size() + b.lcoutp, 0.f);
+        std::copy(pr.begin() + b.bp_off, pr.begin() + b.bp_off + b.coutp, pr.begin() + b.lbp_off);
       }
       blocks.push_back(b);
       cin = b.cout;
@@ -858,6 +875,102 @@ static int dispatch_block(const MbBlock& b, const MbArgs& a, int B, int stem_c, 
   return -1;
 }
 
+// Layered tail of the f16 path (mbv2_layered16 k: features[k..17] as expand GEMM -> depthwise -> project
+// GEMM; the fused blocks' arithmetic with the GEMM engine's k order). Depthwise 3x3/S (pad 1) + BN shift +
+// ReLU6: E f16 NHWC [B,H,H,C] -> D f16 NHWC [B,OH,OH,C], fp32 FMAs from the shift in torch's (kh, kw) tap
+// order. A thread owns one output row of one 8-channel group, its 72 tap weights and a 3 x 3 window of
+// input pixels in registers (mobilenet_x3.hip's mbv2_dw_x3_kernel on f16 data).
+template <int S>
+__global__ __launch_bounds__(256) void mbv2_dw_f16_kernel(const f16* __restrict__ E, int H, int OH, int C,
+                                                          const float* __restrict__ Wd, const float* __restrict__ bd,
+                                                          f16* __restrict__ D, size_t items) {
+  const size_t it = (size_t)blockIdx.x * 256 + threadIdx.x;
+  if (it >= items) return;
+  const int G = C / 8;
+  const size_t row = it / G;  // (image, output row)
+  const int g = (int)(it - row * G);
+  const size_t n = row / OH;
+  const int oy = (int)(row - n * OH);
+  float w[9][8], bias[8];
+  {
+    const float* wd = Wd + (size_t)g * 72;
+#pragma unroll
+    for (int t = 0; t < 9; ++t) {
+      const float4 w0 = *reinterpret_cast<const float4*>(wd + t * 8);
+      const float4 w1 = *reinterpret_cast<const float4*>(wd + t * 8 + 4);
+      w[t][0] = w0.x; w[t][1] = w0.y; w[t][2] = w0.z; w[t][3] = w0.w;
+      w[t][4] = w1.x; w[t][5] = w1.y; w[t][6] = w1.z; w[t][7] = w1.w;
+    }
+    const float4 b0 = *reinterpret_cast<const float4*>(bd + 8 * g);
+    const float4 b1 = *reinterpret_cast<const float4*>(bd + 8 * g + 4);
+    bias[0] = b0.x; bias[1] = b0.y; bias[2] = b0.z; bias[3] = b0.w;
+    bias[4] = b1.x; bias[5] = b1.y; bias[6] = b1.z; bias[7] = b1.w;
+  }
+  bool rok[3];
+  const f16* rp[3];
+#pragma unroll
+  for (int ky = 0; ky < 3; ++ky) {
+    const int iy = oy * S - 1 + ky;
+    rok[ky] = iy >= 0 && iy < H;
+    rp[ky] = E + ((n * H + (rok[ky] ? iy : 0)) * H) * C + 8 * g;
+  }
+  auto load_col = [&](int ix, half8 (&e)[3], bool& ok) {
+    ok = ix >= 0 && ix < H;
+#pragma unroll
+    for (int ky = 0; ky < 3; ++ky)
+      e[ky] = (ok && rok[ky]) ? *reinterpret_cast<const half8*>(rp[ky] + (size_t)ix * C) : half8{0, 0, 0, 0, 0, 0, 0, 0};
+  };
+  half8 win[3][3];  // [kx][ky]: input columns ox S - 1 + kx
+  bool cok[3];
+  load_col(-1, win[0], cok[0]);
+  load_col(0, win[1], cok[1]);
+  f16* dst = D + (row * OH) * C + 8 * g;
+  for (int ox = 0; ox < OH; ++ox) {
+    if (S == 1) {
+      load_col(ox + 1, win[2], cok[2]);
+    } else {
+      load_col(2 * ox, win[1], cok[1]);
+      load_col(2 * ox + 1, win[2], cok[2]);
+    }
+    float d[8];
+#pragma unroll
+    for (int j = 0; j < 8; ++j) d[j] = bias[j];
+#pragma unroll
+    for (int ky = 0; ky < 3; ++ky) {
+      if (!rok[ky]) continue;
+#pragma unroll
+      for (int kx = 0; kx < 3; ++kx) {
+        if (!cok[kx]) continue;
+#pragma unroll
+        for (int j = 0; j < 8; ++j) d[j] = __builtin_fmaf((float)win[kx][ky][j], w[ky * 3 + kx][j], d[j]);
+      }
+    }
+    half8 o;
+#pragma unroll
+    for (int j = 0; j < 8; ++j) o[j] = (f16)relu6f(d[j]);
+    *reinterpret_cast<half8*>(dst + (size_t)ox * C) = o;
+#pragma unroll
+    for (int ky = 0; ky < 3; ++ky) {
+      win[0][ky] = S == 1 ? win[1][ky] : win[2][ky];
+      if (S == 1) win[1][ky] = win[2][ky];
+    }
+    cok[0] = S == 1 ? cok[1] : cok[2];
+    if (S == 1) cok[1] = cok[2];
+  }
+}
+
+// f16 [rows][cin] -> [rows][ld], channels cin .. ld-1 zero (the first layered block's input rows)
+__global__ __launch_bounds__(256) void mbv2_pad_f16_kernel(const f16* __restrict__ x, size_t rows, int cin, int ld,
+                                                           f16* __restrict__ y) {
+  const size_t i = (size_t)blockIdx.x * 256 + threadIdx.x;  // one 8-channel group of one row
+  const int G = ld / 8;
+  if (i >= rows * G) return;
+  const size_t r = i / G;
+  const int c = (int)(i - r * G) * 8;
+  *reinterpret_cast<half8*>(y + r * ld + c) =
+      c < cin ? *reinterpret_cast<const half8*>(x + r * cin + c) : half8{0, 0, 0, 0, 0, 0, 0, 0};
+}
+
 int MobileNetModel::forward_u8(const uint8_t* img, int B, int H, int W, int C, float* feat, float* logits,
                                float* probs, hipStream_t s) {
   MEC_REQUIRE(B >= 0, "image: B < 0");
@@ -868,20 +981,43 @@ int MobileNetModel::forward_u8(const uint8_t* img, int B, int H, int W, int C, f
               "image: input must be u8 [B,48,48,1] (GPU resize) or [B,224,224,{1,3}] (already resized)");
   if (prec == PREC_FP32) return forward_f32(img, B, H, W, C, feat, logits, probs, s);
   if (prec == PREC_FP32X3) return forward_x3(img, B, H, W, C, feat, logits, probs, s);
+  // layered tail: blocks[l0 ..] (features[l0 + 1 ..]) as expand GEMM -> depthwise -> project GEMM
+  size_t l0 = blocks.size();
+  if (opt().mbv2_layered16) {
+    l0 = (size_t)opt().mbv2_layered16 - 1;
+    for (size_t i = l0; i < blocks.size(); ++i)
+      MEC_REQUIRE(blocks[i].lwe_off, "mbv2: mbv2_layered16 names a block without a layered form");
+  }
+  size_t pe = 0, pd = 0, pp = 0;  // per-image elements of E, D and the tail's block I/O rows
+  {
+    int hh = 112;
+    for (size_t i = 0; i < blocks.size(); ++i) {
+      const MbBlock& b = blocks[i];
+      const int oh = b.stride == 2 ? hh / 2 : hh;
+      if (i >= l0) {
+        pe = std::max(pe, (size_t)hh * hh * b.hidp);
+        pd = std::max(pd, (size_t)oh * oh * b.hidp);
+        pp = std::max(pp, std::max((size_t)hh * hh * b.lcinp, (size_t)oh * oh * b.lcoutp));
+      }
+      hh = oh;
+    }
+  }
   const size_t per_big = (size_t)112 * 112 * 16;  // largest block output (features[1]), elements
   const size_t per_last = (size_t)49 * 1280;
-  const size_t per_img = 224 * 224 + (2 * per_big + per_last) * sizeof(f16) + 1280 * sizeof(float);
-  if (B > ws_batch) {
-    MEC_TRY(ws.ensure(per_img * (size_t)B + 4096));
-    ws_batch = B;
-  }
+  const size_t per_img =
+      224 * 224 + (2 * per_big + per_last + pe + pd + 2 * pp) * sizeof(f16) + 1280 * sizeof(float) + 64;
+  if (ws.bytes < per_img * (size_t)B + 4096) MEC_TRY(ws.ensure(per_img * (size_t)B + 4096));
   char* p = ws.as<char>();
   uint8_t* resized = reinterpret_cast<uint8_t*>(p);
   p += ((size_t)B * 224 * 224 + 255) / 256 * 256;
   f16* X = reinterpret_cast<f16*>(p); p += (size_t)B * per_big * sizeof(f16);
   f16* Y = reinterpret_cast<f16*>(p); p += (size_t)B * per_big * sizeof(f16);
   f16* L = reinterpret_cast<f16*>(p); p += (size_t)B * per_last * sizeof(f16);
-  float* pooled = reinterpret_cast<float*>(p);
+  float* pooled = reinterpret_cast<float*>(p); p += ((size_t)B * 1280 * sizeof(float) + 255) / 256 * 256;
+  f16* Eb = reinterpret_cast<f16*>(p); p += (size_t)B * pe * sizeof(f16);
+  f16* Db = reinterpret_cast<f16*>(p); p += (size_t)B * pd * sizeof(f16);
+  f16* P0 = reinterpret_cast<f16*>(p); p += (size_t)B * pp * sizeof(f16);
+  f16* P1 = reinterpret_cast<f16*>(p);
 
   const f16* Wt = wts.as<f16>();
   const float* P = prm.as<float>();
@@ -896,6 +1032,39 @@ int MobileNetModel::forward_u8(const uint8_t* img, int B, int H, int W, int C, f
   int h = 112;
   for (size_t i = 0; i < blocks.size(); ++i) {
     const MbBlock& b = blocks[i];
+    if (i >= l0) {
+      const int oh = b.stride == 2 ? h / 2 : h;
+      const f16* in = cur;
+      f16* pout = (cur == P0) ? P1 : P0;
+      if (i == l0 && b.cin != b.lcinp) {  // the fused blocks' rows -> the layered row stride
+        const size_t rows = (size_t)B * h * h, items = rows * (b.lcinp / 8);
+        hipLaunchKernelGGL(mbv2_pad_f16_kernel, dim3((unsigned)((items + 255) / 256)), dim3(256), 0, s, cur, rows,
+                           b.cin, b.lcinp, P1);
+        MEC_LAUNCH_CHECK();
+        in = P1;
+        pout = P0;
+      }
+      GemmParams g;  // expand + BN + ReLU6 -> E f16
+      g.A = in; g.B = Wt + b.lwe_off; g.bias = P + b.be_off; g.act = ACT_RELU6; g.C16 = Eb;
+      g.M = B * h * h; g.N = b.hidp; g.K = b.lcinp;
+      MEC_TRY(launch_gemm(g, s, nullptr, 0));  // inside the TAG_MBV2_BLOCK window
+      const size_t items = (size_t)B * oh * (b.hidp / 8);  // one output row of one 8-channel group each
+      if (b.stride == 2)
+        hipLaunchKernelGGL(mbv2_dw_f16_kernel<2>, dim3((unsigned)((items + 255) / 256)), dim3(256), 0, s, Eb, h, oh,
+                           b.hidp, P + b.wd_off, P + b.bd_off, Db, items);
+      else
+        hipLaunchKernelGGL(mbv2_dw_f16_kernel<1>, dim3((unsigned)((items + 255) / 256)), dim3(256), 0, s, Eb, h, oh,
+                           b.hidp, P + b.wd_off, P + b.bd_off, Db, items);
+      MEC_LAUNCH_CHECK();
+      g = GemmParams();  // project + BN (+ the block input) -> f16 rows of lcoutp channels
+      g.A = Db; g.B = Wt + b.lwp_off; g.bias = P + b.lbp_off; g.act = ACT_NONE; g.C16 = pout;
+      if (b.stride == 1 && b.cin == b.cout) g.R = in;
+      g.M = B * oh * oh; g.N = b.lcoutp; g.K = b.hidp;
+      MEC_TRY(launch_gemm(g, s, nullptr, 0));
+      cur = pout;
+      h = oh;
+      continue;
+    }
     MbArgs a;
     a.x = cur; a.y = out; a.H = h; a.OH = b.stride == 2 ? h / 2 : h;
     a.cin = b.cin; a.cout = b.cout; a.hidp = b.hidp;

@@ -93,3 +93,20 @@ def test_mbv2_wave_and_workgroup_forms_bit_identical(mb, dev, C):
     for a, b in zip(*outs):
         np.testing.assert_array_equal(a, b)
 
+
+
+@pytest.mark.parametrize('first', [7, 8, 12, 15])
+def test_mbv2_layered_tail_vs_oracle(dev, first):
+    """mbv2_layered16 k: features[k..17] as expand GEMM -> depthwise kernel -> project GEMM on f16
+    operands (csrc/mobilenet.hip) against the oracle at the f16 path's bars (probs 1e-3, argmax
+    exact), and batch invariance (rows of a B=24 batch equal the same rows run as B=5)."""
+    enc = engine.MobileNetImageEncoder(device=dev)
+    enc.set_option('mbv2_layered16', first)
+    gray = syn.image_inputs(24, seed=140 + first)
+    g = engine.to_device(gray, dev)
+    got = _np(enc.forward(g))
+    small = _np(enc.forward(g[:5]))
+    for i, (a, b) in enumerate(zip(got, small)):
+        np.testing.assert_array_equal(a[:5], b, err_msg=f'output {i}')
+    _check(got, o_mb.forward(syn.weights('image_mbv2'), gray))
+    enc.close()
