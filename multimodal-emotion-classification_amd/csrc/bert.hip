@@ -742,59 +742,74 @@ __global__ __launch_bounds__(512, 1) void bert_qkv_attn_kernel(const f16* __rest
 // Same products, term order and k order as the split QKV GEMM, the same attention code: the context
 // planes are bit-identical to the unfused pair (tests/test_gpu_fp32x3.py).
 constexpr int QX_BK = 32, QX_NK = BH / QX_BK;       // 24 K steps of 32
-constexpr int QX_PLANE = (QA_BM + QA_BN) * QX_BK;  // halfs per plane of a stage (32 KB)
-constexpr int QX_STAGE = 2 * QX_PLANE;             // hi + lo planes (64 KB)
 
 __device__ __forceinline__ int qx_sw(int row, int kc) { return kc ^ ((4 - ((row >> 2) & 3)) & 3); }  // sw<32>
 
-__global__ __launch_bounds__(512, 1) void bert_qkv_attn_x3_kernel(const f16* __restrict__ hs, long long hlo,
-                                                                  const f16* __restrict__ wqkv, long long wlo,
-                                                                  float oscale, const float* __restrict__ bqkv,
-                                                                  const int32_t* __restrict__ mask,
-                                                                  f16* __restrict__ ctx, long long clo, int nseq,
-                                                                  unsigned* flag) {
-  __shared__ __attribute__((aligned(16))) f16 smem[2 * QX_STAGE];  // 2 GEMM stages, then Q, then K / V images
-  __shared__ float sBias[ATT_L];
+// HP heads per workgroup: HP = 2, 8 waves (2 x 4, wave tile 64 x 96) on a 128 x 384 tile, 64-KB stages,
+// one workgroup per CU; HP = 1, 4 waves (2 x 2, the same 64 x 96 wave tile) on a 128 x 192 tile, 40-KB
+// stages and 80 KB of LDS in all, so two workgroups share a CU and one's attention phase overlaps the
+// other's GEMM. Both sum every output in the same term and k order: the same bits.
+template <int HP>
+__global__ __launch_bounds__(256 * HP, HP == 1 ? 2 : 1) void bert_qkv_attn_x3_kernel(
+    const f16* __restrict__ hs, long long hlo, const f16* __restrict__ wqkv, long long wlo, float oscale,
+    const float* __restrict__ bqkv, const int32_t* __restrict__ mask, f16* __restrict__ ctx, long long clo, int nseq,
+    unsigned* flag) {
+  static_assert(HP == 1 || HP == 2, "heads per workgroup");
+  constexpr int NW = 4 * HP, WNC = 2 * HP;             // waves; waves along N
+  constexpr int QBN = 192 * HP;                        // Q | K | V columns of the HP heads
+  constexpr int PLANE = (QA_BM + QBN) * QX_BK;         // halfs per plane of a stage
+  constexpr int STAGE = 2 * PLANE;                     // hi + lo planes (64 / 40 KB)
+  constexpr int IT = (QA_BM + QBN) / 16 / NW;          // 16-row wave-instructions per plane per wave
+  constexpr int IMG = ATT_L * BDH;                     // halfs per [128][64] image plane
+  static_assert(IT * 16 * NW == QA_BM + QBN, "loader");
+  static_assert(2 * STAGE >= 4 * HP * IMG, "K / V images (and before them the Q images) fit in the stages");
+  // 2 GEMM stages, then the Q, then the K / V images; HP = 1 keeps the mask bias in the stages too
+  // (past the K / V images), so the workgroup's LDS is exactly 80 KB
+  __shared__ __attribute__((aligned(16))) f16 smem[2 * STAGE];
+  __shared__ float sBias2[HP == 2 ? ATT_L : 1];
+  float* const sBias = HP == 2 ? sBias2 : reinterpret_cast<float*>(smem + 4 * IMG);
+  static_assert(HP == 2 || 4 * IMG + 2 * ATT_L <= 2 * STAGE, "mask bias past the K / V images");
   typedef __attribute__((address_space(3))) void* lds_p;
   const int tid = threadIdx.x, lane = tid & 63;
   const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
-  const int wm = wave >> 2, wn = wave & 3;
+  const int wm = wave / WNC, wn = wave % WNC;
   const int l16 = lane & 15, lq = lane >> 4;
-  // XCD-aware bijective remap: the 6 head pairs of a sequence (which share its token rows) on one XCD
-  const int nwg = nseq * 6;
+  // XCD-aware bijective remap: the 12 / HP head groups of a sequence (which share its token rows) on one XCD
+  constexpr int NG = BHEADS / HP;
+  const int nwg = nseq * NG;
   int bid = blockIdx.x;
   {
     const int xcd = bid & 7, q = nwg >> 3, r = nwg & 7;
     bid = (xcd < r ? xcd * (q + 1) : r * (q + 1) + (xcd - r) * q) + (bid >> 3);
   }
-  const int b = bid / 6, hp = bid - (bid / 6) * 6;
+  const int b = bid / NG, hp = bid - (bid / NG) * NG;
 
   // stage loader: LDS row R < 128 = token row R of the sequence; R >= 128 = weight row
-  // (R-128)/128 * 768 + hp*128 + (R-128)%128; 16 rows of 64 B per wave-instruction, 4 per plane per wave
+  // seg * 768 + (HP hp) * 64 + j for n = R - 128 = seg * 64 HP + j; 16 rows of 64 B per wave-instruction
   const int lrow = lane >> 2, pch = lane & 3;
-  const f16* src[4];
-  long long lo_off[4];
+  const f16* src[IT];
+  long long lo_off[IT];
 #pragma unroll
-  for (int it = 0; it < 4; ++it) {
-    const int R = (it * 8 + wave) * 16 + lrow;
+  for (int it = 0; it < IT; ++it) {
+    const int R = (it * NW + wave) * 16 + lrow;
     const int c = qx_sw(R, pch);
     if (R < QA_BM) {
       src[it] = hs + ((size_t)b * ATT_L + R) * BH + c * 8;
       lo_off[it] = hlo;
     } else {
-      const int n = R - QA_BM, seg = n >> 7, j = n & 127;
-      src[it] = wqkv + ((size_t)seg * BH + hp * 128 + j) * BH + c * 8;
+      const int n = R - QA_BM, seg = n / (64 * HP), j = n - seg * (64 * HP);
+      src[it] = wqkv + ((size_t)seg * BH + hp * 64 * HP + j) * BH + c * 8;
       lo_off[it] = wlo;
     }
   }
   auto issue = [&](int kt, int st) {
-    f16* base = smem + st * QX_STAGE;
+    f16* base = smem + st * STAGE;
 #pragma unroll
     for (int pl = 0; pl < 2; ++pl)
 #pragma unroll
-      for (int it = 0; it < 4; ++it)
+      for (int it = 0; it < IT; ++it)
         __builtin_amdgcn_global_load_lds((const void*)(src[it] + (pl ? lo_off[it] : 0) + kt * QX_BK),
-                                         (lds_p)(base + pl * QX_PLANE + (it * 8 + wave) * 16 * QX_BK), 16, 0, 0);
+                                         (lds_p)(base + pl * PLANE + (it * NW + wave) * 16 * QX_BK), 16, 0, 0);
   };
 
   floatx4 acc[4][6];
@@ -807,23 +822,23 @@ __global__ __launch_bounds__(512, 1) void bert_qkv_attn_x3_kernel(const f16* __r
 #pragma unroll 1
   for (int kt = 0; kt < QX_NK; ++kt) {
     if (kt + 1 < QX_NK)
-      asm volatile("s_waitcnt vmcnt(8)" ::: "memory");
+      asm volatile("s_waitcnt vmcnt(%0)" ::"n"(2 * IT) : "memory");
     else
       asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     __builtin_amdgcn_s_barrier();  // stage kt landed for every wave
-    const f16* sA = smem + (kt & 1) * QX_STAGE;
+    const f16* sA = smem + (kt & 1) * STAGE;
     half8 af[2][4], bf[2][6];  // [plane: 0 hi, 1 lo]
 #pragma unroll
     for (int pl = 0; pl < 2; ++pl) {
 #pragma unroll
       for (int i = 0; i < 4; ++i) {
         const int r = 64 * wm + 16 * i + l16;
-        af[pl][i] = *reinterpret_cast<const half8*>(sA + pl * QX_PLANE + r * QX_BK + qx_sw(r, lq) * 8);
+        af[pl][i] = *reinterpret_cast<const half8*>(sA + pl * PLANE + r * QX_BK + qx_sw(r, lq) * 8);
       }
 #pragma unroll
       for (int j = 0; j < 6; ++j) {
         const int rr = QA_BM + 96 * wn + 16 * j + l16;
-        bf[pl][j] = *reinterpret_cast<const half8*>(sA + pl * QX_PLANE + rr * QX_BK + qx_sw(rr, lq) * 8);
+        bf[pl][j] = *reinterpret_cast<const half8*>(sA + pl * PLANE + rr * QX_BK + qx_sw(rr, lq) * 8);
       }
     }
     // the stage is free once every wave holds its fragments: restage it for kt + 2 before the MFMAs
@@ -855,13 +870,13 @@ __global__ __launch_bounds__(512, 1) void bert_qkv_attn_x3_kernel(const f16* __r
   auto write_seg = [&](int want, f16* img) {
 #pragma unroll
     for (int j = 0; j < 6; ++j) {
-      const int n = 96 * wn + 16 * j + 4 * lq;  // features n .. n+3 (one 128-block, one head)
-      const int seg = n >> 7, hh = (n >> 6) & 1, d = n & 63;
+      const int n = 96 * wn + 16 * j + 4 * lq;  // features n .. n+3 (one 64-column head block)
+      const int seg = n / (64 * HP), hh = (n - seg * 64 * HP) >> 6, d = n & 63;
       if (seg != want) continue;
-      const float4 bv = *reinterpret_cast<const float4*>(bqkv + seg * BH + hp * 128 + (n & 127));
+      const float4 bv = *reinterpret_cast<const float4*>(bqkv + seg * BH + (hp * HP + hh) * 64 + d);
       const float bb[4] = {bv.x, bv.y, bv.z, bv.w};
       // hi plane of this (segment, head); its lo plane follows (Q: [head][plane]; K / V: [seg-1][head][plane])
-      f16* dst = img + (want == 0 ? 2 * hh : 2 * (2 * (seg - 1) + hh)) * (ATT_L * BDH);
+      f16* dst = img + (want == 0 ? 2 * hh : 2 * (HP * (seg - 1) + hh)) * IMG;
 #pragma unroll
       for (int i = 0; i < 4; ++i) {
         const int m = 64 * wm + 16 * i + l16;  // token
@@ -876,42 +891,46 @@ __global__ __launch_bounds__(512, 1) void bert_qkv_attn_x3_kernel(const f16* __r
         }
         const int ch = seg == 2 ? vswz(m, d >> 3) : aswz(m, d >> 3);
         *reinterpret_cast<half4*>(dst + m * BDH + ch * 8 + (d & 7)) = hv;
-        *reinterpret_cast<half4*>(dst + ATT_L * BDH + m * BDH + ch * 8 + (d & 7)) = lv;
+        *reinterpret_cast<half4*>(dst + IMG + m * BDH + ch * 8 + (d & 7)) = lv;
       }
     }
   };
-  // phase 1: Q planes of both heads ([head][plane] at smem), then every wave's query fragments
+  // phase 1: Q planes of the heads ([head][plane] at smem), then every wave's query fragments
   write_seg(0, smem);
   __syncthreads();
-  const int hh = wave >> 2, aw = wave & 3;  // this wave's head (of the pair) and its index among that head's 4
+  const int hh = wave >> 2, aw = wave & 3;  // this wave's head (of the group) and its index among that head's 4
   const int lr = lane & 31, lh = lane >> 5;
   half8 qh[4], ql[4];
   {
-    const f16* qi = smem + hh * 2 * (ATT_L * BDH);
+    const f16* qi = smem + hh * 2 * IMG;
     const int rq = 32 * aw + lr;
 #pragma unroll
     for (int kk = 0; kk < 4; ++kk) {
       const int kc = 2 * kk + lh;
       qh[kk] = *reinterpret_cast<const half8*>(qi + rq * BDH + aswz(rq, kc) * 8);
-      ql[kk] = *reinterpret_cast<const half8*>(qi + ATT_L * BDH + rq * BDH + aswz(rq, kc) * 8);
+      ql[kk] = *reinterpret_cast<const half8*>(qi + IMG + rq * BDH + aswz(rq, kc) * 8);
     }
   }
   asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
   __syncthreads();
-  // phase 2: K and V planes ([K h0 hi, K h0 lo, K h1 hi, K h1 lo, V h0 hi, ..] at smem)
+  // phase 2: K and V planes ([K h0 hi, K h0 lo, (K h1 ..), V h0 hi, ..] at smem)
   write_seg(1, smem);
   write_seg(2, smem);
   x3_raise(flag, bad);
   __syncthreads();
-  f16* const sK[2] = {smem + (0 * 2 + hh) * 2 * (ATT_L * BDH), smem + ((0 * 2 + hh) * 2 + 1) * (ATT_L * BDH)};
-  const f16* const sV[2] = {smem + (1 * 2 + hh) * 2 * (ATT_L * BDH), smem + ((1 * 2 + hh) * 2 + 1) * (ATT_L * BDH)};
-  attn_head_x3<0>(sK, sV, sBias, qh, ql, aw, lane, ctx, clo, b, 2 * hp + hh);
+  f16* const sK[2] = {smem + (0 * HP + hh) * 2 * IMG, smem + ((0 * HP + hh) * 2 + 1) * IMG};
+  const f16* const sV[2] = {smem + (1 * HP + hh) * 2 * IMG, smem + ((1 * HP + hh) * 2 + 1) * IMG};
+  attn_head_x3<0>(sK, sV, sBias, qh, ql, aw, lane, ctx, clo, b, HP * hp + hh);
 }
 
 int launch_bert_qkv_attn_x3(const f16* hs, long long hlo, const f16* wqkv, long long wlo, float oscale,
                             const float* bqkv, const int32_t* mask, f16* ctx, long long clo, int B, hipStream_t s) {
-  hipLaunchKernelGGL(bert_qkv_attn_x3_kernel, dim3(B * 6), dim3(512), 0, s, hs, hlo, wqkv, wlo, oscale, bqkv, mask, ctx,
-                     clo, B, range_flag());
+  if (opt().bert_qkv_attn_x3_heads == 1)
+    hipLaunchKernelGGL(bert_qkv_attn_x3_kernel<1>, dim3(B * 12), dim3(256), 0, s, hs, hlo, wqkv, wlo, oscale, bqkv,
+                       mask, ctx, clo, B, range_flag());
+  else
+    hipLaunchKernelGGL(bert_qkv_attn_x3_kernel<2>, dim3(B * 6), dim3(512), 0, s, hs, hlo, wqkv, wlo, oscale, bqkv,
+                       mask, ctx, clo, B, range_flag());
   MEC_LAUNCH_CHECK();
   return 0;
 }

@@ -98,6 +98,9 @@ struct Options {
   // the downsample, 2 -> 3), 2 also the 256 -> 128 seam into layer2
   int pw_chain_x3 = 2;
   int bert_qkv_attn = 1;    // fused BERT QKV projection + attention
+  // fp32x3 fused QKV + attention: heads per workgroup (2: 8 waves, 128 KB of LDS, one per CU; 1: 4 waves,
+  // 80 KB, two per CU so one's attention overlaps the other's GEMM); same bits
+  int bert_qkv_attn_x3_heads = 1;
   int bert_ln_rows = 2;     // BERT LayerNorm rows per wave (1 | 2 | 4): 27.0 / 25.7 / 26.3 us at B = 256
   // BERT's last layer on the [CLS] rows only (the outputs -- pooler, logits, CLS feature -- read
   // nothing else of it): K / V for every token, Q, attention, O-projection, LayerNorms and FFN for

@@ -423,14 +423,16 @@ def test_text_fp32x3_fused_qkv_attention_bit_identical(dev, B, ragged):
     ids, mask = syn.text_inputs(B, 128, seed=800 + B, ragged=ragged)
     args = (engine.to_device(ids, dev), engine.to_device(mask, dev))
     outs = []
-    for fused in (1, 0):
+    for fused, heads in ((0, 2), (1, 2), (1, 1)):  # heads per workgroup of the fused kernel: 2 or 1
         enc = engine.TextEncoder(device=dev, precision='fp32x3')
         enc.set_option('bert_qkv_attn', fused)
+        enc.set_option('bert_qkv_attn_x3_heads', heads)
         outs.append(_np(enc.forward(*args)))
         enc.check()
         enc.close()
-    for k, (a, b) in enumerate(zip(*outs)):
-        assert np.array_equal(a, b), f'output {k}: max |d| {np.abs(a - b).max()}'
+    for form, o in zip(('fused, 2 heads', 'fused, 1 head'), outs[1:]):
+        for k, (a, b) in enumerate(zip(outs[0], o)):
+            assert np.array_equal(a, b), f'{form}, output {k}: max |d| {np.abs(a - b).max()}'
 
 
 # ------------------------------------------------------------------ MobileNetV2 on the fp32x3 path
