@@ -587,49 +587,62 @@ int launch_bert_attention_x3_cls(const f16* kv, long long lo, const int32_t* mas
 constexpr int QA_BM = 128, QA_BN = 384, QA_BK = 64, QA_NK = BH / QA_BK;
 constexpr int QA_STAGE = (QA_BM + QA_BN) * QA_BK;  // halfs per stage (64 KB)
 
-template <int DBG = 0>  // probe builds (wrong results): 1 = no attention, 2 = main loop only
-__global__ __launch_bounds__(512, 1) void bert_qkv_attn_kernel(const f16* __restrict__ h16,
-                                                               const f16* __restrict__ wqkv,
-                                                               const float* __restrict__ bqkv,
-                                                               const int32_t* __restrict__ mask,
-                                                               f16* __restrict__ ctx, int nseq) {
-  __shared__ __attribute__((aligned(16))) f16 smem[2 * QA_STAGE];  // 2 GEMM stages, then Q/K/V images
-  __shared__ float sBias[ATT_L];
+// HP heads per workgroup: HP = 2, 8 waves on the 128 x 384 tile, 64-KB stages, one workgroup per CU;
+// HP = 1 (bert_qkv_attn_heads 1), 4 waves (2 x 2 of the same 64 x 96 wave tile) on a 128 x 192 tile,
+// 40-KB stages and 80 KB of LDS in all (the mask bias inside it), so two workgroups share a CU and one's
+// attention overlaps the other's GEMM. Same sums in the same order: the same bits.
+template <int DBG = 0, int HP = 2>  // probe builds (wrong results): DBG 1 = no attention, 2 = main loop only
+__global__ __launch_bounds__(256 * HP, HP == 1 ? 2 : 1) void bert_qkv_attn_kernel(const f16* __restrict__ h16,
+                                                                                  const f16* __restrict__ wqkv,
+                                                                                  const float* __restrict__ bqkv,
+                                                                                  const int32_t* __restrict__ mask,
+                                                                                  f16* __restrict__ ctx, int nseq) {
+  static_assert(HP == 1 || HP == 2, "heads per workgroup");
+  constexpr int NW = 4 * HP, WNC = 2 * HP;        // waves; waves along N
+  constexpr int STAGE = (QA_BM + 192 * HP) * QA_BK;  // halfs per stage (64 / 40 KB)
+  constexpr int IT = (QA_BM + 192 * HP) / 8 / NW;  // 8-row wave-instructions per stage per wave
+  constexpr int IMG = ATT_L * BDH;
+  static_assert(IT * 8 * NW == QA_BM + 192 * HP, "loader");
+  static_assert(HP == 2 || 3 * IMG + 2 * ATT_L <= 2 * STAGE, "mask bias past the Q / K / V images");
+  __shared__ __attribute__((aligned(16))) f16 smem[2 * STAGE];  // 2 GEMM stages, then Q/K/V images
+  __shared__ float sBias2[HP == 2 ? ATT_L : 1];
+  float* const sBias = HP == 2 ? sBias2 : reinterpret_cast<float*>(smem + 3 * IMG);
   typedef __attribute__((address_space(3))) void* lds_p;
   const int tid = threadIdx.x, lane = tid & 63;
   const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
-  const int wm = wave >> 2, wn = wave & 3;
+  const int wm = wave / WNC, wn = wave % WNC;
   const int l16 = lane & 15, lq = lane >> 4;
-  // XCD-aware bijective remap: the 6 head pairs of a sequence (which share its 192-KB token
+  // XCD-aware bijective remap: the 12 / HP head groups of a sequence (which share its 192-KB token
   // rows) run on one XCD's L2
-  const int nwg = nseq * 6;
+  constexpr int NG = BHEADS / HP;
+  const int nwg = nseq * NG;
   int bid = blockIdx.x;
   {
     const int xcd = bid & 7, q = nwg >> 3, r = nwg & 7;
     bid = (xcd < r ? xcd * (q + 1) : r * (q + 1) + (xcd - r) * q) + (bid >> 3);
   }
-  const int b = bid / 6, hp = bid - (bid / 6) * 6;
+  const int b = bid / NG, hp = bid - (bid / NG) * NG;
 
   // stage loader: LDS row R < 128 = token row R of the sequence; R >= 128 = W row
-  // (R-128)/128 * 768 + hp*128 + (R-128)%128 (Q, K, V blocks of the two heads)
+  // seg * 768 + (HP hp) * 64 + j for n = R - 128 = seg * 64 HP + j (the Q, K, V blocks of the heads)
   const int lrow = lane >> 3, pch = lane & 7;
-  const f16* src0[8];
+  const f16* src0[IT];
 #pragma unroll
-  for (int it = 0; it < 8; ++it) {
-    const int R = (it * 8 + wave) * 8 + lrow;  // 64 rows per pass of the 8 waves
+  for (int it = 0; it < IT; ++it) {
+    const int R = (it * NW + wave) * 8 + lrow;  // 8 NW rows per pass of the waves
     const int c = pch ^ ((R >> 1) & 7);
     if (R < QA_BM) {
       src0[it] = h16 + ((size_t)b * ATT_L + R) * BH + c * 8;
     } else {
-      const int n = R - QA_BM, seg = n >> 7, j = n & 127;
-      src0[it] = wqkv + ((size_t)seg * BH + hp * 128 + j) * BH + c * 8;
+      const int n = R - QA_BM, seg = n / (64 * HP), j = n - seg * (64 * HP);
+      src0[it] = wqkv + ((size_t)seg * BH + hp * 64 * HP + j) * BH + c * 8;
     }
   }
   auto issue = [&](int kt, int st) {
-    f16* base = smem + st * QA_STAGE;
+    f16* base = smem + st * STAGE;
 #pragma unroll
-    for (int it = 0; it < 8; ++it)
-      __builtin_amdgcn_global_load_lds((const void*)(src0[it] + kt * QA_BK), (lds_p)(base + (it * 8 + wave) * 8 * QA_BK),
+    for (int it = 0; it < IT; ++it)
+      __builtin_amdgcn_global_load_lds((const void*)(src0[it] + kt * QA_BK), (lds_p)(base + (it * NW + wave) * 8 * QA_BK),
                                        16, 0, 0);
   };
 
@@ -643,11 +656,11 @@ __global__ __launch_bounds__(512, 1) void bert_qkv_attn_kernel(const f16* __rest
 #pragma unroll 1
   for (int kt = 0; kt < QA_NK; ++kt) {
     if (kt + 1 < QA_NK)
-      asm volatile("s_waitcnt vmcnt(8)" ::: "memory");
+      asm volatile("s_waitcnt vmcnt(%0)" ::"n"(IT) : "memory");
     else
       asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     __builtin_amdgcn_s_barrier();  // stage kt landed for every wave
-    const f16* sA = smem + (kt & 1) * QA_STAGE;
+    const f16* sA = smem + (kt & 1) * STAGE;
     const f16* sB = sA + QA_BM * QA_BK;
     half8 af[2][4], bf[2][6];
 #pragma unroll
@@ -690,16 +703,17 @@ __global__ __launch_bounds__(512, 1) void bert_qkv_attn_kernel(const f16* __rest
     if (t == 12345.678f) ctx[tid] = (f16)t;
     return;
   }
-  // ---- epilogue: (acc + bias) + 0 -> f16 -> the attention's Q / K / V LDS images
+  // ---- epilogue: (acc + bias) + 0 -> f16 -> the attention's Q / K / V LDS images (every wave is past
+  // its last stage read: the loop's second barrier)
   if (tid < ATT_L) sBias[tid] = mask[(size_t)b * ATT_L + tid] ? 0.f : -3.4028234663852886e38f;  // finfo(f32).min
-  f16* img = smem;  // [Q0 Q1 K0 K1 V0 V1], each [128][64]
+  f16* img = smem;  // [Q (HP heads) | K | V], each [128][64]
 #pragma unroll
   for (int j = 0; j < 6; ++j) {
-    const int n = 96 * wn + 16 * j + 4 * lq;  // features n .. n+3 (one 128-block, one head)
-    const int seg = n >> 7, hh = (n >> 6) & 1, d = n & 63;
-    const float4 bv = *reinterpret_cast<const float4*>(bqkv + seg * BH + hp * 128 + (n & 127));
+    const int n = 96 * wn + 16 * j + 4 * lq;  // features n .. n+3 (one 64-column head block)
+    const int seg = n / (64 * HP), hh = (n - seg * 64 * HP) >> 6, d = n & 63;
+    const float4 bv = *reinterpret_cast<const float4*>(bqkv + seg * BH + (hp * HP + hh) * 64 + d);
     const float bb[4] = {bv.x, bv.y, bv.z, bv.w};
-    f16* dst = img + (seg * 2 + hh) * (ATT_L * BDH);
+    f16* dst = img + (seg * HP + hh) * IMG;
 #pragma unroll
     for (int i = 0; i < 4; ++i) {
       const int m = 64 * wm + 16 * i + l16;  // token
@@ -720,10 +734,9 @@ __global__ __launch_bounds__(512, 1) void bert_qkv_attn_kernel(const f16* __rest
     return;
   }
   const int hh = wave >> 2;
-  attn_head(img + hh * (ATT_L * BDH), img + (2 + hh) * (ATT_L * BDH), img + (4 + hh) * (ATT_L * BDH), sBias,
-            wave & 3, lane, ctx + (size_t)b * ATT_L * BH + (2 * hp + hh) * BDH);
+  attn_head(img + hh * IMG, img + (HP + hh) * IMG, img + (2 * HP + hh) * IMG, sBias, wave & 3, lane,
+            ctx + (size_t)b * ATT_L * BH + (HP * hp + hh) * BDH);
 }
-
 
 // ----------------------------------------------------------------------------- fp32x3 QKV + attention
 // The fp32x3 path's QKV projection and attention of one (sequence, head pair) in one workgroup, as
@@ -1142,6 +1155,9 @@ int TextModel::forward(const int32_t* ids, const int32_t* mask, int B, int L, fl
         hipLaunchKernelGGL((bert_qkv_attn_kernel<2>), dim3(B * 6), dim3(512), 0, s, h16, wqkv, bqkv, mask, ctx16, B);
       else
 #endif
+      if (opt().bert_qkv_attn_heads == 1)
+        hipLaunchKernelGGL((bert_qkv_attn_kernel<0, 1>), dim3(B * 12), dim3(256), 0, s, h16, wqkv, bqkv, mask, ctx16, B);
+      else
         hipLaunchKernelGGL((bert_qkv_attn_kernel<0>), dim3(B * 6), dim3(512), 0, s, h16, wqkv, bqkv, mask, ctx16, B);
       MEC_LAUNCH_CHECK();
       MEC_TRY(prof.end(TAG_BERT_ATTN, s));

@@ -101,6 +101,7 @@ struct Options {
   // fp32x3 fused QKV + attention: heads per workgroup (2: 8 waves, 128 KB of LDS, one per CU; 1: 4 waves,
   // 80 KB, two per CU so one's attention overlaps the other's GEMM); same bits
   int bert_qkv_attn_x3_heads = 1;
+  int bert_qkv_attn_heads = 1;  // the same for the f16 fused kernel (bert_qkv_attn_kernel)
   int bert_ln_rows = 2;     // BERT LayerNorm rows per wave (1 | 2 | 4): 27.0 / 25.7 / 26.3 us at B = 256
   // BERT's last layer on the [CLS] rows only (the outputs -- pooler, logits, CLS feature -- read
   // nothing else of it): K / V for every token, Q, attention, O-projection, LayerNorms and FFN for

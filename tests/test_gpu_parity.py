@@ -10,6 +10,7 @@ from oracle import fusion as o_f, image as o_i, speech as o_s, text as o_t
 pytestmark = pytest.mark.gpu
 
 PROB_TOL = 1e-3        # north_star: softmax probabilities within 1e-3
+HEADS_DEFAULT = 1      # bert_qkv_attn_heads' default (csrc/mec_common.h), restored after the A/B test
 F32_TOL = 2e-5         # fp32 kernels (speech, fusion) vs fp32 oracle
 
 
@@ -167,18 +168,22 @@ def test_bad_shapes_raise(models, dev):
 
 @pytest.mark.parametrize('B', [1, 3, 9])
 def test_text_qkv_attn_bit_identical(models, dev, B):
-    """BERT with the fused QKV-projection + attention kernel and with the QKV GEMM followed by
-    the attention kernel: identical CLS features, logits and probabilities (B = 9: 54
-    workgroups over the XCD remap with a remainder)."""
+    """BERT with the fused QKV-projection + attention kernel (two heads per workgroup, and one:
+    bert_qkv_attn_heads) and with the QKV GEMM followed by the attention kernel: identical CLS
+    features, logits and probabilities (B = 9: 54 / 108 workgroups over the XCD remap with a
+    remainder)."""
     ids, mask = syn.text_inputs(B, 128, seed=300 + B, ragged=True)
     args = (engine.to_device(ids, dev), engine.to_device(mask, dev))
     enc = models['text']
     outs = []
-    for fused in (1, 0):
+    for fused, heads in ((1, 2), (1, 1), (0, 2)):
         enc.set_option('bert_qkv_attn', fused)
+        enc.set_option('bert_qkv_attn_heads', heads)
         try:
             outs.append(_np(enc.forward(*args)))
         finally:
             enc.set_option('bert_qkv_attn', 1)
-    for a, b in zip(*outs):
-        np.testing.assert_array_equal(a, b)
+            enc.set_option('bert_qkv_attn_heads', HEADS_DEFAULT)
+    for o in outs[1:]:
+        for a, b in zip(outs[0], o):
+            np.testing.assert_array_equal(a, b)
