@@ -18,6 +18,7 @@ from ._lib import MecError
 
 TAG_BERT_FFN2 = 5  # launch class of BERT's FFN2 GEMM (mec_common.h Tag)
 TAG_BERT_QKV = 1  # ... and of its QKV GEMM
+TAG_BERT_OPROJ = 3  # ... and of its attention output projection
 
 KINDS = synthetic.KIND_IDS
 
@@ -335,9 +336,13 @@ class FusedPipeline:
             # the same for the fp32x3 path: FFN2 on the 256 x 256 K-interleaved split tile (384 tiles,
             # 1.5 rounds of 256 CUs: the image stream fills the half-empty round) instead of the
             # autotuner's 128 x 128 / 256 x 128 pick: 26.62 vs 27.49 ms per step (interleaved A/B,
-            # tools/gpu_ab_x3tags.sh, profiles/r03_ab_x3tag_ffn2.txt; the O-projection pinned the
-            # same way measured within 0.3 %). Every interleaved tile gives the same bits.
+            # tools/gpu_ab_x3tags.sh, profiles/r03_ab_x3tag_ffn2.txt). Every interleaved tile gives
+            # the same bits.
             self.text.set_option('gemm_x3_tag', TAG_BERT_FFN2 * 100000 + 70256)
+            # the O-projection (N = 768) the same way, since the fused QKV kernels share CUs two at a
+            # time: 25.00 vs 25.21 ms per step (11 interleaved rounds, profiles/r04_ab_x3tag_oproj2.txt;
+            # within 0.3 % in round 3, before that change)
+            self.text.set_option('gemm_x3_tag', TAG_BERT_OPROJ * 100000 + 70256)
             # QKV (N = 2304: 1152 tiles, 4.5 rounds) on the same tile, which the autotuner picks alone
             # too but not on every run: 25.45 vs 25.58 ms per step autotuned, 256 x 128 / 128 x 128
             # 25.95 / 25.86 (profiles/r03_ab_x3tag_qkv.txt)
