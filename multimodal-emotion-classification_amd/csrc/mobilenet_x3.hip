@@ -53,9 +53,12 @@ struct MxGeom {
   static constexpr int EF = MX_HC + 4;   // f32 row of the expanded chunk
   static constexpr int ELD = MX_HC + 8;  // f16 plane row of the depthwise output
   static constexpr int NQ = TO * TO;
+  // depthwise-output rows: the output pixels rounded up to whole 16-pixel project fragments (16 for
+  // a 4 x 4 tile, where 64 rows put the stride-2 blocks at three workgroups per CU instead of four)
+  static constexpr int NDR = (NQ + 15) / 16 * 16;
   static constexpr int OT = COUTP / 16, KX = CINP / 32;
   static constexpr size_t LDS_FIXED = (size_t)(EXPAND ? 2 * MP * XLD * 2 + MP * EF * 4 : MP * XF * 4) +
-                                      2 * 64 * ELD * 2 + (HIDP * (EXPAND ? 2 : 1) + COUTP) * 4;
+                                      2 * NDR * ELD * 2 + (HIDP * (EXPAND ? 2 : 1) + COUTP) * 4;
   // depthwise weights staged in LDS when they fit beside the tile (else read through L1 / L2)
   static constexpr bool DWL = LDS_FIXED + HIDP * 9 * 4 <= 128 * 1024;
 };
@@ -64,7 +67,7 @@ template <int S, int TO, int CINP, int HIDP, int COUTP, bool EXPAND, bool RES, i
 __global__ __launch_bounds__(256) void mbv2_x3_kernel(const MbX3Args a) {
   using G = MxGeom<S, TO, CINP, HIDP, COUTP, EXPAND, RES, STEM>;
   constexpr int IR = G::IR, NP = G::NP, MP = G::MP, XLD = G::XLD, XF = G::XF, EF = G::EF, ELD = G::ELD;
-  constexpr int NQ = G::NQ, OT = G::OT, KX = G::KX;
+  constexpr int NQ = G::NQ, NDR = G::NDR, OT = G::OT, KX = G::KX;
   static_assert(NQ <= 64, "tile");
   static_assert(!STEM || (CINP == 32 && HIDP == 32 && !EXPAND && S == 1), "stem fuses into block 1 only");
   static_assert(STEM || EXPAND, "t = 1 blocks only as block 1 (with the stem)");
@@ -72,8 +75,8 @@ __global__ __launch_bounds__(256) void mbv2_x3_kernel(const MbX3Args a) {
   __shared__ __attribute__((aligned(16))) f16 sXl[EXPAND ? MP * XLD : 8];
   __shared__ __attribute__((aligned(16))) float sXf[EXPAND ? 4 : MP * XF];
   __shared__ __attribute__((aligned(16))) float sE[EXPAND ? MP * EF : 4];
-  __shared__ __attribute__((aligned(16))) f16 sDh[64 * ELD];
-  __shared__ __attribute__((aligned(16))) f16 sDl[64 * ELD];
+  __shared__ __attribute__((aligned(16))) f16 sDh[NDR * ELD];
+  __shared__ __attribute__((aligned(16))) f16 sDl[NDR * ELD];
   __shared__ __attribute__((aligned(16))) float sWd[G::DWL ? HIDP * 9 : 4];
   __shared__ __attribute__((aligned(16))) float sBd[HIDP];
   __shared__ __attribute__((aligned(16))) float sBe[EXPAND ? HIDP : 4];
@@ -293,13 +296,16 @@ __global__ __launch_bounds__(256) void mbv2_x3_kernel(const MbX3Args a) {
           ol[j] = (f16)(v - (float)oh[j]);
         }
       }
-      *reinterpret_cast<half8*>(sDh + dq * ELD + 8 * dcg) = oh;
-      *reinterpret_cast<half8*>(sDl + dq * ELD + 8 * dcg) = ol;
+      if (dq < NDR) {  // rows NQ .. NDR - 1: zeros for the last fragment's padding pixels
+        *reinterpret_cast<half8*>(sDh + dq * ELD + 8 * dcg) = oh;
+        *reinterpret_cast<half8*>(sDl + dq * ELD + 8 * dcg) = ol;
+      }
     }
     __syncthreads();
 
-    // ---- project: out^T[o][q] += Wp[o][h0..h0+31] . D[q][:]; wave w owns pixels 16w..16w+15
-    {
+    // ---- project: out^T[o][q] += Wp[o][h0..h0+31] . D[q][:]; wave w owns pixels 16w..16w+15 (the
+    // waves past the tile's pixels have nothing to project)
+    if (16 * wave < NDR) {
       const half8 bh = *reinterpret_cast<const half8*>(sDh + (16 * wave + l16) * ELD + 8 * lq);
       const half8 bl = *reinterpret_cast<const half8*>(sDl + (16 * wave + l16) * ELD + 8 * lq);
 #pragma unroll

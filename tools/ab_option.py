@@ -31,6 +31,8 @@ def main():
     ap.add_argument('--rounds', type=int, default=5)
     ap.add_argument('--probes', action='store_true', help='load libmec_hip_probes.so (probe option values)')
     ap.add_argument('--precision', default='f16', choices=['f16', 'fp32', 'fp32x3'])
+    ap.add_argument('--save', help='write the first value\'s outputs to this .npz (cross-build bit comparisons, '
+                                   'with MEC_LIB naming the other build)')
     a = ap.parse_args()
     dev = torch.device('cuda', 0)
     lib = _lib.load()
@@ -75,6 +77,9 @@ def main():
             torch.cuda.synchronize()
             times[v].append((time.perf_counter() - t0) * 1e3 / a.iters)
     base = outs[a.values[0]]
+    if a.save:
+        import numpy as np
+        np.savez(a.save, *[t.cpu().numpy() for t in base])
     for v in a.values:
         d = [float((x - y).abs().max()) for x, y in zip(outs[v], base)]
         print(json.dumps({'enc': a.enc, 'precision': a.precision, a.opt: v, 'ms': round(sorted(times[v])[len(times[v]) // 2], 4),
