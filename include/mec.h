@@ -182,6 +182,8 @@ int mec_conv_f32(const float* x, const float* w, const float* bias, const float*
  *                          the pooler, logits and CLS feature read nothing else of it; same bits as 0
  *   "resnet_chunk" [0]|n   ResNet layers 1-2 over n-image chunks (f16 and fp32x3; measured slower)
  *   "mbv2_x3_tile" 0|[4]   fp32x3 MobileNetV2: 4x4 output tiles for the stride-2 blocks at 56 / 28 outputs
+ *   "mbv2_x3_tpw" 1|[2]..16 fp32x3 MobileNetV2 fused blocks: output tiles per workgroup, the next tile's
+ *                          input loaded into registers while one computes (same bits for every value)
  *   "mbv2_layered" 0|7..17 [8]  fp32x3 MobileNetV2: features[k..17] as expand GEMM -> depthwise -> project GEMM
  *   "mbv2_layered16" 0|7..17 [8]  the same on the f16 path
  *   "mbv2_impl" [0]|1|2    MobileNetV2 block form: 0 = time both per block shape, 1 = workgroup, 2 = wave

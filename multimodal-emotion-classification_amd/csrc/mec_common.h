@@ -113,6 +113,7 @@ struct Options {
   // workgroups per CU), 0 = 8x8 / 7x7 (17x17 / 15x15 inputs, one per CU); same bits. 4: 2.99 -> 2.92 ms
   // at B = 256 (profiles/r04_ab_mbv2x3_tile.txt)
   int mbv2_x3_tile = 4;
+  int mbv2_x3_tpw = 2;  // fp32x3 MobileNetV2 fused blocks: output tiles per workgroup (next tile's input prefetched)
   // fp32x3 MobileNetV2: features[k..17] as expand GEMM -> depthwise kernel -> project GEMM on hi / lo
   // planes (the "layered" form; k = 7..17, 0 = every block fused)
   int mbv2_layered = 8;

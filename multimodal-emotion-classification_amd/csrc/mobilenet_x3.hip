@@ -41,6 +41,7 @@ struct MbX3Args {
   const float* stem_w;     // [C*9][32] folded stem weights (STEM > 0)
   const float* stem_corr;  // [4][32] bias per border class (STEM > 0)
   unsigned* flag;          // range flag (x3_raise): a block input outside the f16 range
+  int ntiles;              // B * (OH / TO)^2 output tiles, walked with a stride of gridDim.x
 };
 
 __device__ __forceinline__ float relu6x(float v) { return fminf(fmaxf(v, 0.f), 6.f); }
@@ -64,7 +65,7 @@ struct MxGeom {
 };
 
 template <int S, int TO, int CINP, int HIDP, int COUTP, bool EXPAND, bool RES, int STEM>
-__global__ __launch_bounds__(256) void mbv2_x3_kernel(const MbX3Args a) {
+__global__ __launch_bounds__(256, 4) void mbv2_x3_kernel(const MbX3Args a) {
   using G = MxGeom<S, TO, CINP, HIDP, COUTP, EXPAND, RES, STEM>;
   constexpr int IR = G::IR, NP = G::NP, MP = G::MP, XLD = G::XLD, XF = G::XF, EF = G::EF, ELD = G::ELD;
   constexpr int NQ = G::NQ, NDR = G::NDR, OT = G::OT, KX = G::KX;
@@ -88,10 +89,6 @@ __global__ __launch_bounds__(256) void mbv2_x3_kernel(const MbX3Args a) {
   const int tid = threadIdx.x, lane = tid & 63;
   const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
   const int tpr = a.OH / TO;
-  const int n = blockIdx.x / (tpr * tpr);
-  const int tt = blockIdx.x - n * tpr * tpr;
-  const int oy0 = (tt / tpr) * TO, ox0 = (tt - (tt / tpr) * tpr) * TO;
-  const int iy0 = oy0 * S - 1, ix0 = ox0 * S - 1;  // input tile origin (pad 1)
   const int H = a.H;
   const int l16 = lane & 15, lq = lane >> 4;
 
@@ -116,17 +113,15 @@ __global__ __launch_bounds__(256) void mbv2_x3_kernel(const MbX3Args a) {
         afl[ht][k] = *reinterpret_cast<const half8*>(a.We + a.we_lo + o);
       }
   };
-  if constexpr (EXPAND) load_af(0);
-
-  // ---- stage the block input tile (zeros outside the image and past cin)
-  if constexpr (STEM == 0) {
-    // f32 -> hi / lo planes: x - hi is exact in f32, lo = f16(x - hi)
-    constexpr int C4 = CINP / 4;
-    constexpr int NIT = (MP * C4 + 255) / 256;
+  // block input tile t (+ halo) -> registers: zeros outside the image and past cin
+  constexpr int C4 = CINP / 4;
+  constexpr int NIT = STEM == 0 ? (MP * C4 + 255) / 256 : 1;
+  auto load_in = [&](int t, float4 (&v)[NIT]) {
+    const int n = t / (tpr * tpr), tt = t - n * tpr * tpr;
+    const int iy0 = (tt / tpr) * TO * S - 1, ix0 = (tt - (tt / tpr) * tpr) * TO * S - 1;
     const float* xin = reinterpret_cast<const float*>(a.x) + (size_t)n * H * H * a.cin;
-    float4 v[NIT];
 #pragma unroll
-    for (int j = 0; j < NIT; ++j) {  // all loads first ...
+    for (int j = 0; j < NIT; ++j) {
       const int i = tid + 256 * j;
       const int p = i / C4, c4 = i - (i / C4) * C4;
       const int py = p / IR, px = p - (p / IR) * IR;
@@ -135,21 +130,49 @@ __global__ __launch_bounds__(256) void mbv2_x3_kernel(const MbX3Args a) {
       if (i < MP * C4 && p < NP && iy >= 0 && iy < H && ix >= 0 && ix < H && c4 * 4 < a.cin)
         v[j] = *reinterpret_cast<const float4*>(xin + ((size_t)iy * H + ix) * a.cin + c4 * 4);
     }
+  };
+  float4 xv[NIT];
+  if constexpr (STEM == 0)
+    if (blockIdx.x < a.ntiles) load_in(blockIdx.x, xv);
+
+  // depthwise item of this thread: output pixel dq, channels 8 dcg .. 8 dcg + 7 of the chunk
+  const int dq = tid >> 2, dcg = tid & 3;
+  const int dqy = dq / TO, dqx = dq - (dq / TO) * TO;
+  const int dp0 = (dqy * S) * IR + dqx * S;  // top-left tap of the 3x3 window
+  const float* wdsrc = G::DWL ? sWd : a.Wd;
+
+  // Tiles blockIdx.x, + gridDim.x, ...: tile t + gridDim.x's input is loaded into registers while tile
+  // t computes. No barrier is needed before the next tile's LDS stores: every wave has passed the
+  // barrier after the last chunk's depthwise (sX, sE and sXf are read before it), and the next
+  // tile's depthwise writes sD only after the barrier behind its staging, which no wave passes while
+  // another still projects.
+#pragma unroll 1
+  for (int t = blockIdx.x; t < a.ntiles; t += gridDim.x) {
+  const int n = t / (tpr * tpr);
+  const int tt = t - n * tpr * tpr;
+  const int oy0 = (tt / tpr) * TO, ox0 = (tt - (tt / tpr) * tpr) * TO;
+  const int iy0 = oy0 * S - 1, ix0 = ox0 * S - 1;  // input tile origin (pad 1)
+  if constexpr (EXPAND) load_af(0);
+
+  // ---- stage the block input tile
+  if constexpr (STEM == 0) {
+    // f32 -> hi / lo planes: x - hi is exact in f32, lo = f16(x - hi)
     bool bad = false;
 #pragma unroll
     for (int j = 0; j < NIT; ++j) {  // ... then the split and the LDS stores
       const int i = tid + 256 * j;
       const int p = i / C4, c4 = i - (i / C4) * C4;
       if (i < MP * C4) {
-        const half4 h = {(f16)v[j].x, (f16)v[j].y, (f16)v[j].z, (f16)v[j].w};
-        const half4 l = {(f16)(v[j].x - (float)h[0]), (f16)(v[j].y - (float)h[1]), (f16)(v[j].z - (float)h[2]),
-                         (f16)(v[j].w - (float)h[3])};
+        const half4 h = {(f16)xv[j].x, (f16)xv[j].y, (f16)xv[j].z, (f16)xv[j].w};
+        const half4 l = {(f16)(xv[j].x - (float)h[0]), (f16)(xv[j].y - (float)h[1]), (f16)(xv[j].z - (float)h[2]),
+                         (f16)(xv[j].w - (float)h[3])};
         *reinterpret_cast<half4*>(sXh + p * XLD + c4 * 4) = h;
         *reinterpret_cast<half4*>(sXl + p * XLD + c4 * 4) = l;
-        bad |= x3_out_of_range4(v[j]);
+        bad |= x3_out_of_range4(xv[j]);
       }
     }
     x3_raise(a.flag, bad);
+    if (t + (int)gridDim.x < a.ntiles) load_in(t + gridDim.x, xv);  // lands under this tile's MFMAs
   } else {
     // stem conv 3x3/2 pad 1 on the u8 image for stem pixel (iy, ix) of the 112x112 grid, in fp32
     const uint8_t* img = reinterpret_cast<const uint8_t*>(a.x) + (size_t)n * 224 * 224 * STEM;
@@ -200,12 +223,6 @@ __global__ __launch_bounds__(256) void mbv2_x3_kernel(const MbX3Args a) {
   floatx4 acc[OT];
 #pragma unroll
   for (int o = 0; o < OT; ++o) acc[o] = floatx4{0.f, 0.f, 0.f, 0.f};
-
-  // depthwise item of this thread: output pixel dq, channels 8 dcg .. 8 dcg + 7 of the chunk
-  const int dq = tid >> 2, dcg = tid & 3;
-  const int dqy = dq / TO, dqx = dq - (dq / TO) * TO;
-  const int dp0 = (dqy * S) * IR + dqx * S;  // top-left tap of the 3x3 window
-  const float* wdsrc = G::DWL ? sWd : a.Wd;
 
 #pragma unroll 1
   for (int h0 = 0; h0 < HIDP; h0 += MX_HC) {
@@ -347,6 +364,7 @@ __global__ __launch_bounds__(256) void mbv2_x3_kernel(const MbX3Args a) {
       }
     }
   }
+  }  // tiles
 }
 
 // f32 [n4 * 4] -> f16 hi / lo planes (the features[18] GEMM's A operand)
@@ -484,10 +502,14 @@ __global__ __launch_bounds__(256) void mbv2_dw_x3_kernel(const float* __restrict
 }
 
 template <int S, int TO, int CINP, int HIDP, int COUTP, bool EXPAND, bool RES, int STEM>
-int launch_x3_block(const MbX3Args& a, int B, hipStream_t s) {
-  const int tpr = a.OH / TO;
-  hipLaunchKernelGGL((mbv2_x3_kernel<S, TO, CINP, HIDP, COUTP, EXPAND, RES, STEM>), dim3(B * tpr * tpr), dim3(256),
-                     0, s, a);
+int launch_x3_block(const MbX3Args& a0, int B, hipStream_t s) {
+  const int tpr = a0.OH / TO;
+  MbX3Args a = a0;
+  a.ntiles = B * tpr * tpr;
+  // opt().mbv2_x3_tpw tiles per workgroup (1: one tile each, no prefetch)
+  const int tpw = std::max(1, opt().mbv2_x3_tpw);
+  hipLaunchKernelGGL((mbv2_x3_kernel<S, TO, CINP, HIDP, COUTP, EXPAND, RES, STEM>), dim3((a.ntiles + tpw - 1) / tpw),
+                     dim3(256), 0, s, a);
   MEC_LAUNCH_CHECK();
   return 0;
 }
@@ -495,7 +517,7 @@ int launch_x3_block(const MbX3Args& a, int B, hipStream_t s) {
 // The 17 block shapes of mobilenet_v2 at 224x224 (as mobilenet.hip dispatch_block)
 int dispatch_x3_block(const MbBlock& b, const MbX3Args& a, int B, int stem_c, hipStream_t s) {
   const bool res = b.stride == 1 && b.cin == b.cout;
-  // stride-2 blocks at 56 / 28 outputs: 4x4 output tiles (9x9 inputs, 40 KB of LDS, four workgroups
+  // stride-2 blocks at 56 / 28 outputs: 4x4 output tiles (9x9 inputs, 36-39 KB of LDS, four workgroups
   // per CU) when opt().mbv2_x3_tile == 4, else 8x8 / 7x7 tiles (17x17 / 15x15 inputs, one per CU)
   const int TO = (opt().mbv2_x3_tile == 4 && b.stride == 2 && a.OH % 4 == 0) ? 4 : (a.OH % 8 == 0) ? 8 : 7;
 #define MX_CASE(S_, TO_, CI_, HI_, CO_, RS_)                                                                      \

@@ -481,6 +481,25 @@ def test_mobilenet_v2_fp32x3_layered_tail_vs_oracle(dev, first):
     assert err <= PROB_TOL and ferr <= FEAT_RTOL and (probs[sub].argmax(1) == rp.argmax(1)).all()
 
 
+@pytest.mark.parametrize('B', [3, 256])
+def test_mobilenet_v2_fp32x3_tiles_per_workgroup_bit_identical(dev, B):
+    """mbv2_x3_tpw k (each fused-block workgroup walks k output tiles, the next tile's input loaded
+    while one computes; the stem block, RGB and gray, included) against one tile per workgroup: the
+    same per-tile arithmetic, so the same bits, also when k does not divide the tile count (B = 3);
+    every block fused (mbv2_layered 0) so all the fused shapes run."""
+    g = engine.to_device(syn.image_inputs(B, seed=210 + B), dev)
+    enc = engine.MobileNetImageEncoder(device=dev, precision='fp32x3')
+    enc.set_option('mbv2_layered', 0)
+    outs = {}
+    for k in (1, 3, 4):
+        enc.set_option('mbv2_x3_tpw', k)
+        outs[k] = [t.cpu() for t in enc.forward(g)]
+    enc.check()
+    for k in (3, 4):
+        for i, (a, b) in enumerate(zip(outs[1], outs[k])):
+            assert torch.equal(a, b), f'tpw {k}, output {i}: max |d| {float((a - b).abs().max())}'
+
+
 def test_mobilenet_v2_fp32x3_batch_invariance_and_entry_shapes(dev):
     """Rows of a B=64 batch equal the same rows run as B=8 bit for bit (per-tile kernels, and the
     features[18] split GEMM's interleaved tiles share one k order); the RGB and already-resized
