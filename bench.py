@@ -10,9 +10,12 @@ region ends after the last batch's gather (device synchronize).
 
 The path runs at three precisions on the same inputs; rank 0 prints ONE JSON line:
   headline  "fp32x3": the reference's fp32 arithmetic (inference/text_inference.py:91-93,
-            inference/image_inference.py:116-118) with every GEMM / conv operand carried as an
-            exact f16 hi + lo pair and each product as hi.hi + hi.lo + lo.hi on the f16 MFMA into
-            one fp32 accumulator; LayerNorm, softmax, attention, GELU, residual stream, heads,
+            inference/image_inference.py:116-118) with every GEMM / conv operand carried as a
+            pair of f16 planes (hi + lo: 22 significant bits; activations at a per-tensor
+            power-of-two plane scale fixed at handle creation, weights at a per-matrix one; a range
+            flag that check() raises if a plane leaves the f16 range: INTEGRATION.md "fp32x3
+            envelope") and each product as hi.hi + hi.lo + lo.hi on the f16 MFMA into one fp32
+            accumulator; LayerNorm, softmax, attention, GELU, residual stream, heads,
             speech and fusion in fp32 as on the exact path. Held to the fp32 path's parity bars,
             and closer to float64 than the exact-f32 MFMA engine per GEMM (its 32-deep MFMA sums
             round the accumulator 8x less often: tests/test_gpu_fp32x3.py) -- `value`;
@@ -217,16 +220,21 @@ def _oracle_chain(w, x, ids, mask, gray, sel, times=None):
     return {'speech': rs, 'text': rt, 'image': ri, 'fusion': rf}
 
 
-CPU_SAMPLE_ROWS, CPU_PASSES = 32, 3
+# cpu_baseline (BASELINE.md "CPU baseline"): the whole timed batch (up to CPU_SAMPLE_ROWS rows), median
+# of CPU_PASSES passes at the box's CPU share; the physical-core repeat is a secondary, smaller sample
+CPU_SAMPLE_ROWS, CPU_PASSES = 256, 5
+CPU_PHYS_ROWS, CPU_PHYS_PASSES = 32, 3
 
 
 def oracle_run(x, ids, mask, gray, rows, timed: bool):
     """The CPU oracle (fp32 torch-CPU / numpy restatement of the reference arithmetic) on `rows`
-    of the batch: the parity reference (one pass). timed=True also returns the cpu_baseline record
-    (BASELINE.md): the oracle chain on a bounded sample (the first CPU_SAMPLE_ROWS
-    rows of the timed batch), after a 2-row warm-up, CPU_PASSES timed passes -> median, at
-    torch threads = OMP_NUM_THREADS (the box's CPU share for one GPU: `value`) and again at the
-    physical cores in the affinity mask; per-modality rates at both."""
+    of the batch: the parity reference. timed=True also returns the cpu_baseline record (SURVEY
+    §8(d)): the oracle chain on the first CPU_SAMPLE_ROWS rows of the timed batch (all
+    256 at the headline config), after a 2-row warm-up, CPU_PASSES timed passes -> median, at torch
+    threads = OMP_NUM_THREADS (the box's CPU share for one GPU: `value`). When the sample is the
+    parity rows, the first timed pass's outputs are the parity reference (the same computation, not
+    run twice). Secondary: CPU_PHYS_PASSES passes over CPU_PHYS_ROWS rows at every physical core in
+    the affinity mask; per-modality rates at both."""
     sys.path.insert(0, ROOT)
     from mec import synthetic as syn
     threads, phys, avail, phys_mask = host_cpus()
@@ -234,38 +242,44 @@ def oracle_run(x, ids, mask, gray, rows, timed: bool):
     w = {k: syn.weights(k) for k in ('speech', 'text', 'image', 'fusion')}
     r = np.asarray(rows)
     torch.set_num_threads(threads)
-    t0 = time.perf_counter()
-    ref = _oracle_chain(w, x, ids, mask, gray, r)
-    ref_s = time.perf_counter() - t0
+    sample = np.arange(min(CPU_SAMPLE_ROWS, len(x)))
+    shared = timed and len(r) == len(sample) and np.array_equal(r, sample)
+    ref, ref_s = None, None
+    if not shared:
+        t0 = time.perf_counter()
+        ref = _oracle_chain(w, x, ids, mask, gray, r)
+        ref_s = time.perf_counter() - t0
     cb = None
     if timed:
-        sample = np.arange(min(CPU_SAMPLE_ROWS, len(x)))
-        runs = {}
-        counts = [threads] + ([phys_mask] if phys_mask and phys_mask != threads else [])
-        for nt in counts:
+        def run(nt, rows_, passes):
+            nonlocal ref, ref_s
             torch.set_num_threads(nt)
-            _oracle_chain(w, x, ids, mask, gray, sample[:2])  # warm-up
+            _oracle_chain(w, x, ids, mask, gray, rows_[:2])  # warm-up
             times = {}
-            for _ in range(CPU_PASSES):
-                _oracle_chain(w, x, ids, mask, gray, sample, times)
+            for i in range(passes):
+                out = _oracle_chain(w, x, ids, mask, gray, rows_, times)
+                if ref is None and nt == threads and i == 0:
+                    ref, ref_s = out, times['fused'][0]
             med = {k: float(np.median(v)) for k, v in times.items()}
-            runs[nt] = {'fused_samples_per_s': len(sample) / med['fused'],
-                        'per_modality_samples_per_s': {k: len(sample) / med[k] for k in ('speech', 'text', 'image', 'fusion')},
-                        'median_pass_s': med['fused'], 'passes_s': [round(v, 3) for v in times['fused']]}
-        head = runs[threads]
+            return {'rows': len(rows_), 'passes': passes, 'fused_samples_per_s': len(rows_) / med['fused'],
+                    'per_modality_samples_per_s': {k: len(rows_) / med[k] for k in ('speech', 'text', 'image', 'fusion')},
+                    'median_pass_s': med['fused'], 'passes_s': [round(v, 3) for v in times['fused']]}
+        head = run(threads, sample, CPU_PASSES)
+        physrun = None
+        if phys_mask and phys_mask != threads:
+            physrun = {'cores': phys_mask, **run(phys_mask, sample[:CPU_PHYS_ROWS], CPU_PHYS_PASSES)}
         cb = {'value': head['fused_samples_per_s'], 'unit': 'fused samples/s', 'cores': threads, 'kind': 'port',
-              'sample': f'the first {len(sample)} samples of the timed batch (L=128 full rows, 48x48 u8) through '
-                        f'oracle/ (fp32 torch-CPU restatement: speech DNN, BERT, ResNet50, fusion), 2-sample warm-up, '
-                        f'median of {CPU_PASSES} passes',
+              'sample': f'the {len(sample)} rows of the timed batch (L=128 full rows, 48x48 u8) through oracle/ '
+                        f'(fp32 torch-CPU restatement: speech DNN, BERT, ResNet50, fusion), 2-row warm-up, median of '
+                        f'{CPU_PASSES} passes' + ('; the first pass is also the parity reference' if shared else ''),
               'per_modality_samples_per_s': head['per_modality_samples_per_s'],
               'median_pass_s': head['median_pass_s'], 'passes_s': head['passes_s'],
               'threads_note': 'cores = torch threads = OMP_NUM_THREADS, the CPU share the GPU box gives one GPU; '
-                              '`at_physical_cores_in_affinity_mask` repeats the sample on every physical core '
-                              'this process may run on',
-              'at_physical_cores_in_affinity_mask': ({'cores': phys_mask, **runs[phys_mask]}
-                                                     if phys_mask in runs and phys_mask != threads else None),
+                              '`at_physical_cores_in_affinity_mask` repeats a smaller sample on every physical core '
+                              'this process may run on (secondary)',
+              'at_physical_cores_in_affinity_mask': physrun,
               'parity_pass': {'rows': len(r), 'seconds': ref_s, 'fused_samples_per_s': len(r) / ref_s,
-                              'cores': threads},
+                              'cores': threads, 'shared_with_timed_pass': shared},
               'host_physical_cores': phys, 'host_logical_cpus_in_affinity': avail,
               'host_physical_cores_in_affinity': phys_mask}
     torch.set_num_threads(prev)

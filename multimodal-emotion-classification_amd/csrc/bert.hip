@@ -32,9 +32,10 @@ __global__ __launch_bounds__(256) void bert_embed_ln_kernel(const int32_t* __res
                                                             const float* __restrict__ type,
                                                             const float* __restrict__ g,
                                                             const float* __restrict__ b, float* h32,
-                                                            f16* h16, long long lo, unsigned* flag) {
-  // lo != 0 (the fp32x3 path): h16 is a hi plane and h16 + lo the lo plane, f16(y - hi); a value
-  // outside the f16 range raises `flag` (x3_raise)
+                                                            f16* h16, long long lo, float up, unsigned* flag) {
+  // lo != 0 (the fp32x3 path): h16 is a hi plane and h16 + lo the lo plane of y up (hi = f16(y up),
+  // lo = f16(y up - hi); up = 2^s, the planes' scale); a value outside the f16 range raises `flag`
+  // (x3_raise)
   const int lane = threadIdx.x & 63;
   const int row = blockIdx.x * 4 + (threadIdx.x >> 6);
   if (row >= M) return;
@@ -71,15 +72,17 @@ __global__ __launch_bounds__(256) void bert_embed_ln_kernel(const int32_t* __res
     o.z = (v[4 * j + 2] - mean) * rstd * g[c + 2] + b[c + 2];
     o.w = (v[4 * j + 3] - mean) * rstd * g[c + 3] + b[c + 3];
     *reinterpret_cast<float4*>(h32 + (size_t)row * BH + c) = o;
-    if (h16) {  // null on the fp32 path
-      half4 hh = {(f16)o.x, (f16)o.y, (f16)o.z, (f16)o.w};
+    if (h16 && lo) {
+      const float4 u = make_float4(o.x * up, o.y * up, o.z * up, o.w * up);
+      const half4 hh = {(f16)u.x, (f16)u.y, (f16)u.z, (f16)u.w};
+      const half4 hl = {(f16)(u.x - (float)hh[0]), (f16)(u.y - (float)hh[1]), (f16)(u.z - (float)hh[2]),
+                        (f16)(u.w - (float)hh[3])};
       *reinterpret_cast<half4*>(h16 + (size_t)row * BH + c) = hh;
-      if (lo) {
-        half4 hl = {(f16)(o.x - (float)hh[0]), (f16)(o.y - (float)hh[1]), (f16)(o.z - (float)hh[2]),
-                    (f16)(o.w - (float)hh[3])};
-        *reinterpret_cast<half4*>(h16 + lo + (size_t)row * BH + c) = hl;
-        x3_raise(flag, x3_out_of_range4(o));
-      }
+      *reinterpret_cast<half4*>(h16 + lo + (size_t)row * BH + c) = hl;
+      x3_raise(flag, x3_out_of_range4(u));
+    } else if (h16) {  // f16 path (null on the fp32 path)
+      const half4 hh = {(f16)o.x, (f16)o.y, (f16)o.z, (f16)o.w};
+      *reinterpret_cast<half4*>(h16 + (size_t)row * BH + c) = hh;
     }
   }
 }
@@ -92,7 +95,7 @@ __global__ __launch_bounds__(256) void bert_layernorm_kernel(const float* x, int
                                                              const float* __restrict__ g,
                                                              const float* __restrict__ b, float* h32,
                                                              f16* h16, float2* stats, long long lo,
-                                                             unsigned* flag) {
+                                                             float up, unsigned* flag) {
   // h32 may be null: the consumer of the f32 output (the next residual add) then
   // re-derives it from x and `stats` in its GEMM epilogue (GemmParams::r_stats)
   const int lane = threadIdx.x & 63;
@@ -138,48 +141,53 @@ __global__ __launch_bounds__(256) void bert_layernorm_kernel(const float* x, int
       o.z = __builtin_fmaf((v[r][4 * j + 2] - mean) * rstd, gg[j].z, bb[j].z);
       o.w = __builtin_fmaf((v[r][4 * j + 3] - mean) * rstd, gg[j].w, bb[j].w);
       if (h32) *reinterpret_cast<float4*>(h32 + (size_t)row * BH + c) = o;
-      if (h16) {  // null on the fp32 path
-        half4 hh = {(f16)o.x, (f16)o.y, (f16)o.z, (f16)o.w};
+      if (h16 && lo) {  // fp32x3 path: planes of o up (up = 2^s, the planes' scale) and the range guard
+        const float4 u = make_float4(o.x * up, o.y * up, o.z * up, o.w * up);
+        const half4 hh = {(f16)u.x, (f16)u.y, (f16)u.z, (f16)u.w};
+        const half4 hl = {(f16)(u.x - (float)hh[0]), (f16)(u.y - (float)hh[1]), (f16)(u.z - (float)hh[2]),
+                          (f16)(u.w - (float)hh[3])};
         *reinterpret_cast<half4*>(h16 + (size_t)row * BH + c) = hh;
-        if (lo) {  // fp32x3 path: the lo plane (and the range guard)
-          half4 hl = {(f16)(o.x - (float)hh[0]), (f16)(o.y - (float)hh[1]), (f16)(o.z - (float)hh[2]),
-                      (f16)(o.w - (float)hh[3])};
-          *reinterpret_cast<half4*>(h16 + lo + (size_t)row * BH + c) = hl;
-          x3_raise(flag, x3_out_of_range4(o));
-        }
+        *reinterpret_cast<half4*>(h16 + lo + (size_t)row * BH + c) = hl;
+        x3_raise(flag, x3_out_of_range4(u));
+      } else if (h16) {  // f16 path (null on the fp32 path)
+        const half4 hh = {(f16)o.x, (f16)o.y, (f16)o.z, (f16)o.w};
+        *reinterpret_cast<half4*>(h16 + (size_t)row * BH + c) = hh;
       }
     }
   }
 }
 
 static void launch_ln_rows(const float* x, int M, const float* g, const float* b, float* h32, f16* h16, float2* st,
-                           hipStream_t s, long long lo = 0) {
+                           hipStream_t s, long long lo, float up) {
   unsigned* fl = lo ? range_flag() : nullptr;
   if (opt().bert_ln_rows == 4)
-    hipLaunchKernelGGL(bert_layernorm_kernel<4>, dim3((M + 15) / 16), dim3(256), 0, s, x, M, g, b, h32, h16, st, lo, fl);
+    hipLaunchKernelGGL(bert_layernorm_kernel<4>, dim3((M + 15) / 16), dim3(256), 0, s, x, M, g, b, h32, h16, st, lo, up,
+                       fl);
   else if (opt().bert_ln_rows == 2)
-    hipLaunchKernelGGL(bert_layernorm_kernel<2>, dim3((M + 7) / 8), dim3(256), 0, s, x, M, g, b, h32, h16, st, lo, fl);
+    hipLaunchKernelGGL(bert_layernorm_kernel<2>, dim3((M + 7) / 8), dim3(256), 0, s, x, M, g, b, h32, h16, st, lo, up,
+                       fl);
   else
-    hipLaunchKernelGGL(bert_layernorm_kernel<1>, dim3((M + 3) / 4), dim3(256), 0, s, x, M, g, b, h32, h16, st, lo, fl);
+    hipLaunchKernelGGL(bert_layernorm_kernel<1>, dim3((M + 3) / 4), dim3(256), 0, s, x, M, g, b, h32, h16, st, lo, up,
+                       fl);
 }
 
 // Host launchers (also used by the fp32 path, bert_f32.hip). One wave per token row.
 int launch_bert_embed_ln(const int32_t* ids, int M, int L, const float* emb, float* h32, f16* h16, hipStream_t s,
-                         long long lo) {
+                         long long lo, float up) {
   const float* word = emb;
   const float* pos = word + (size_t)BVOCAB * BH;
   const float* type = pos + (size_t)BMAXPOS * BH;
   const float* lng = type + 2 * BH;
   const float* lnb = lng + BH;
   hipLaunchKernelGGL(bert_embed_ln_kernel, dim3((M + 3) / 4), dim3(256), 0, s, ids, M, L, word, pos, type, lng, lnb,
-                     h32, h16, lo, lo ? range_flag() : nullptr);
+                     h32, h16, lo, up, lo ? range_flag() : nullptr);
   MEC_LAUNCH_CHECK();
   return 0;
 }
 
 int launch_bert_layernorm(const float* x, int M, const float* g, const float* b, float* h32, f16* h16, float2* stats,
-                          hipStream_t s, long long lo) {
-  launch_ln_rows(x, M, g, b, h32, h16, stats, s, lo);
+                          hipStream_t s, long long lo, float up) {
+  launch_ln_rows(x, M, g, b, h32, h16, stats, s, lo, up);
   MEC_LAUNCH_CHECK();
   return 0;
 }
@@ -374,7 +382,7 @@ __global__ __launch_bounds__(256) void bert_attention_cls_kernel(const f16* __re
 template <int CLS>
 __device__ __forceinline__ void attn_head_x3(f16* const (&sK)[2], const f16* const (&sV)[2], const float* sBias,
                                              const half8 (&qh)[4], const half8 (&ql)[4], int wave, int lane, f16* ctx,
-                                             long long clo, int b, int h) {
+                                             long long clo, int b, int h, float qks) {
   const int lr = lane & 31, lh = lane >> 5;
   floatx16 s[4];
 #pragma unroll
@@ -399,7 +407,7 @@ __device__ __forceinline__ void attn_head_x3(f16* const (&sK)[2], const f16* con
 #pragma unroll
     for (int e = 0; e < 16; ++e) {
       const int key = 32 * t + (e & 3) + 8 * (e >> 2) + 4 * lh;
-      const float v = s[t][e] * 0.125f + sBias[key];
+      const float v = s[t][e] * qks + sBias[key];  // qks = 1/8 2^-(s_q + s_k) (Q, K planes at 2^s_q, 2^s_k): exact
       s[t][e] = v;
       mx = fmaxf(mx, v);
     }
@@ -503,7 +511,7 @@ template <int CLS = 0>
 __global__ __launch_bounds__(256, 2) void bert_attention_x3_kernel(const f16* __restrict__ qkv, long long lo,
                                                                    const int32_t* __restrict__ mask,
                                                                    f16* __restrict__ ctx, long long clo,
-                                                                   const f16* __restrict__ qc, long long qclo) {
+                                                                   const f16* __restrict__ qc, long long qclo, float qks) {
   constexpr int LD = CLS ? 2 * BH : 3 * BH;  // row stride of qkv
   constexpr int KO = CLS ? 0 : BH;           // K column offset (V at KO + BH)
   __shared__ __attribute__((aligned(16))) f16 sK[2][ATT_L * BDH];
@@ -552,21 +560,21 @@ __global__ __launch_bounds__(256, 2) void bert_attention_x3_kernel(const f16* __
   if (CLS && wave != 0) return;
   f16* const sKp[2] = {sK[0], sK[1]};
   const f16* const sVp[2] = {sV[0], sV[1]};
-  attn_head_x3<CLS>(sKp, sVp, sBias, qh, ql, wave, lane, ctx, clo, b, h);
+  attn_head_x3<CLS>(sKp, sVp, sBias, qh, ql, wave, lane, ctx, clo, b, h, qks);
 }
 
 int launch_bert_attention_x3(const f16* qkv, long long lo, const int32_t* mask, f16* ctx, long long clo, int B,
-                             hipStream_t s) {
+                             float qks, hipStream_t s) {
   hipLaunchKernelGGL(bert_attention_x3_kernel<0>, dim3(B * BHEADS), dim3(256), 0, s, qkv, lo, mask, ctx, clo,
-                     nullptr, 0LL);
+                     nullptr, 0LL, qks);
   MEC_LAUNCH_CHECK();
   return 0;
 }
 
 int launch_bert_attention_x3_cls(const f16* kv, long long lo, const int32_t* mask, const f16* qc, long long qclo,
-                                 f16* ctx, long long clo, int B, hipStream_t s) {
+                                 f16* ctx, long long clo, int B, float qks, hipStream_t s) {
   hipLaunchKernelGGL(bert_attention_x3_kernel<1>, dim3(B * BHEADS), dim3(256), 0, s, kv, lo, mask, ctx, clo, qc,
-                     qclo);
+                     qclo, qks);
   MEC_LAUNCH_CHECK();
   return 0;
 }
@@ -766,7 +774,7 @@ template <int HP>
 __global__ __launch_bounds__(256 * HP, HP == 1 ? 2 : 1) void bert_qkv_attn_x3_kernel(
     const f16* __restrict__ hs, long long hlo, const f16* __restrict__ wqkv, long long wlo, float oscale,
     const float* __restrict__ bqkv, const int32_t* __restrict__ mask, f16* __restrict__ ctx, long long clo, int nseq,
-    unsigned* flag) {
+    float qks, unsigned* flag) {
   static_assert(HP == 1 || HP == 2, "heads per workgroup");
   constexpr int NW = 4 * HP, WNC = 2 * HP;             // waves; waves along N
   constexpr int QBN = 192 * HP;                        // Q | K | V columns of the HP heads
@@ -933,17 +941,18 @@ __global__ __launch_bounds__(256 * HP, HP == 1 ? 2 : 1) void bert_qkv_attn_x3_ke
   __syncthreads();
   f16* const sK[2] = {smem + (0 * HP + hh) * 2 * IMG, smem + ((0 * HP + hh) * 2 + 1) * IMG};
   const f16* const sV[2] = {smem + (1 * HP + hh) * 2 * IMG, smem + ((1 * HP + hh) * 2 + 1) * IMG};
-  attn_head_x3<0>(sK, sV, sBias, qh, ql, aw, lane, ctx, clo, b, HP * hp + hh);
+  attn_head_x3<0>(sK, sV, sBias, qh, ql, aw, lane, ctx, clo, b, HP * hp + hh, qks);
 }
 
 int launch_bert_qkv_attn_x3(const f16* hs, long long hlo, const f16* wqkv, long long wlo, float oscale,
-                            const float* bqkv, const int32_t* mask, f16* ctx, long long clo, int B, hipStream_t s) {
+                            const float* bqkv, const int32_t* mask, f16* ctx, long long clo, int B, float qks,
+                            hipStream_t s) {
   if (opt().bert_qkv_attn_x3_heads == 1)
     hipLaunchKernelGGL(bert_qkv_attn_x3_kernel<1>, dim3(B * 12), dim3(256), 0, s, hs, hlo, wqkv, wlo, oscale, bqkv,
-                       mask, ctx, clo, B, range_flag());
+                       mask, ctx, clo, B, qks, range_flag());
   else
     hipLaunchKernelGGL(bert_qkv_attn_x3_kernel<2>, dim3(B * 6), dim3(512), 0, s, hs, hlo, wqkv, wlo, oscale, bqkv,
-                       mask, ctx, clo, B, range_flag());
+                       mask, ctx, clo, B, qks, range_flag());
   MEC_LAUNCH_CHECK();
   return 0;
 }
@@ -1021,9 +1030,65 @@ int TextModel::create(const float* blob, size_t n) {
   std::copy(bc, bc + 7, pr.begin() + ho);
   MEC_TRY(upload(emb, e.data(), e.size() * sizeof(float)));
   if (prec == PREC_FP32X3) {
+    // Activation-plane exponents from rigorous bounds (activation_exp, target 2^15, so no plane can
+    // overflow): a LayerNorm output is at most sqrt(H - 1) max|gamma| + max|beta| (a zero-mean,
+    // unit-variance row of H values has no entry above sqrt(H - 1)); a projection row j of such rows is
+    // at most bound ||W_j||_1 + |b_j|, and GELU never grows it; the context is a convex combination of
+    // V rows, so it shares V's exponent. Q, K and V get one exponent each: their weight rows and
+    // biases are pre-scaled by 2^s_q | 2^s_k | 2^s_v before the split (exact), so one epilogue scale
+    // serves the whole QKV GEMM; the scores carry 2^(s_q + s_k) (qks undoes it). Every consumer's
+    // epilogue scale folds in 2^(s_out - s_in).
+    auto ln_bound = [&](const float* g, const float* b) {
+      double mg = 0.0, mb = 0.0;
+      for (int i = 0; i < BH; ++i) {
+        mg = std::max(mg, std::fabs((double)g[i]));
+        mb = std::max(mb, std::fabs((double)b[i]));
+      }
+      return std::sqrt((double)BH - 1.0) * mg + mb;
+    };
+    auto proj_bound = [&](double in, const float* W, const float* b, int N, int K) {
+      double mx = 0.0;
+      for (int j = 0; j < N; ++j) {
+        double l1 = 0.0;
+        for (int k = 0; k < K; ++k) l1 += std::fabs((double)W[(size_t)j * K + k]);
+        mx = std::max(mx, in * l1 + std::fabs((double)b[j]));
+      }
+      return mx;
+    };
+    double b_in = ln_bound(lg, lb);
+    x3_s_emb = activation_exp(b_in, kX3BoundTarget);
+    std::vector<int> s_in(BLAYERS);
+    x3_s_ln1.assign(BLAYERS, 0);
+    x3_s_ln2.assign(BLAYERS, 0);
+    x3_s_q.assign(BLAYERS, 0);
+    x3_s_k.assign(BLAYERS, 0);
+    x3_s_v.assign(BLAYERS, 0);
+    x3_s_ffn.assign(BLAYERS, 0);
+    std::vector<float> bq((size_t)2304 * BLAYERS);
+    for (int l = 0; l < BLAYERS; ++l) {
+      float* wl = w32.data() + WT_LAYER * l;
+      const float* pl = pr.data() + PRM_LAYER * l;
+      s_in[l] = l ? x3_s_ln2[l - 1] : x3_s_emb;
+      int sqkv[3];
+      for (int q = 0; q < 3; ++q)
+        sqkv[q] = activation_exp(proj_bound(b_in, wl + (size_t)q * BH * BH, pl + q * BH, BH, BH), kX3BoundTarget);
+      const double b1 = ln_bound(pl + 3072, pl + 3840);
+      x3_s_ln1[l] = activation_exp(b1, kX3BoundTarget);
+      x3_s_ffn[l] =
+          activation_exp(proj_bound(b1, wl + (size_t)2304 * BH + BH * BH, pl + 4608, BI, BH), kX3BoundTarget);
+      b_in = ln_bound(pl + 8448, pl + 9216);
+      x3_s_ln2[l] = activation_exp(b_in, kX3BoundTarget);
+      x3_s_q[l] = sqkv[0];
+      x3_s_k[l] = sqkv[1];
+      x3_s_v[l] = sqkv[2];
+      for (int q = 0; q < 3; ++q) {
+        for (size_t i = 0; i < (size_t)BH * BH; ++i) wl[(size_t)q * BH * BH + i] = std::ldexp(wl[(size_t)q * BH * BH + i], sqkv[q]);
+        for (int j = 0; j < BH; ++j) bq[(size_t)2304 * l + q * BH + j] = std::ldexp(pl[q * BH + j], sqkv[q]);
+      }
+    }
     // each GEMM's B matrix (Wqkv | Wo | Wi | Wo2 of a layer) scaled by 2^e (max |w| 2^e <= 2^14,
     // exact) and split into hi = f16(w 2^e) and lo = f16(w 2^e - hi) planes; the GEMM epilogue
-    // multiplies the accumulator by 2^-e (GemmParams::oscale)
+    // multiplies the accumulator by 2^-e and the activation-plane factors (GemmParams::oscale)
     const size_t total = WT_LAYER * BLAYERS;
     std::vector<f16> hl(2 * total);
     x3_lo = total;
@@ -1035,7 +1100,12 @@ int TextModel::create(const float* blob, size_t n) {
         x3_scale[4 * l + mtx] = split_planes(w32.data() + off, sizes[mtx], hl.data() + off, hl.data() + total + off);
         off += sizes[mtx];
       }
+      x3_scale[4 * l + 0] = std::ldexp(x3_scale[4 * l + 0], -s_in[l]);
+      x3_scale[4 * l + 1] = std::ldexp(x3_scale[4 * l + 1], -x3_s_v[l]);
+      x3_scale[4 * l + 2] = std::ldexp(x3_scale[4 * l + 2], -x3_s_ln1[l]);
+      x3_scale[4 * l + 3] = std::ldexp(x3_scale[4 * l + 3], -x3_s_ffn[l]);
     }
+    MEC_TRY(upload(x3b, bq.data(), bq.size() * sizeof(float)));
     MEC_TRY(upload(wts, hl.data(), hl.size() * sizeof(f16)));
   } else if (f32) {
     MEC_TRY(upload(wts32, w32.data(), w32.size() * sizeof(float)));
@@ -1095,7 +1165,7 @@ int TextModel::forward(const int32_t* ids, const int32_t* mask, int B, int L, fl
   const float* lnb = lng + BH;
   const dim3 rows_grid((M + 3) / 4);
   hipLaunchKernelGGL(bert_embed_ln_kernel, rows_grid, dim3(256), 0, s, ids, M, L, word, pos, type, lng, lnb, h32,
-                     h16, 0LL, nullptr);
+                     h16, 0LL, 1.f, nullptr);
   MEC_LAUNCH_CHECK();
   const f16* W = wts.as<f16>();
   const float* P = prm.as<float>();
@@ -1133,7 +1203,7 @@ int TextModel::forward(const int32_t* ids, const int32_t* mask, int B, int L, fl
       g.A = ctxc; g.B = wo; g.bias = bo; g.R = h32c; g.r_f32 = 1; g.r_stats = st2c; g.r_g = pg2; g.r_b = pg2 + BH;
       g.C32 = t32c; g.M = B; g.N = BH; g.K = BH;
       MEC_TRY(launch_gemm(g, s, &prof, TAG_NONE));
-      launch_ln_rows(t32c, B, g1, b1, nullptr, h16c, st1c, s);
+      launch_ln_rows(t32c, B, g1, b1, nullptr, h16c, st1c, s, 0, 1.f);
       MEC_LAUNCH_CHECK();
       g = GemmParams();
       g.A = h16c; g.B = wi; g.bias = bi; g.act = ACT_GELU; g.C16 = fc; g.M = B; g.N = BI; g.K = BH;
@@ -1142,7 +1212,7 @@ int TextModel::forward(const int32_t* ids, const int32_t* mask, int B, int L, fl
       g.A = fc; g.B = wo2; g.bias = bo2; g.R = t32c; g.r_f32 = 1; g.r_stats = st1c; g.r_g = g1; g.r_b = b1;
       g.C32 = h32c; g.M = B; g.N = BH; g.K = BI;
       MEC_TRY(launch_gemm(g, s, &prof, TAG_NONE));
-      launch_ln_rows(h32c, B, g2, b2, h32c, h16c, st2c, s);  // in place, written in full (the pooler's input)
+      launch_ln_rows(h32c, B, g2, b2, h32c, h16c, st2c, s, 0, 1.f);  // in place, written in full (the pooler's input)
       MEC_LAUNCH_CHECK();
       break;
     }
@@ -1180,7 +1250,7 @@ int TextModel::forward(const int32_t* ids, const int32_t* mask, int B, int L, fl
       if (!first) { g.r_stats = st2; g.r_g = pg2; g.r_b = pg2 + BH; }  // else: the embedding LN, written in full
       MEC_TRY(launch_gemm(g, s, &prof, TAG_BERT_OPROJ));
       MEC_TRY(prof.begin(TAG_BERT_LN, s));
-      launch_ln_rows(t32, M, g1, b1, nullptr, h16, st1, s);
+      launch_ln_rows(t32, M, g1, b1, nullptr, h16, st1, s, 0, 1.f);
       MEC_LAUNCH_CHECK();
       MEC_TRY(prof.end(TAG_BERT_LN, s));
     }
@@ -1194,7 +1264,7 @@ int TextModel::forward(const int32_t* ids, const int32_t* mask, int B, int L, fl
     MEC_TRY(prof.begin(TAG_BERT_LN, s));
     // the last LN's f32 output feeds the pooler / CLS feature, so it is written in full
     // (in place: each wave holds its row in registers before writing it)
-    launch_ln_rows(h32, M, g2, b2, last ? h32 : nullptr, h16, st2, s);
+    launch_ln_rows(h32, M, g2, b2, last ? h32 : nullptr, h16, st2, s, 0, 1.f);
     MEC_LAUNCH_CHECK();
     MEC_TRY(prof.end(TAG_BERT_LN, s));
   }

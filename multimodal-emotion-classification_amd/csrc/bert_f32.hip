@@ -289,7 +289,7 @@ int TextModel::forward_x3(const int32_t* ids, const int32_t* mask, int B, int L,
   const bool cls_last = opt().bert_cls_last != 0;
   const int gelu_act = opt().gelu_x3 ? ACT_GELU_F32 : ACT_GELU_EXACT;  // FFN1's erf GELU
 
-  MEC_TRY(launch_bert_embed_ln(ids, M, L, emb.as<float>(), h32, hs, s, MH));
+  MEC_TRY(launch_bert_embed_ln(ids, M, L, emb.as<float>(), h32, hs, s, MH, std::ldexp(1.0f, x3_s_emb)));
   const f16* W = wts.as<f16>();
   const float* P = prm.as<float>();
   const long long wlo = (long long)x3_lo;
@@ -300,8 +300,15 @@ int TextModel::forward_x3(const int32_t* ids, const int32_t* mask, int B, int L,
     const f16* wo2 = wi + (size_t)FF * H;
     const float* sc = x3_scale.data() + 4 * l;
     const float* pl = P + PRM_LAYER * l;
-    const float *bqkv = pl, *bo = pl + 2304, *g1 = pl + 3072, *b1 = pl + 3840, *bi = pl + 4608, *bo2 = pl + 7680,
+    const float *bo = pl + 2304, *g1 = pl + 3072, *b1 = pl + 3840, *bi = pl + 4608, *bo2 = pl + 7680,
                 *g2 = pl + 8448, *b2 = pl + 9216;
+    // activation-plane scales (TextModel::create): Q / K / V through the pre-scaled Wqkv planes and bqkv
+    // (x3b), the scores by 1/8 2^-(s_q + s_k), the LN outputs by up1 / up2, the FFN intermediate by
+    // cscale (ffs)
+    const float* bqkv = x3b.as<float>() + (size_t)2304 * l;
+    const float qks = std::ldexp(0.125f, -(x3_s_q[l] + x3_s_k[l]));
+    const float up1 = std::ldexp(1.0f, x3_s_ln1[l]), up2 = std::ldexp(1.0f, x3_s_ln2[l]);
+    const float ffs = std::ldexp(1.0f, x3_s_ffn[l]);
     GemmParams g;
     if (cls_last && l == NL - 1) {
       // [CLS]-only last layer (TextModel::forward): K / V for every token, the rest on the [CLS] rows
@@ -328,34 +335,37 @@ int TextModel::forward_x3(const int32_t* ids, const int32_t* mask, int B, int L,
       g.split = 1; g.A = hsc; g.a_lo = BHc; g.B = wqkv; g.b_lo = wlo; g.oscale = sc[0];
       g.bias = bqkv; g.C16 = qsc; g.c_lo = BHc; g.M = B; g.N = H; g.K = H;
       MEC_TRY(launch_gemm(g, s, &prof, TAG_NONE));  // Q planes of the [CLS] rows
-      MEC_TRY(launch_bert_attention_x3_cls(bigs, kvlo, mask, qsc, BHc, csc, BHc, B, s));
+      MEC_TRY(launch_bert_attention_x3_cls(bigs, kvlo, mask, qsc, BHc, csc, BHc, B, qks, s));
       g = GemmParams();
       g.split = 1; g.A = csc; g.a_lo = BHc; g.B = wo; g.b_lo = wlo; g.oscale = sc[1];
       g.bias = bo; g.R = h32c; g.r_f32 = 1; g.C32 = t32c; g.M = B; g.N = H; g.K = H;
       if (l > 0) { g.r_stats = st2c; g.r_g = pg2; g.r_b = pg2 + H; }
       MEC_TRY(launch_gemm(g, s, &prof, TAG_NONE));
-      MEC_TRY(launch_bert_layernorm(t32c, B, g1, b1, h32c, hsc, nullptr, s, BHc));
+      MEC_TRY(launch_bert_layernorm(t32c, B, g1, b1, h32c, hsc, nullptr, s, BHc, up1));
       g = GemmParams();
       g.split = 1; g.A = hsc; g.a_lo = BHc; g.B = wi; g.b_lo = wlo; g.oscale = sc[2];
-      g.bias = bi; g.act = gelu_act; g.C16 = fsc; g.c_lo = BFc; g.M = B; g.N = FF; g.K = H;
+      g.bias = bi; g.act = gelu_act; g.C16 = fsc; g.c_lo = BFc; g.cscale = ffs; g.M = B; g.N = FF; g.K = H;
       MEC_TRY(launch_gemm(g, s, &prof, TAG_NONE));
       g = GemmParams();
       g.split = 1; g.A = fsc; g.a_lo = BFc; g.B = wo2; g.b_lo = wlo; g.oscale = sc[3];
       g.bias = bo2; g.R = h32c; g.r_f32 = 1; g.C32 = t32c; g.M = B; g.N = H; g.K = FF;
       MEC_TRY(launch_gemm(g, s, &prof, TAG_NONE));
-      MEC_TRY(launch_bert_layernorm(t32c, B, g2, b2, h32c, hsc, nullptr, s, BHc));
+      MEC_TRY(launch_bert_layernorm(t32c, B, g2, b2, h32c, hsc, nullptr, s, BHc, up2));
       break;
     }
-    if (opt().bert_qkv_attn == 1 && L == 128) {  // QKV projection + attention fused: Q / K / V stay on chip
+    // QKV projection + attention fused (Q / K / V stay on chip). The fused kernel sums in the K-interleaved
+    // term order only, so with gemm_x3_order 0 (pass-major) the split GEMM + attention pair runs instead
+    // and every split product of the forward keeps one term order
+    if (opt().bert_qkv_attn == 1 && L == 128 && opt().gemm_x3_order == 1) {
       MEC_TRY(prof.begin(TAG_BERT_QKV, s));
-      MEC_TRY(launch_bert_qkv_attn_x3(hs, MH, wqkv, wlo, sc[0], bqkv, mask, cs, MH, B, s));
+      MEC_TRY(launch_bert_qkv_attn_x3(hs, MH, wqkv, wlo, sc[0], bqkv, mask, cs, MH, B, qks, s));
       MEC_TRY(prof.end(TAG_BERT_QKV, s));
     } else {
       g.split = 1; g.A = hs; g.a_lo = MH; g.B = wqkv; g.b_lo = wlo; g.oscale = sc[0];
       g.bias = bqkv; g.C16 = bigs; g.c_lo = (long long)M * 2304; g.M = M; g.N = 2304; g.K = H;
       MEC_TRY(launch_gemm(g, s, &prof, TAG_BERT_QKV));
       MEC_TRY(prof.begin(TAG_BERT_ATTN, s));
-      MEC_TRY(launch_bert_attention_x3(bigs, (long long)M * 2304, mask, cs, MH, B, s));
+      MEC_TRY(launch_bert_attention_x3(bigs, (long long)M * 2304, mask, cs, MH, B, qks, s));
       MEC_TRY(prof.end(TAG_BERT_ATTN, s));
     }
     // deferred LayerNorm (as on the f16 path): the LN kernels write the GEMM operand planes and the
@@ -371,11 +381,11 @@ int TextModel::forward_x3(const int32_t* ids, const int32_t* mask, int B, int L,
     if (!first) { g.r_stats = st2; g.r_g = pg2; g.r_b = pg2 + H; }  // else: the embedding LN, written in full
     MEC_TRY(launch_gemm(g, s, &prof, TAG_BERT_OPROJ));
     MEC_TRY(prof.begin(TAG_BERT_LN, s));
-    MEC_TRY(launch_bert_layernorm(t32, M, g1, b1, nullptr, hs, st1, s, MH));
+    MEC_TRY(launch_bert_layernorm(t32, M, g1, b1, nullptr, hs, st1, s, MH, up1));
     MEC_TRY(prof.end(TAG_BERT_LN, s));
     g = GemmParams();
     g.split = 1; g.A = hs; g.a_lo = MH; g.B = wi; g.b_lo = wlo; g.oscale = sc[2];
-    g.bias = bi; g.act = gelu_act; g.C16 = bigs; g.c_lo = MF; g.M = M; g.N = FF; g.K = H;
+    g.bias = bi; g.act = gelu_act; g.C16 = bigs; g.c_lo = MF; g.cscale = ffs; g.M = M; g.N = FF; g.K = H;
     MEC_TRY(launch_gemm(g, s, &prof, TAG_BERT_FFN1));
     g = GemmParams();
     g.split = 1; g.A = bigs; g.a_lo = MF; g.B = wo2; g.b_lo = wlo; g.oscale = sc[3];
@@ -384,7 +394,7 @@ int TextModel::forward_x3(const int32_t* ids, const int32_t* mask, int B, int L,
     MEC_TRY(launch_gemm(g, s, &prof, TAG_BERT_FFN2));
     MEC_TRY(prof.begin(TAG_BERT_LN, s));
     // the last LN's f32 output feeds the pooler, so it is written in full (in place)
-    MEC_TRY(launch_bert_layernorm(h32, M, g2, b2, last ? h32 : nullptr, hs, st2, s, MH));
+    MEC_TRY(launch_bert_layernorm(h32, M, g2, b2, last ? h32 : nullptr, hs, st2, s, MH, up2));
     MEC_TRY(prof.end(TAG_BERT_LN, s));
   }
   const float* head = P + PRM_LAYER * NL;

@@ -259,20 +259,22 @@ __device__ __forceinline__ void gemm_epilogue(const GemmParams& p, accv (&acc)[T
       }
       if (row < M && (!NOSTORE || v[0] == 1234.5f)) {
         const size_t base = (size_t)row * N + col0;
-        if (p.C16) {
+        if (p.C16 && p.c_lo) {  // split output: planes of v * cscale, the lo plane carries the rest
+          half8 h, l;
+#pragma unroll
+          for (int q = 0; q < 8; ++q) {
+            const float u = v[q] * p.cscale;
+            h[q] = (f16)u;
+            l[q] = (f16)(u - (float)h[q]);
+            x3bad |= x3_out_of_range(u);
+          }
+          *reinterpret_cast<half8*>(p.C16 + base) = h;
+          *reinterpret_cast<half8*>(p.C16 + p.c_lo + base) = l;
+        } else if (p.C16) {
           half8 h;
 #pragma unroll
           for (int q = 0; q < 8; ++q) h[q] = (f16)v[q];
           *reinterpret_cast<half8*>(p.C16 + base) = h;
-          if (p.c_lo) {  // split output: the lo plane carries v - hi
-            half8 l;
-#pragma unroll
-            for (int q = 0; q < 8; ++q) {
-              l[q] = (f16)(v[q] - (float)h[q]);
-              x3bad |= x3_out_of_range(v[q]);
-            }
-            *reinterpret_cast<half8*>(p.C16 + p.c_lo + base) = l;
-          }
         }
         if (p.C32) {
           *reinterpret_cast<float4*>(p.C32 + base) = make_float4(v[0], v[1], v[2], v[3]);

@@ -343,7 +343,10 @@ int launch_gemm_f32(const GemmParams& p, hipStream_t s, Prof* prof, int tag) {
     } else {
       id = heuristic_tile(p);
     }
-    if (!capturing) tune_cache().put(key, id);  // inside capture: untimed, so not cached
+    // inside capture the heuristic tile is untimed: not cached while the autotune family is held to one
+    // MFMA shape (gemm_f32_family 16 / 32: every tile sums in one k order, same bits), so the first
+    // eager launch still tunes; cached with both families allowed, so replay and eager bits agree
+    if (!capturing || !opt().gemm_f32_family) tune_cache().put(key, id);
     if (getenv("MEC_GEMM_TRACE"))
       fprintf(stderr, "MEC_GEMM_F32 amode=%d M=%d N=%d K=%d H=%d C=%d ks=%d stride=%d act=%d R=%d tile=%d\n", p.amode,
               p.M, p.N, p.K, p.H, p.C, p.ks, p.stride, p.act, p.R != nullptr, id);

@@ -489,20 +489,22 @@ __device__ __forceinline__ void pp_epilogue(const GemmParams& p, floatx4 (&acc)[
       act4(v);
       if (row < M && (!NOSTORE || v[0] == 1234.5f)) {
         const size_t base = (size_t)row * N + col;
-        if (p.C16) {
+        if (p.C16 && p.c_lo) {  // split output: planes of v * cscale, the lo plane carries the rest
+          half4 h, l;
+#pragma unroll
+          for (int e = 0; e < 4; ++e) {
+            const float u = v[e] * p.cscale;
+            h[e] = (f16)u;
+            l[e] = (f16)(u - (float)h[e]);
+            x3bad |= x3_out_of_range(u);
+          }
+          *reinterpret_cast<half4*>(p.C16 + base) = h;
+          *reinterpret_cast<half4*>(p.C16 + p.c_lo + base) = l;
+        } else if (p.C16) {
           half4 h;
 #pragma unroll
           for (int e = 0; e < 4; ++e) h[e] = (f16)v[e];
           *reinterpret_cast<half4*>(p.C16 + base) = h;
-          if (p.c_lo) {  // split output: the lo plane carries v - hi
-            half4 l;
-#pragma unroll
-            for (int e = 0; e < 4; ++e) {
-              l[e] = (f16)(v[e] - (float)h[e]);
-              x3bad |= x3_out_of_range(v[e]);
-            }
-            *reinterpret_cast<half4*>(p.C16 + p.c_lo + base) = l;
-          }
         }
         if (p.C32) *reinterpret_cast<float4*>(p.C32 + base) = make_float4(v[0], v[1], v[2], v[3]);
       }
@@ -990,9 +992,12 @@ int launch_gemm_glds(const GemmParams& p0, hipStream_t s, int force_bn) {
       tune_cache().put(key, bn);
     } else {
       bn = heuristic_bn(p);
-      // a launch inside graph capture cannot time tiles: it runs the heuristic tile without caching
-      // it, so the first launch outside capture still tunes the shape (same bits either way)
-      if (!capturing) tune_cache().put(key, bn);
+      // a launch inside graph capture cannot time tiles: it runs the heuristic tile. For K-interleaved
+      // split operands it does not cache it, so the first launch outside capture still tunes the shape
+      // (every 7xxxx tile sums in one k order: same bits either way); other operands cache it, since
+      // their tiles differ in MFMA shape and k order, and a graph replay and an eager launch of one
+      // shape must compute the same bits
+      if (!capturing || p.split != 2) tune_cache().put(key, bn);
     }
     if (getenv("MEC_GEMM_TRACE"))  // one line per distinct shape, at its first launch
       fprintf(stderr, "MEC_GEMM amode=%d M=%d N=%d K=%d H=%d C=%d ks=%d stride=%d act=%d R=%d r_f32=%d split=%d tile=%d\n",

@@ -285,6 +285,10 @@ struct GemmParams {
   long long a_lo = 0, b_lo = 0;
   float oscale = 1.f;
   long long c_lo = 0;  // != 0: C16 is written as a hi plane and a lo plane (C16 + c_lo): f16(v), f16(v - hi)
+  // split output's activation-plane scale (a power of two, exact): the planes carry v * cscale, v the
+  // value after the activation (C32, when also written, carries v). Chosen per tensor at handle
+  // creation so the planes' magnitudes sit where the lo plane is a normal f16 (activation_exp below)
+  float cscale = 1.f;
   unsigned* ovf = nullptr;  // split output's range flag (x3_raise); launch_gemm fills in range_flag()
   long long r_lo = 0;  // != 0: the f16 residual R is a hi plane + a lo plane at R + r_lo (R = hi + lo)
 };

@@ -30,13 +30,14 @@ struct MbX3Args {
   int H, OH, cin, cout;
   const f16* We;        // expand hi plane [HIDP][CINP]; lo plane at We + we_lo
   long long we_lo;
-  float we_scale;       // 2^-e of the expand planes
+  float x_up;           // 2^s: the block input's plane scale (the planes carry x 2^s)
+  float we_scale;       // 2^-e 2^-s: undoes the expand planes' pre-scale and the input's plane scale
   const float* be;      // [HIDP]
   const float* Wd;      // [HIDP/8][9][8]
   const float* bd;      // [HIDP]
   const f16* Wp;        // project hi plane [COUTP][HIDP]; lo plane at Wp + wp_lo
   long long wp_lo;
-  float wp_scale;
+  float wp_scale;       // 2^-e 2^-13: the project planes' pre-scale and the depthwise output's (kDwUp)
   const float* bp;      // [COUTP]
   const float* stem_w;     // [C*9][32] folded stem weights (STEM > 0)
   const float* stem_corr;  // [4][32] bias per border class (STEM > 0)
@@ -45,6 +46,10 @@ struct MbX3Args {
 };
 
 __device__ __forceinline__ float relu6x(float v) { return fminf(fmaxf(v, 0.f), 6.f); }
+
+// The depthwise output (ReLU6: in [0, 6]) is split at a fixed scale 2^13 (6 2^13 = 49152 < 65504): its
+// planes keep 22 significant bits down to 2^-16 and can never overflow
+constexpr float kDwUp = 8192.f;
 
 template <int S, int TO, int CINP, int HIDP, int COUTP, bool EXPAND, bool RES, int STEM>
 struct MxGeom {
@@ -156,19 +161,20 @@ __global__ __launch_bounds__(256, 4) void mbv2_x3_kernel(const MbX3Args a) {
 
   // ---- stage the block input tile
   if constexpr (STEM == 0) {
-    // f32 -> hi / lo planes: x - hi is exact in f32, lo = f16(x - hi)
+    // f32 x 2^s -> hi / lo planes (x_up = 2^s: exact): x 2^s - hi is exact in f32, lo = f16(x 2^s - hi)
     bool bad = false;
 #pragma unroll
     for (int j = 0; j < NIT; ++j) {  // ... then the split and the LDS stores
       const int i = tid + 256 * j;
       const int p = i / C4, c4 = i - (i / C4) * C4;
       if (i < MP * C4) {
-        const half4 h = {(f16)xv[j].x, (f16)xv[j].y, (f16)xv[j].z, (f16)xv[j].w};
-        const half4 l = {(f16)(xv[j].x - (float)h[0]), (f16)(xv[j].y - (float)h[1]), (f16)(xv[j].z - (float)h[2]),
-                         (f16)(xv[j].w - (float)h[3])};
+        const float4 u = make_float4(xv[j].x * a.x_up, xv[j].y * a.x_up, xv[j].z * a.x_up, xv[j].w * a.x_up);
+        const half4 h = {(f16)u.x, (f16)u.y, (f16)u.z, (f16)u.w};
+        const half4 l = {(f16)(u.x - (float)h[0]), (f16)(u.y - (float)h[1]), (f16)(u.z - (float)h[2]),
+                         (f16)(u.w - (float)h[3])};
         *reinterpret_cast<half4*>(sXh + p * XLD + c4 * 4) = h;
         *reinterpret_cast<half4*>(sXl + p * XLD + c4 * 4) = l;
-        bad |= x3_out_of_range4(xv[j]);
+        bad |= x3_out_of_range4(u);
       }
     }
     x3_raise(a.flag, bad);
@@ -308,7 +314,7 @@ __global__ __launch_bounds__(256, 4) void mbv2_x3_kernel(const MbX3Args a) {
           }
 #pragma unroll
         for (int j = 0; j < 8; ++j) {
-          const float v = relu6x(d[j]);  // in [0, 6]: always inside the f16 range
+          const float v = relu6x(d[j]) * kDwUp;  // in [0, 6 2^13]: always inside the f16 range
           oh[j] = (f16)v;
           ol[j] = (f16)(v - (float)oh[j]);
         }
@@ -367,12 +373,13 @@ __global__ __launch_bounds__(256, 4) void mbv2_x3_kernel(const MbX3Args a) {
   }  // tiles
 }
 
-// f32 [n4 * 4] -> f16 hi / lo planes (the features[18] GEMM's A operand)
-__global__ __launch_bounds__(256) void mbv2_split_kernel(const float* __restrict__ x, size_t n4, f16* __restrict__ hi,
-                                                         long long lo, unsigned* flag) {
+// f32 [n4 * 4] -> f16 hi / lo planes of x up (up = 2^s, exact; the features[18] GEMM's A operand)
+__global__ __launch_bounds__(256) void mbv2_split_kernel(const float* __restrict__ x, size_t n4, float up,
+                                                         f16* __restrict__ hi, long long lo, unsigned* flag) {
   const size_t i = (size_t)blockIdx.x * 256 + threadIdx.x;
   if (i >= n4) return;
-  const float4 v = reinterpret_cast<const float4*>(x)[i];
+  float4 v = reinterpret_cast<const float4*>(x)[i];
+  v.x *= up; v.y *= up; v.z *= up; v.w *= up;
   const half4 h = {(f16)v.x, (f16)v.y, (f16)v.z, (f16)v.w};
   const half4 l = {(f16)(v.x - (float)h[0]), (f16)(v.y - (float)h[1]), (f16)(v.z - (float)h[2]),
                    (f16)(v.w - (float)h[3])};
@@ -381,16 +388,18 @@ __global__ __launch_bounds__(256) void mbv2_split_kernel(const float* __restrict
   x3_raise(flag, x3_out_of_range4(v));
 }
 
-// f32 [rows][cin] -> f16 hi / lo planes [rows][ld] (lo at + lo), channels cin .. ld-1 zero: the first
-// layered block's input
+// f32 [rows][cin] -> f16 hi / lo planes [rows][ld] of x up (up = 2^s; lo at + lo), channels cin .. ld-1
+// zero: the first layered block's input
 __global__ __launch_bounds__(256) void mbv2_split_pad_kernel(const float* __restrict__ x, size_t rows, int cin, int ld,
-                                                             f16* __restrict__ hi, long long lo, unsigned* flag) {
+                                                             float up, f16* __restrict__ hi, long long lo,
+                                                             unsigned* flag) {
   const size_t i = (size_t)blockIdx.x * 256 + threadIdx.x;  // one 4-channel group of one row
   const int G = ld / 4;
   if (i >= rows * G) return;
   const size_t r = i / G;
   const int c = (int)(i - r * G) * 4;
-  const float4 v = c < cin ? *reinterpret_cast<const float4*>(x + r * cin + c) : make_float4(0.f, 0.f, 0.f, 0.f);
+  float4 v = c < cin ? *reinterpret_cast<const float4*>(x + r * cin + c) : make_float4(0.f, 0.f, 0.f, 0.f);
+  v.x *= up; v.y *= up; v.z *= up; v.w *= up;
   const half4 h = {(f16)v.x, (f16)v.y, (f16)v.z, (f16)v.w};
   const half4 l = {(f16)(v.x - (float)h[0]), (f16)(v.y - (float)h[1]), (f16)(v.z - (float)h[2]),
                    (f16)(v.w - (float)h[3])};
@@ -400,7 +409,7 @@ __global__ __launch_bounds__(256) void mbv2_split_pad_kernel(const float* __rest
 }
 
 // Depthwise 3x3/S (pad 1) + BN shift + ReLU6 of a layered block: E f32 NHWC [B,H,H,C] (the expand GEMM's
-// ReLU6 output) -> D hi / lo planes NHWC [B,OH,OH,C] (lo at D + dlo), the project GEMM's A operand. A
+// ReLU6 output) -> hi / lo planes of D 2^13 (kDwUp) NHWC [B,OH,OH,C] (lo at D + dlo), the project GEMM's A operand. A
 // thread owns one output row of one 8-channel group: its 72 tap weights and a 3-row x 3-column window
 // of input pixels stay in registers while it walks the row, so each input pixel is loaded about 3 / S
 // times instead of 9 (consecutive threads take consecutive channel groups: every load is part of a
@@ -482,7 +491,7 @@ __global__ __launch_bounds__(256) void mbv2_dw_x3_kernel(const float* __restrict
     half8 oh, ol;
 #pragma unroll
     for (int j = 0; j < 8; ++j) {
-      const float v = relu6x(d[j]);  // in [0, 6]: inside the f16 range
+      const float v = relu6x(d[j]) * kDwUp;  // in [0, 6 2^13]: inside the f16 range
       oh[j] = (f16)v;
       ol[j] = (f16)(v - (float)oh[j]);
     }
@@ -557,6 +566,7 @@ int MobileNetModel::create_x3(const float* blob, size_t n) {
   std::vector<float> w, pr;
   auto align4 = [&]() { while (pr.size() % 4) pr.push_back(0.f); };
   auto pad_to = [](int v, int m) { return (v + m - 1) / m * m; };
+  double est = 0.0;  // the last BN's output estimate, max_c |beta_c| + 6 |gamma_c| (activation_exp)
   auto bn_scale_shift = [&](int c, std::vector<double>& scale, std::vector<double>& shift) {
     const float* g = rd.take(c);
     const float* b = rd.take(c);
@@ -564,10 +574,12 @@ int MobileNetModel::create_x3(const float* blob, size_t n) {
     const float* rv = rd.take(c);
     scale.assign(c, 0.0);
     shift.assign(c, 0.0);
+    est = 0.0;
     if (!rd.ok) return;
     for (int i = 0; i < c; ++i) {
       scale[i] = (double)g[i] / std::sqrt((double)rv[i] + 1e-5);
       shift[i] = (double)b[i] - (double)rm[i] * scale[i];
+      est = std::max(est, std::fabs((double)b[i]) + 6.0 * std::fabs((double)g[i]));
     }
   };
   std::vector<double> sc, sh;
@@ -650,6 +662,7 @@ int MobileNetModel::create_x3(const float* blob, size_t n) {
       {
         const float* wp = rd.take((size_t)b.cout * b.hid);
         bn_scale_shift(b.cout, sc, sh);
+        b.x3_est = est;
         b.wp_off = w.size();
         w.resize(w.size() + (size_t)b.coutp * b.hidp, 0.f);
         align4();
@@ -712,17 +725,49 @@ int MobileNetModel::create_x3(const float* blob, size_t n) {
     for (int j = 0; j < 7; ++j) pr[fc2_off + (size_t)i * 7 + j] = f2w[(size_t)j * 512 + i];
   fc2b_off = pr.size();
   pr.insert(pr.end(), f2b, f2b + 7);
+  // Activation-plane exponents (activation_exp, BN estimates): one per stage (a (t, c, n, s) setting:
+  // its first block is the only one without a residual, so a stage's outputs -- a residual block's output
+  // and its input -- share it), the stage estimate being the running sum of the projection BN estimates
+  // along the residual chain. Block inputs are the previous stage's planes; the depthwise outputs are at
+  // kDwUp. Every epilogue scale below folds in 2^(s_out - s_in) (the fused blocks' and the expand GEMMs'
+  // outputs are f32: s_out = 0 there).
+  {
+    int s_prev = 0;
+    for (size_t b0 = 0; b0 < blocks.size();) {
+      size_t b1 = b0 + 1;
+      while (b1 < blocks.size() && blocks[b1].stride == 1 && blocks[b1].cin == blocks[b1].cout) ++b1;
+      double e = 0.0, e_max = 0.0;
+      for (size_t i = b0; i < b1; ++i) {
+        e = blocks[i].x3_est + (i > b0 ? e : 0.0);
+        e_max = std::max(e_max, e);
+      }
+      const int st = activation_exp(e_max, kX3EstimateTarget);
+      for (size_t i = b0; i < b1; ++i) {
+        blocks[i].x3_s_in = i == b0 ? s_prev : st;
+        blocks[i].x3_s_out = st;
+      }
+      s_prev = st;
+      b0 = b1;
+    }
+  }
+  for (MbBlock& b : blocks)
+    if (b.lwe_off) {
+      align4();
+      b.lbp_x3_off = pr.size();
+      for (int o = 0; o < b.lcoutp; ++o) pr.push_back(std::ldexp(pr[b.lbp_off + o], b.x3_s_out));
+    }
   // split every 1x1 matrix: hi planes at the f32 offsets, lo planes x3_lo halfs later
   x3_lo = w.size();
   std::vector<f16> hl(2 * w.size(), (f16)0.f);
   auto split = [&](size_t off, size_t cnt) { return split_planes(w.data() + off, cnt, hl.data() + off, hl.data() + x3_lo + off); };
+  const int dw_s = (int)std::log2(kDwUp);
   for (MbBlock& b : blocks) {
-    x3_scale.push_back(b.t != 1 ? split(b.we_off, (size_t)b.hidp * b.cinp) : 1.f);
-    x3_scale.push_back(split(b.wp_off, (size_t)b.coutp * b.hidp));
-    lx3_scale.push_back(b.lwe_off ? split(b.lwe_off, (size_t)b.hidp * b.lcinp) : 1.f);
-    lx3_scale.push_back(b.lwe_off ? split(b.lwp_off, (size_t)b.lcoutp * b.hidp) : 1.f);
+    x3_scale.push_back(b.t != 1 ? std::ldexp(split(b.we_off, (size_t)b.hidp * b.cinp), -b.x3_s_in) : 1.f);
+    x3_scale.push_back(std::ldexp(split(b.wp_off, (size_t)b.coutp * b.hidp), -dw_s));
+    lx3_scale.push_back(b.lwe_off ? std::ldexp(split(b.lwe_off, (size_t)b.hidp * b.lcinp), -b.x3_s_in) : 1.f);
+    lx3_scale.push_back(b.lwe_off ? std::ldexp(split(b.lwp_off, (size_t)b.lcoutp * b.hidp), b.x3_s_out - dw_s) : 1.f);
   }
-  x3_scale.push_back(split(last_w_off, (size_t)1280 * 320));
+  x3_scale.push_back(std::ldexp(split(last_w_off, (size_t)1280 * 320), -blocks.back().x3_s_out));
   MEC_TRY(upload(wts, hl.data(), hl.size() * sizeof(f16)));
   MEC_TRY(upload(prm, pr.data(), pr.size() * sizeof(float)));
   return 0;
@@ -795,7 +840,8 @@ int MobileNetModel::forward_x3(const uint8_t* img, int B, int H, int W, int C, f
       if (i == l0) {  // the fused blocks' f32 output -> planes with the layered row stride
         const size_t rows = (size_t)B * h * h, items = rows * (b.lcinp / 4);
         hipLaunchKernelGGL(mbv2_split_pad_kernel, dim3((unsigned)((items + 255) / 256)), dim3(256), 0, s,
-                           reinterpret_cast<const float*>(cur), rows, b.cin, b.lcinp, pin, plo, range_flag());
+                           reinterpret_cast<const float*>(cur), rows, b.cin, b.lcinp, std::ldexp(1.0f, b.x3_s_in), pin,
+                           plo, range_flag());
         MEC_LAUNCH_CHECK();
       }
       f16* pout = pin == P0 ? P1 : P0;
@@ -812,9 +858,9 @@ int MobileNetModel::forward_x3(const uint8_t* img, int B, int H, int W, int C, f
         hipLaunchKernelGGL(mbv2_dw_x3_kernel<1>, dim3((unsigned)((items + 255) / 256)), dim3(256), 0, s, Eb, h, oh,
                            b.hidp, P + b.wd_off, P + b.bd_off, Db, dlo, items);
       MEC_LAUNCH_CHECK();
-      g = GemmParams();  // project: Y = Wp D 2^-e + bp (+ the block input's planes), hi / lo planes
+      g = GemmParams();  // project: Y 2^s = Wp D 2^-e 2^(s - 13) + bp 2^s (+ the block input's planes), hi / lo planes
       g.split = 1; g.A = Db; g.a_lo = dlo; g.B = Wt + b.lwp_off; g.b_lo = wlo; g.oscale = lx3_scale[2 * i + 1];
-      g.bias = P + b.lbp_off; g.act = ACT_NONE; g.C16 = pout; g.c_lo = plo;
+      g.bias = P + b.lbp_x3_off; g.act = ACT_NONE; g.C16 = pout; g.c_lo = plo;
       if (b.stride == 1 && b.cin == b.cout) {
         g.R = pin;
         g.r_lo = plo;
@@ -828,7 +874,7 @@ int MobileNetModel::forward_x3(const uint8_t* img, int B, int H, int W, int C, f
     MbX3Args a;
     a.x = cur; a.y = out; a.H = h; a.OH = b.stride == 2 ? h / 2 : h;
     a.cin = b.cin; a.cout = b.cout;
-    a.We = Wt + b.we_off; a.we_lo = wlo; a.we_scale = x3_scale[2 * i];
+    a.We = Wt + b.we_off; a.we_lo = wlo; a.we_scale = x3_scale[2 * i]; a.x_up = std::ldexp(1.0f, b.x3_s_in);
     a.be = P + b.be_off; a.Wd = P + b.wd_off; a.bd = P + b.bd_off;
     a.Wp = Wt + b.wp_off; a.wp_lo = wlo; a.wp_scale = x3_scale[2 * i + 1];
     a.bp = P + b.bp_off;
@@ -850,7 +896,8 @@ int MobileNetModel::forward_x3(const uint8_t* img, int B, int H, int W, int C, f
       llo = plo;
     } else {
       hipLaunchKernelGGL(mbv2_split_kernel, dim3((unsigned)((n4 + 255) / 256)), dim3(256), 0, s,
-                         reinterpret_cast<const float*>(cur), n4, Lin, llo, range_flag());
+                         reinterpret_cast<const float*>(cur), n4, std::ldexp(1.0f, blocks.back().x3_s_out), Lin, llo,
+                         range_flag());
       MEC_LAUNCH_CHECK();
     }
     GemmParams g;

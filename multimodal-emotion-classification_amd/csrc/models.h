@@ -99,34 +99,57 @@ struct TextModel : Model {
   // (4 per layer) the epilogue scale 2^-e of its planes
   size_t x3_lo = 0;
   std::vector<float> x3_scale;
+  // activation-plane exponents (activation_exp, rigorous bounds): the embedding LN's, per layer LN1's,
+  // LN2's, Q's, K's, V's (= the context's) and the FFN intermediate's; x3b: bq 2^s_q | bk 2^s_k | bv 2^s_v
+  // per layer (the Wqkv planes carry the same factors). The epilogue scales in x3_scale already fold them
+  // in (2^-e 2^(s_out - s_in))
+  int x3_s_emb = 0;
+  std::vector<int> x3_s_ln1, x3_s_ln2, x3_s_q, x3_s_k, x3_s_v, x3_s_ffn;
+  DevBuf x3b;
   int forward_x3(const int32_t* ids, const int32_t* mask, int B, int L, float* cls, float* logits,
                  float* probs, hipStream_t s);  // bert_f32.hip
 };
 // lo != 0 (fp32x3 path): h16 is written as a hi plane and h16 + lo as the lo plane f16(y - hi)
+// (planes of y up: up = 2^s, the planes' activation scale, activation_exp)
 int launch_bert_embed_ln(const int32_t* ids, int M, int L, const float* emb, float* h32, f16* h16, hipStream_t s,
-                         long long lo = 0);
+                         long long lo = 0, float up = 1.f);
 int launch_bert_layernorm(const float* x, int M, const float* g, const float* b, float* h32, f16* h16, float2* stats,
-                          hipStream_t s, long long lo = 0);
-// fp32x3 attention (bert.hip): Q|K|V as f16 hi / lo planes [B*128, 2304] (lo at qkv + lo), ctx
-// written as hi / lo planes [B*128, 768] (lo at ctx + clo)
+                          hipStream_t s, long long lo = 0, float up = 1.f);
+// fp32x3 attention (bert.hip): Q|K|V as f16 hi / lo planes [B*128, 2304] (lo at qkv + lo) of q 2^s_q,
+// k 2^s_k, v 2^s_v; ctx 2^s_v written as hi / lo planes [B*128, 768] (lo at ctx + clo); qks = 1/8
+// 2^-(s_q + s_k) (the scores' scale)
 int launch_bert_attention_x3(const f16* qkv, long long lo, const int32_t* mask, f16* ctx, long long clo, int B,
-                             hipStream_t s);
+                             float qks, hipStream_t s);
 // its [CLS]-only form (bert_cls_last): K | V planes [B*128, 1536] (lo at kv + lo), the [CLS] query
 // planes [B, 768] (lo at qc + qclo), the [CLS] context planes [B, 768] (lo at ctx + clo)
 int launch_bert_attention_x3_cls(const f16* kv, long long lo, const int32_t* mask, const f16* qc, long long qclo,
-                                 f16* ctx, long long clo, int B, hipStream_t s);
+                                 f16* ctx, long long clo, int B, float qks, hipStream_t s);
 
 // fp32x3 QKV projection + attention of one (sequence, head pair) per workgroup (bert.hip, L = 128):
 // h planes [B*128, 768] (lo at hs + hlo), Wqkv planes (lo at wqkv + wlo, epilogue scale oscale) ->
 // ctx planes [B*128, 768] (lo at ctx + clo); Q / K / V never reach HBM
 int launch_bert_qkv_attn_x3(const f16* hs, long long hlo, const f16* wqkv, long long wlo, float oscale,
-                            const float* bqkv, const int32_t* mask, f16* ctx, long long clo, int B, hipStream_t s);
+                            const float* bqkv, const int32_t* mask, f16* ctx, long long clo, int B, float qks,
+                            hipStream_t s);
 
 // Split n fp32 weights into f16 planes for the fp32x3 path: hi = f16(w 2^e), lo = f16(w 2^e - hi)
 // with e the largest power of two keeping max |w| 2^e <= 2^14 (so hi never overflows and lo
 // stays out of the f16 subnormals for all but the smallest weights); returns 2^-e, the GEMM
 // epilogue's oscale. Host code (runtime.hip).
 float split_planes(const float* w, size_t n, f16* hi, f16* lo);
+
+// fp32x3 activation planes. An activation x is carried as hi = f16(x 2^s), lo = f16(x 2^s - hi)
+// with s fixed per tensor at handle creation; its consumer folds 2^-s into its epilogue scale (exact).
+// The lo plane is a normal f16 -- 22 significant bits -- while |x 2^s| >= 2^-3, and hi stays finite
+// while |x 2^s| < 65520. activation_exp(bound, target) = the largest s with bound 2^s <= target:
+//   * a rigorous bound (BERT: LayerNorm outputs, |y| <= sqrt(H - 1) max|gamma| + max|beta|, and the
+//     projections of such rows, max_j (bound ||W_j||_1 + |b_j|)) with target 2^15: never overflows;
+//   * a BatchNorm estimate (ResNet50 / MobileNetV2: max_c |beta_c| + 6 |gamma_c| per BN output, summed
+//     along residual paths) with target 2^10: 64x headroom to the f16 range over that estimate, and
+//     the estimate's typical values near 2^7, far above the 2^-3 floor.
+// Clamped to [-40, 40]; 0 for a zero or non-finite bound. Host code (runtime.hip).
+int activation_exp(double bound, double target);
+constexpr double kX3BoundTarget = 32768.0, kX3EstimateTarget = 1024.0;
 
 // ---------------------------------------------------------------- image encoders
 // Both backbones take the same u8 inputs and produce the same (512-d feature, logits, probs).
@@ -144,10 +167,17 @@ struct ConvLayer {
   size_t w_off = 0;   // f16 [Cout][kh][kw][Cin] (BN scale folded)
   size_t b_off = 0;   // f32 [Cout] (BN shift)
   int cin = 0, cout = 0, ks = 1, stride = 1, pad = 0;
-  float x3_scale = 1.f;  // fp32x3 path: the epilogue scale 2^-e of this conv's weight planes
+  // fp32x3 path: the epilogue scale 2^-e 2^(x3_s - s_in) (weight planes' pre-scale, activation-plane
+  // scales of output and input), the BN output estimate, the output planes' exponent x3_s, and the BN
+  // shift times 2^x3_s (at x3b_off in prm)
+  float x3_scale = 1.f;
+  double x3_est = 0.0;
+  int x3_s = 0;
+  size_t x3b_off = 0;
 };
 struct Bottleneck {
-  ConvLayer c1, c2, c3, ds;
+  ConvLayer c1, c2, c3, ds;  // fp32x3: c3.x3_s = the stage's residual-stream exponent (the block output)
+  int x3_s_in = 0;           // fp32x3: the block input planes' exponent
   bool has_ds = false;
   size_t c3ds_w_off = 0, c3ds_b_off = 0;  // block 0: [conv3 | downsample] weights [4w][w+cin], summed bias
   float c3ds_x3_scale = 1.f;              // fp32x3 path: its planes' scale (in wts_dual) and lo offset
@@ -177,6 +207,7 @@ struct ImageModel : ImageNet {
   // planes at x3_lo halfs (w_off indexes both); the stem, pooling and head run as on the fp32 path
   size_t x3_lo = 0;
   float stem_x3_up = 1.f;  // 2^e: the gray stem's weight pre-scale (stem.x3_scale = 2^-e)
+  int x3_s_out = 0;        // the last stage's activation-plane exponent (undone by the average pool)
   DevBuf wts_dual;  // fp32x3: block 0's [conv3 | downsample] hi / lo planes (c3ds_w_off, c3ds_x3_lo)
   int forward_x3(const uint8_t* img, int B, int H, int W, int C, float* feat, float* logits, float* probs,
                  hipStream_t s);
@@ -194,6 +225,12 @@ struct MbBlock {
   // to 64, lcinp = the previous block's lcoutp), project bias [lcoutp]
   int lcinp = 0, lcoutp = 0;
   size_t lwe_off = 0, lwp_off = 0, lbp_off = 0;
+  // fp32x3 activation planes (activation_exp, BN estimates): the block input's and output's exponents
+  // (a stage's outputs share one, as a residual block's output and input must), the project BN
+  // estimate, and the layered project bias times 2^x3_s_out (lbp_x3_off)
+  int x3_s_in = 0, x3_s_out = 0;
+  double x3_est = 0.0;
+  size_t lbp_x3_off = 0;
 };
 struct MobileNetModel : ImageNet {
   DevBuf wts;   // f16 1x1 weights

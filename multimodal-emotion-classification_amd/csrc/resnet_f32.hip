@@ -363,6 +363,8 @@ int ImageModel::create_f32(const float* blob, size_t n) {
   BlobReader rd(blob, n);
   std::vector<float> w;
   std::vector<float> pr;
+  // BN output estimate (fp32x3 activation planes, activation_exp): max_c |beta_c| + 6 |gamma_c|
+  double est = 0.0;
   auto bn_fold = [&](int c, std::vector<float>& scale) {
     const float* g = rd.take(c);
     const float* b = rd.take(c);
@@ -370,10 +372,12 @@ int ImageModel::create_f32(const float* blob, size_t n) {
     const float* rv = rd.take(c);
     scale.resize(c);
     const size_t off = pr.size();
+    est = 0.0;
     for (int i = 0; i < c; ++i) {
       const double sc = (double)g[i] / std::sqrt((double)rv[i] + 1e-5);
       scale[i] = (float)sc;
       pr.push_back((float)((double)b[i] - (double)rm[i] * sc));
+      est = std::max(est, std::fabs((double)b[i]) + 6.0 * std::fabs((double)g[i]));
     }
     return off;
   };
@@ -383,6 +387,7 @@ int ImageModel::create_f32(const float* blob, size_t n) {
     const float* src = rd.take((size_t)cout * cin * ks * ks);
     std::vector<float> scale;
     L.b_off = bn_fold(cout, scale);
+    L.x3_est = est;
     L.w_off = w.size();
     w.resize(w.size() + (size_t)cout * cin * ks * ks);
     if (!rd.ok) return L;
@@ -398,6 +403,7 @@ int ImageModel::create_f32(const float* blob, size_t n) {
     const float* src = rd.take((size_t)64 * 3 * 49);
     std::vector<float> scale;
     stem.b_off = bn_fold(64, scale);
+    stem.x3_est = est;
     stem.cin = 3; stem.cout = 64; stem.ks = 7; stem.stride = 2; stem.pad = 3;
     stem.w_off = w.size();
     w.resize(w.size() + (size_t)64 * STEM_K, 0.f);
@@ -474,35 +480,77 @@ int ImageModel::create_f32(const float* blob, size_t n) {
       stem_x3_up = std::ldexp(1.0f, e);
       stem.x3_scale = std::ldexp(1.0f, -e);
     }
-    auto split = [&](ConvLayer& L) {
+    // Activation-plane scales (activation_exp, BN estimates): the stem output, each block's conv1 /
+    // conv2 outputs, and one scale per stage for the residual stream (a block's output and its
+    // identity input share it). A conv's planes then carry y 2^s_out for input planes x 2^s_in: its
+    // epilogue scale becomes 2^-e 2^(s_out - s_in) and its BN shift b 2^s_out (ReLU and the residual
+    // add commute with the power of two: the f32 values are the unscaled ones times 2^s_out exactly).
+    // The downsample of a stage's first block reads the block input (s_in) beside conv3's T2 (s_t2)
+    // in one dual GEMM: its weights are pre-scaled by 2^(s_t2 - s_in) so both halves of K carry 2^s_t2.
+    stem.x3_s = activation_exp(stem.x3_est, kX3EstimateTarget);
+    {
+      int s_prev = stem.x3_s;
+      double e_stream = stem.x3_est;
+      for (size_t b0 = 0; b0 < blocks.size();) {
+        size_t b1 = b0 + 1;
+        while (b1 < blocks.size() && !blocks[b1].has_ds) ++b1;  // [b0, b1): one stage
+        double e_max = 0.0;
+        for (size_t bi = b0; bi < b1; ++bi) {
+          Bottleneck& bk = blocks[bi];
+          e_stream = bk.c3.x3_est + (bk.has_ds ? bk.ds.x3_est : e_stream);
+          e_max = std::max(e_max, e_stream);
+        }
+        const int s_stage = activation_exp(e_max, kX3EstimateTarget);
+        for (size_t bi = b0; bi < b1; ++bi) {
+          Bottleneck& bk = blocks[bi];
+          bk.c1.x3_s = activation_exp(bk.c1.x3_est, kX3EstimateTarget);
+          bk.c2.x3_s = activation_exp(bk.c2.x3_est, kX3EstimateTarget);
+          bk.c3.x3_s = s_stage;
+          bk.x3_s_in = bi == b0 ? s_prev : s_stage;
+        }
+        s_prev = s_stage;
+        b0 = b1;
+      }
+      x3_s_out = s_prev;
+    }
+    auto scaled_bias = [&](size_t b_off, int cout, int s) {
+      const size_t off = pr.size();
+      for (int o = 0; o < cout; ++o) pr.push_back(std::ldexp(pr[b_off + o], s));
+      return off;
+    };
+    stem.x3b_off = scaled_bias(stem.b_off, 64, stem.x3_s);
+    auto split = [&](ConvLayer& L, int s_in) {
       const size_t cnt = (size_t)L.cout * L.cin * L.ks * L.ks;
-      L.x3_scale = split_planes(w.data() + L.w_off, cnt, hl.data() + L.w_off, hl.data() + x3_lo + L.w_off);
+      L.x3_scale = std::ldexp(split_planes(w.data() + L.w_off, cnt, hl.data() + L.w_off, hl.data() + x3_lo + L.w_off),
+                              L.x3_s - s_in);
+      L.x3b_off = scaled_bias(L.b_off, L.cout, L.x3_s);
     };
     for (Bottleneck& bk : blocks) {
-      split(bk.c1);
-      split(bk.c2);
-      split(bk.c3);
-      if (bk.has_ds) split(bk.ds);
+      split(bk.c1, bk.x3_s_in);
+      split(bk.c2, bk.c1.x3_s);
+      split(bk.c3, bk.c2.x3_s);
     }
     // block 0 of each stage: conv3 and the downsample as ONE dual-source GEMM over K = [w | cin]
-    // (the f16 path's A_DUAL), weights [W3 | Wds] split with one scale, bias b3 + bds
+    // (the f16 path's A_DUAL), weights [W3 | Wds 2^(s_t2 - s_in)] split with one scale, bias b3 + bds
     std::vector<float> cat;
     std::vector<f16> hl2;
     for (Bottleneck& bk : blocks) {
       if (!bk.has_ds) continue;
       const int wd = bk.c3.cin, cin = bk.ds.cin, Kt = wd + cin, No = bk.c3.cout;
+      const int dsh = bk.c2.x3_s - bk.x3_s_in;
       cat.assign((size_t)No * Kt, 0.f);
       for (int o = 0; o < No; ++o) {
         for (int k = 0; k < wd; ++k) cat[(size_t)o * Kt + k] = w[bk.c3.w_off + (size_t)o * wd + k];
-        for (int k = 0; k < cin; ++k) cat[(size_t)o * Kt + wd + k] = w[bk.ds.w_off + (size_t)o * cin + k];
+        for (int k = 0; k < cin; ++k) cat[(size_t)o * Kt + wd + k] = std::ldexp(w[bk.ds.w_off + (size_t)o * cin + k], dsh);
       }
       bk.c3ds_w_off = hl2.size();
       hl2.resize(hl2.size() + 2 * cat.size());
-      bk.c3ds_x3_scale = split_planes(cat.data(), cat.size(), hl2.data() + bk.c3ds_w_off,
-                                      hl2.data() + bk.c3ds_w_off + cat.size());
+      bk.c3ds_x3_scale = std::ldexp(split_planes(cat.data(), cat.size(), hl2.data() + bk.c3ds_w_off,
+                                                 hl2.data() + bk.c3ds_w_off + cat.size()),
+                                    bk.c3.x3_s - bk.c2.x3_s);
       bk.c3ds_x3_lo = cat.size();
       bk.c3ds_b_off = pr.size();
-      for (int o = 0; o < No; ++o) pr.push_back(pr[bk.c3.b_off + o] + pr[bk.ds.b_off + o]);
+      for (int o = 0; o < No; ++o) pr.push_back(std::ldexp(pr[bk.c3.b_off + o] + pr[bk.ds.b_off + o], bk.c3.x3_s));
     }
     MEC_TRY(upload(wts, hl.data(), hl.size() * sizeof(f16)));
     MEC_TRY(upload(wts_dual, hl2.data(), hl2.size() * sizeof(f16)));
@@ -511,12 +559,13 @@ int ImageModel::create_f32(const float* blob, size_t n) {
   return 0;
 }
 
-// fp32 tensor -> f16 hi / lo planes (the fp32x3 path's stem output): hi = f16(x), lo = f16(x - hi)
-__global__ __launch_bounds__(256) void split_f32_kernel(const float* __restrict__ x, size_t n4, f16* __restrict__ hi,
-                                                        long long lo, unsigned* flag) {
+// fp32 tensor -> f16 hi / lo planes (the fp32x3 path's stem output): hi = f16(x up), lo = f16(x up - hi)
+__global__ __launch_bounds__(256) void split_f32_kernel(const float* __restrict__ x, size_t n4, float up,
+                                                        f16* __restrict__ hi, long long lo, unsigned* flag) {
   const size_t i = (size_t)blockIdx.x * 256 + threadIdx.x;
   if (i >= n4) return;
-  const float4 v = reinterpret_cast<const float4*>(x)[i];
+  float4 v = reinterpret_cast<const float4*>(x)[i];
+  v.x *= up; v.y *= up; v.z *= up; v.w *= up;  // the planes' scale (a power of two: exact)
   const half4 h = {(f16)v.x, (f16)v.y, (f16)v.z, (f16)v.w};
   const half4 l = {(f16)(v.x - (float)h[0]), (f16)(v.y - (float)h[1]), (f16)(v.z - (float)h[2]),
                    (f16)(v.w - (float)h[3])};
@@ -525,16 +574,16 @@ __global__ __launch_bounds__(256) void split_f32_kernel(const float* __restrict_
   x3_raise(flag, x3_out_of_range4(v));
 }
 
-// global average pool of an NHWC tensor held as f16 hi / lo planes (x = hi + lo exactly), the
-// same summation order as avgpool_f32_kernel
+// global average pool of an NHWC tensor held as f16 hi / lo planes (x 2^s = hi + lo exactly), the
+// same summation order as avgpool_f32_kernel, then times down = 2^-s (exact)
 __global__ __launch_bounds__(256) void avgpool_split_kernel(const f16* __restrict__ x, long long lo, int HW, int C,
-                                                            float* __restrict__ y) {
+                                                            float down, float* __restrict__ y) {
   const int b = blockIdx.x, c = blockIdx.y * 256 + threadIdx.x;
   if (c >= C) return;
   const f16* p = x + (size_t)b * HW * C + c;
   float s = 0.f;
   for (int q = 0; q < HW; ++q) s += (float)p[(size_t)q * C] + (float)p[(size_t)q * C + lo];
-  y[(size_t)b * C + c] = s / (float)HW;
+  y[(size_t)b * C + c] = (s / (float)HW) * down;
 }
 
 int ImageModel::forward_f32(const uint8_t* img, int B, int H, int W, int C, float* feat, float* logits, float* probs,
@@ -694,7 +743,7 @@ int ImageModel::forward_x3(const uint8_t* img, int B, int H, int W, int C, float
     }
     const int ntiles = B * 49;
     hipLaunchKernelGGL(stem_pool_gray_x3_kernel, dim3(std::min(ntiles, ncu)), dim3(512), 0, s, stem_in, ntiles,
-                       Wt32 + stem_gray32_off, stem_x3_up, stem.x3_scale, P + stem.b_off, Xs, L,
+                       Wt32 + stem_gray32_off, stem_x3_up, std::ldexp(stem.x3_scale, stem.x3_s), P + stem.x3b_off, Xs, L,
                        range_flag());
     MEC_LAUNCH_CHECK();
   } else {
@@ -711,7 +760,8 @@ int ImageModel::forward_x3(const uint8_t* img, int B, int H, int W, int C, float
     hipLaunchKernelGGL(maxpool_f32_kernel, dim3((unsigned)((tp + 255) / 256)), dim3(256), 0, s, Y32, B, 112, 64, 56, S32);
     MEC_LAUNCH_CHECK();
     const size_t n4 = (size_t)B * 56 * 56 * 64 / 4;
-    hipLaunchKernelGGL(split_f32_kernel, dim3((unsigned)((n4 + 255) / 256)), dim3(256), 0, s, S32, n4, Xs, L, range_flag());
+    hipLaunchKernelGGL(split_f32_kernel, dim3((unsigned)((n4 + 255) / 256)), dim3(256), 0, s, S32, n4,
+                       std::ldexp(1.0f, stem.x3_s), Xs, L, range_flag());
     MEC_LAUNCH_CHECK();
   }
   MEC_TRY(prof.end(TAG_RESNET_STEM, s));
@@ -731,14 +781,14 @@ int ImageModel::forward_x3(const uint8_t* img, int B, int H, int W, int C, float
       GemmParams g;
       if (!conv1_done) {
         g.split = 1; g.A = in; g.a_lo = L; g.B = Wt + bk.c1.w_off; g.b_lo = wlo; g.oscale = bk.c1.x3_scale;
-        g.bias = P + bk.c1.b_off; g.act = ACT_RELU; g.C16 = t1; g.c_lo = L;
+        g.bias = P + bk.c1.x3b_off; g.act = ACT_RELU; g.C16 = t1; g.c_lo = L;
         g.M = nb * Hc * Hc; g.N = wd; g.K = cin;
         MEC_TRY(launch_gemm(g, s, &prof, TAG_RESNET_CONV1X1));
       }
       conv1_done = false;
       g = GemmParams();
       g.split = 1; g.amode = A_CONV; g.A = t1; g.a_lo = L; g.B = Wt + bk.c2.w_off; g.b_lo = wlo;
-      g.oscale = bk.c2.x3_scale; g.bias = P + bk.c2.b_off; g.act = ACT_RELU; g.C16 = t2; g.c_lo = L;
+      g.oscale = bk.c2.x3_scale; g.bias = P + bk.c2.x3b_off; g.act = ACT_RELU; g.C16 = t2; g.c_lo = L;
       g.M = nb * OH * OH; g.N = wd; g.K = 9 * wd;
       g.H = Hc; g.W = Hc; g.C = wd; g.OH = OH; g.OW = OH; g.ks = 3; g.stride = st; g.pad = 1;
       MEC_TRY(launch_gemm(g, s, &prof, TAG_RESNET_CONV3X3));
@@ -753,11 +803,11 @@ int ImageModel::forward_x3(const uint8_t* img, int B, int H, int W, int C, float
         MEC_TRY(prof.begin(TAG_RESNET_CONV1X1, s));
         if (bk.has_ds)
           MEC_TRY(launch_pw_chain_x3(t2, in, L, Wd + bk.c3ds_w_off, (long long)bk.c3ds_x3_lo, bk.c3ds_x3_scale,
-                                     P + bk.c3ds_b_off, Wt + nx->c1.w_off, wlo, nx->c1.x3_scale, P + nx->c1.b_off, out,
+                                     P + bk.c3ds_b_off, Wt + nx->c1.w_off, wlo, nx->c1.x3_scale, P + nx->c1.x3b_off, out,
                                      T1 + (size_t)i0 * OH * OH * nx->c1.cout, nb * OH * OH, nx->c1.cout, true, s));
         else
-          MEC_TRY(launch_pw_chain_x3(t2, in, L, Wt + bk.c3.w_off, wlo, bk.c3.x3_scale, P + bk.c3.b_off,
-                                     Wt + nx->c1.w_off, wlo, nx->c1.x3_scale, P + nx->c1.b_off, out,
+          MEC_TRY(launch_pw_chain_x3(t2, in, L, Wt + bk.c3.w_off, wlo, bk.c3.x3_scale, P + bk.c3.x3b_off,
+                                     Wt + nx->c1.w_off, wlo, nx->c1.x3_scale, P + nx->c1.x3b_off, out,
                                      T1 + (size_t)i0 * OH * OH * nx->c1.cout, nb * OH * OH, nx->c1.cout, false, s));
         MEC_TRY(prof.end(TAG_RESNET_CONV1X1, s));
         conv1_done = true;
@@ -772,7 +822,7 @@ int ImageModel::forward_x3(const uint8_t* img, int B, int H, int W, int C, float
         g.oscale = bk.c3ds_x3_scale; g.bias = P + bk.c3ds_b_off; g.K = wd + cin;
         g.H = Hc; g.W = Hc; g.C = cin; g.OH = OH; g.OW = OH; g.ks = 1; g.stride = st; g.pad = 0;
       } else {  // relu(bn3(conv3(t2)) + x)
-        g.A = t2; g.B = Wt + bk.c3.w_off; g.b_lo = wlo; g.oscale = bk.c3.x3_scale; g.bias = P + bk.c3.b_off;
+        g.A = t2; g.B = Wt + bk.c3.w_off; g.b_lo = wlo; g.oscale = bk.c3.x3_scale; g.bias = P + bk.c3.x3b_off;
         g.R = in; g.r_lo = L; g.K = wd;
       }
       MEC_TRY(launch_gemm(g, s, &prof, TAG_RESNET_CONV1X1));
@@ -798,7 +848,8 @@ int ImageModel::forward_x3(const uint8_t* img, int B, int H, int W, int C, float
   }
   MEC_TRY(run_blocks(kL12, blocks.size(), 0, B, 28, cur, other));
   const int Hc = 7;
-  hipLaunchKernelGGL(avgpool_split_kernel, dim3(B, 2048 / 256), dim3(256), 0, s, cur, L, Hc * Hc, 2048, pooled);
+  hipLaunchKernelGGL(avgpool_split_kernel, dim3(B, 2048 / 256), dim3(256), 0, s, cur, L, Hc * Hc, 2048,
+                     std::ldexp(1.0f, -x3_s_out), pooled);
   MEC_LAUNCH_CHECK();
   MEC_TRY(launch_linear_mfma<BACT_RELU>(pooled, 2048, B, 2048, P + fc1_off, P + fc1b_off, 512, feat, 512, nullptr, 0, s));
   MEC_TRY(launch_head7(feat, B, 512, P + fc2_off, P + fc2b_off, logits, probs, s));

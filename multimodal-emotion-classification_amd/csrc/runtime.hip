@@ -130,4 +130,11 @@ float split_planes(const float* w, size_t n, f16* hi, f16* lo) {
   return std::ldexp(1.0f, -e);
 }
 
+int activation_exp(double bound, double target) {
+  if (!(bound > 0.0) || !std::isfinite(bound)) return 0;
+  int e = (int)std::floor(std::log2(target / bound));
+  while (std::ldexp(bound, e) > target) --e;  // guard the log2 rounding
+  return std::max(-40, std::min(40, e));
+}
+
 }  // namespace mec

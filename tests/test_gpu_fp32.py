@@ -124,14 +124,34 @@ def test_precision_query(dev):
     assert m.lib.mec_precision(m.handle) == 1
 
 
-def test_text_fp32_golden(dev, golden):
-    """BERT fp32 against the fixture pinned to HF BertForSequenceClassification (eager)."""
+@pytest.mark.parametrize('precision', ['fp32', 'fp32x3'])
+def test_text_fp32_golden(dev, golden, precision):
+    """BERT at both fp32-class precisions (the exact-f32 engine, and fp32x3 -- the bench headline's)
+    against the fixture pinned to HF BertForSequenceClassification (eager): probs within 1e-5, CLS
+    feature within 1e-4 relative, argmax exact (inference/text_inference.py:124-127)."""
     gd = golden('text_bert.npz')
-    enc = engine.TextEncoder(device=dev, precision='fp32')
+    enc = engine.TextEncoder(device=dev, precision=precision)
     cls, logits, probs = _np(enc.forward(engine.to_device(gd['ids'], dev), engine.to_device(gd['mask'], dev)))
-    err, agree = _report('text fp32 golden', probs, gd['probs'])
+    enc.check()
+    err, agree = _report(f'text {precision} golden', probs, gd['probs'])
     ferr = float(np.abs(cls - gd['cls']).max() / np.abs(gd['cls']).max())
     print(f'  cls rel err {ferr:.3g}, logits max|d| {np.abs(logits - gd["logits"]).max():.3g}')
+    assert agree == len(probs) and err <= FP32_PROB_TOL and ferr <= FP32_FEAT_RTOL
+
+
+@pytest.mark.parametrize('precision', ['fp32', 'fp32x3'])
+def test_image_fp32_golden(dev, golden, precision):
+    """ResNet50 + head at both fp32-class precisions against the committed image fixture
+    (tests/golden/image_full.npz: the oracle/image.py restatement, torchvision absent, so
+    restatement-pinned; its resize is PIL-pinned): probs within 1e-5, 512-d feature within 1e-4
+    relative, argmax exact (inference/image_inference.py:116-118)."""
+    gd = golden('image_full.npz')
+    enc = engine.ImageEncoder(device=dev, precision=precision)
+    feat, logits, probs = _np(enc.forward(engine.to_device(gd['gray'], dev)))
+    enc.check()
+    err, agree = _report(f'image {precision} golden', probs, gd['probs'])
+    ferr = float(np.abs(feat - gd['feat']).max() / np.abs(gd['feat']).max())
+    print(f'  feat rel err {ferr:.3g}, logits max|d| {np.abs(logits - gd["logits"]).max():.3g}')
     assert agree == len(probs) and err <= FP32_PROB_TOL and ferr <= FP32_FEAT_RTOL
 
 

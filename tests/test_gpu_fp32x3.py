@@ -1,6 +1,6 @@
 """GPU: the fp32x3 path (MEC_PREC_FP32X3) -- the fp32 path's arithmetic with every GEMM / conv
-operand carried as an exact f16 hi/lo pair on the f16 MFMA (three products per fp32 product,
-one fp32 accumulator) -- held to the fp32 path's own bars against the oracle: probs within
+operand carried as a pair of f16 planes (hi + lo, 22 significant bits, activations at a per-tensor
+power-of-two plane scale) on the f16 MFMA (three products per fp32 product, one fp32 accumulator) -- held to the fp32 path's own bars against the oracle: probs within
 1e-5, features within 1e-4 relative, argmax exact on every row; and compared with the exact
 fp32 path on the same inputs (the two differ by reassociation-scale amounts only)."""
 import numpy as np
@@ -287,15 +287,16 @@ def _plane_output(dev, lib, tile):
 
 # ------------------------------------------------------------------ the fp32x3 range envelope
 # Weights are split after a per-matrix power-of-two pre-scale (csrc/runtime.hip split_planes).
-# Activations are split as they are produced: hi = f16(x), lo = f16(x - hi), which holds 22
-# significant bits for 2^-3 <= |x| < 65520 (lo a normal f16). Below 2^-3, lo is an f16 subnormal:
-# each operand then carries an absolute error <= 2^-25 instead. At |x| >= 65520 hi is inf: every
-# producer of activation planes raises the handle's range flag and mec_model_check fails the
-# forward (INTEGRATION.md "fp32x3 envelope").
+# Activations are split at a per-tensor power-of-two scale fixed at handle creation (models.h
+# activation_exp): hi = f16(x 2^s), lo = f16(x 2^s - hi), which holds 22 significant bits while
+# 2^-3 <= |x 2^s| < 65520; the consumer's epilogue scale folds in 2^-s (exact). At |x 2^s| >= 65520
+# hi is inf: every producer of activation planes raises the handle's range flag and mec_model_check
+# fails the forward (INTEGRATION.md "fp32x3 envelope").
 
 
-def _gemm_pair(dev, A, W):
-    """(exact-f32 engine, split engine) outputs of A . W^T, and the float64 reference."""
+def _gemm_pair(dev, A, W, s_a=0):
+    """(exact-f32 engine, split engine with A's planes at 2^s_a) outputs of A . W^T, and the float64
+    reference."""
     import ctypes
     from mec import _lib
     lib = _lib.load()
@@ -305,94 +306,272 @@ def _gemm_pair(dev, A, W):
     p = lambda t: ctypes.c_void_p(t.data_ptr())  # noqa: E731
     Ad, Wd = torch.from_numpy(A).to(dev), torch.from_numpy(W).to(dev)
     e = float(np.ceil(np.log2(16384 / np.abs(W).max())) - 1)
-    Axd, Wxd = torch.from_numpy(_split(A)).to(dev), torch.from_numpy(_split(W, 2.0 ** e)).to(dev)
+    Axd, Wxd = torch.from_numpy(_split(A, 2.0 ** s_a)).to(dev), torch.from_numpy(_split(W, 2.0 ** e)).to(dev)
     C32, Cx = torch.empty((M, N), device=dev), torch.empty((M, N), device=dev)
     _lib.check(lib.mec_gemm_f32(p(Ad), p(Wd), None, None, p(C32), M, N, K, 0, st), 'mec_gemm_f32')
-    _lib.check(lib.mec_gemm_f16x3(p(Axd), M * K, p(Wxd), N * K, ctypes.c_float(2.0 ** -e), None, None, None, 0,
+    _lib.check(lib.mec_gemm_f16x3(p(Axd), M * K, p(Wxd), N * K, ctypes.c_float(2.0 ** (-e - s_a)), None, None, None, 0,
                                   p(Cx), M, N, K, 0, st), 'mec_gemm_f16x3')
     torch.cuda.synchronize()
     return C32.cpu().numpy(), Cx.cpu().numpy(), A.astype(np.float64) @ W.astype(np.float64).T
 
 
+def _act_exp(bound, target=32768.0):
+    """csrc/runtime.hip activation_exp: the largest s with bound 2^s <= target."""
+    s = int(np.floor(np.log2(target / bound)))
+    while bound * 2.0 ** s > target:
+        s -= 1
+    return s
+
+
 def test_split_gemm_mixed_magnitude_activations_1e6_to_1e4(dev):
-    """Activations whose magnitudes span 1e-6 .. 1e4 inside every row (log-uniform, random signs):
-    the split engine stays within the fp32 GEMM bar (2e-6 x sum |a w|) of float64, as the exact-f32
-    engine does; tiny entries lose relative bits to the subnormal lo plane, but the bar is relative
-    to the row's sum and both engines are held to it."""
+    """Activations whose magnitudes span 1e-6 .. 1e4 inside every row (log-uniform, random signs),
+    split at the plane scale the model rule gives (max |a| 2^s <= 2^15): the split engine stays within
+    the fp32 GEMM bar (2e-6 x sum |a w|) of float64, as the exact-f32 engine does; tiny entries lose
+    relative bits, but the bar is relative to the row's sum and both engines are held to it."""
     rng = np.random.default_rng(11)
     M, N, K = 1024, 768, 768
     A = (np.sign(rng.standard_normal((M, K))) * 10.0 ** rng.uniform(-6, 4, (M, K))).astype(np.float32)
     W = (rng.standard_normal((N, K)) * 0.02).astype(np.float32)
-    c32, cx, ref = _gemm_pair(dev, A, W)
+    c32, cx, ref = _gemm_pair(dev, A, W, _act_exp(float(np.abs(A).max())))
     bound = 2e-6 * (np.abs(A).astype(np.float64) @ np.abs(W).astype(np.float64).T + 1)
     e32, ex3 = np.abs(c32 - ref), np.abs(cx - ref)
     print(f'mixed 1e-6..1e4: exact-f32 max err/bound {(e32 / bound).max():.3g}, split {(ex3 / bound).max():.3g}')
     assert (e32 <= bound).all() and (ex3 <= bound).all()
 
 
-@pytest.mark.parametrize('scale', [1e-1, 1e-3])
-def test_split_gemm_small_activations_absolute_floor(dev, scale):
-    """Activations uniformly small (N(0,1) x scale): below 2^-3 the lo plane is an f16 subnormal, so
-    each operand carries an absolute error <= 2^-25. The split engine stays within the fp32 bar plus
-    that floor, 2e-6 x sum |a w| + 2^-25 x sum |w|, and its error against the exact-f32 engine's is
-    printed (the envelope INTEGRATION.md states; MEC_PREC_FP32 has no such floor)."""
+@pytest.mark.parametrize('scale', [1e-1, 1e-3, 1e-5])
+def test_split_gemm_small_activations_scaled_planes(dev, scale):
+    """Activations uniformly small (N(0,1) x scale) split at their plane scale (max |a| 2^s <= 2^15,
+    the rule activation_exp applies to the models' bounds): the split engine holds the plain fp32 GEMM
+    bar, 2e-6 x sum |a w|, with no absolute term, as the exact-f32 engine does. Unscaled planes (s = 0)
+    would leave the lo plane an f16 subnormal below 2^-3 (an absolute error of 2^-25 per operand): that
+    error is printed beside it."""
     rng = np.random.default_rng(12)
     M, N, K = 1024, 768, 768
     A = (rng.standard_normal((M, K)) * scale).astype(np.float32)
     W = (rng.standard_normal((N, K)) * 0.02).astype(np.float32)
-    c32, cx, ref = _gemm_pair(dev, A, W)
+    s_a = _act_exp(float(np.abs(A).max()))
+    c32, cx, ref = _gemm_pair(dev, A, W, s_a)
+    _, cu, _ = _gemm_pair(dev, A, W, 0)
     aw = np.abs(A).astype(np.float64) @ np.abs(W).astype(np.float64).T
-    e32, ex3 = np.abs(c32 - ref), np.abs(cx - ref)
-    bound = 2e-6 * (aw + 1e-30) + 2.0 ** -25 * np.abs(W).astype(np.float64).sum(1)[None, :]
-    print(f'A ~ N(0,1) x {scale:g}: max err / sum|a w|: exact-f32 {(e32 / aw).max():.3g}, split {(ex3 / aw).max():.3g}')
+    e32, ex3, eu = np.abs(c32 - ref), np.abs(cx - ref), np.abs(cu - ref)
+    print(f'A ~ N(0,1) x {scale:g} (planes at 2^{s_a}): max err / sum|a w|: exact-f32 {(e32 / aw).max():.3g}, '
+          f'split {(ex3 / aw).max():.3g} (unscaled planes {(eu / aw).max():.3g})')
     assert (e32 <= 2e-6 * aw + 1e-30).all()
-    assert (ex3 <= bound).all()
+    assert (ex3 <= 2e-6 * aw + 1e-30).all()
 
 
-def _force_overflow(kind, name, factor):
-    w = dict(syn.weights(kind))  # a copy: syn.weights returns the cached dict every handle shares
-    w[name] = (w[name] * np.float32(factor)).astype(np.float32)
+def _edit(kind, edits):
+    """A copy of the seeded weights with edits {name: factor | (index, value)} applied (syn.weights
+    returns the cached dict every handle shares)."""
+    w = dict(syn.weights(kind))
+    for name, e in edits.items():
+        a = np.array(w[name], np.float32)
+        if isinstance(e, tuple):
+            a.flat[e[0]] = e[1]
+        else:
+            a = (a * np.float32(e)).astype(np.float32)
+        w[name] = a
     return w
 
 
-@pytest.mark.parametrize('name', ['bert.encoder.layer.0.intermediate.dense.weight',
-                                  'bert.embeddings.LayerNorm.weight'])
-def test_text_fp32x3_overflow_raises_at_check(dev, name):
-    """A weight scaled so one activation plane leaves the f16 range (FFN1's GEMM epilogue output,
-    or the embedding LayerNorm's output): the forward completes, and check() raises MecError
-    (mec_model_check) instead of the probabilities silently going NaN. The flag is cleared by the
-    check: a second check passes. The exact-fp32 path runs the same weights without complaint."""
+def _raises_then_clears(enc):
     from mec._lib import MecError
-    w = _force_overflow('text', name, 1e5)
+    torch.cuda.synchronize()
+    with pytest.raises(MecError, match='f16 hi / lo range'):
+        enc.check()
+    enc.check()  # the check cleared the flag
+
+
+# Non-finite values are no fp32 operands: whichever producer first writes one as planes raises the
+# flag. BERT's plane scales come from rigorous bounds, so only a NaN / inf can reach the guard there.
+@pytest.mark.parametrize('name,idx,value,fused', [
+    ('bert.embeddings.word_embeddings.weight', 101 * 768 + 5, np.nan, 1),   # embedding LayerNorm
+    ('bert.encoder.layer.0.attention.self.query.weight', 0, np.inf, 1),      # fused QKV + attention kernel
+    ('bert.encoder.layer.0.attention.self.value.weight', 0, np.inf, 0),      # split QKV GEMM epilogue
+    ('bert.encoder.layer.0.intermediate.dense.weight', 0, np.inf, 1)])       # FFN1 GEMM epilogue
+def test_text_fp32x3_nonfinite_raises_at_check(dev, name, idx, value, fused):
+    """A NaN / inf in the weights reaches an activation plane: the forward completes and check() raises
+    MecError (mec_model_check) instead of returning NaN probabilities unannounced; the check clears the
+    flag, so a second check passes."""
+    w = _edit('text', {name: (idx, value)})
     ids, mask = syn.text_inputs(4, 128, seed=3, ragged=True)
-    args = (engine.to_device(ids, dev), engine.to_device(mask, dev))
     enc = engine.TextEncoder(w, device=dev, precision='fp32x3')
+    enc.set_option('bert_qkv_attn', fused)
     enc.check()  # clean handle
-    enc.forward(*args)
-    torch.cuda.synchronize()
-    with pytest.raises(MecError, match='f16 hi / lo range'):
-        enc.check()
+    enc.forward(engine.to_device(ids, dev), engine.to_device(mask, dev))
+    _raises_then_clears(enc)
+
+
+@pytest.mark.parametrize('name', ['bert.encoder.layer.0.intermediate.dense.weight', 'bert.embeddings.LayerNorm.weight'])
+def test_text_fp32x3_large_weights_adapt_plane_scale(dev, name):
+    """A weight scaled by 1e5 (FFN1 outputs near 1e5, or embedding LayerNorm outputs near 3e6: past the
+    f16 range unscaled): the bound-derived plane exponents follow (models.h activation_exp), so the
+    forward raises no flag and matches the oracle on the same weights at the fp32 bars."""
+    w = _edit('text', {name: 1e5})
+    ids, mask = syn.text_inputs(4, 128, seed=3, ragged=True)
+    enc = engine.TextEncoder(w, device=dev, precision='fp32x3')
+    cls, _, probs = _np(enc.forward(engine.to_device(ids, dev), engine.to_device(mask, dev)))
     enc.check()
-    e32 = engine.TextEncoder(w, device=dev, precision='fp32')
-    _, _, p32 = _np(e32.forward(*args))
-    e32.check()
-    assert np.isfinite(p32).all()
+    rc, _, rp = o_t.forward(w, ids, mask)
+    err, agree = float(np.abs(probs - rp).max()), int((probs.argmax(1) == rp.argmax(1)).sum())
+    ferr = float(np.abs(cls - rc).max() / np.abs(rc).max())
+    print(f'{name} x 1e5: probs max|d| {err:.3g}, cls rel err {ferr:.3g}')
+    assert agree == 4 and err <= PROB_TOL and ferr <= FEAT_RTOL
 
 
-def test_resnet_fp32x3_overflow_raises_at_check(dev):
-    """The stem's output planes (stem_pool_gray_x3_kernel) out of the f16 range -> check() raises;
-    the same handle with in-range inputs afterwards checks clean."""
-    from mec._lib import MecError
-    w = _force_overflow('image', 'base.bn1.weight', 1e6)
-    enc = engine.ImageEncoder(w, device=dev, precision='fp32x3')
+# ResNet50 / MobileNetV2 plane scales come from BatchNorm estimates: activations far above what the BN
+# parameters predict (a conv weight scaled, BN unchanged) overflow and raise the flag.
+@pytest.mark.parametrize('name,seam', [('base.layer1.0.conv1.weight', 2),  # conv1 GEMM epilogue
+                                       ('base.layer1.0.conv3.weight', 2),  # layer1 dual seam (pw_chain_x3)
+                                       ('base.layer1.1.conv3.weight', 2),  # layer1 residual seam
+                                       ('base.layer1.1.conv3.weight', 0),  # conv3 GEMM epilogue (residual)
+                                       ('base.layer3.0.conv3.weight', 2)])  # dual conv3 + downsample GEMM
+def test_resnet_fp32x3_overflow_raises_at_check(dev, name, seam):
+    """A conv weight scaled by 1e6 with its BN unchanged: the activations leave the estimate's 64x
+    headroom and the f16 range -> check() raises; a handle with the seeded weights checks clean."""
+    enc = engine.ImageEncoder(_edit('image', {name: 1e6}), device=dev, precision='fp32x3')
+    enc.set_option('pw_chain_x3', seam)
     enc.forward(engine.to_device(syn.image_inputs(2, seed=5), dev))
-    torch.cuda.synchronize()
-    with pytest.raises(MecError, match='f16 hi / lo range'):
-        enc.check()
+    _raises_then_clears(enc)
     ok = engine.ImageEncoder(device=dev, precision='fp32x3')
     ok.forward(engine.to_device(syn.image_inputs(2, seed=5), dev))
     torch.cuda.synchronize()
     ok.check()
+
+
+@pytest.mark.parametrize('name,layered', [('base.features.2.conv.2.weight', 8),   # fused block input split
+                                          ('base.features.7.conv.2.weight', 8),   # layered tail's first split
+                                          ('base.features.9.conv.2.weight', 8),   # layered project epilogue
+                                          ('base.features.17.conv.2.weight', 0)])  # features[18] input split
+def test_mobilenet_v2_fp32x3_overflow_raises_at_check(dev, name, layered):
+    """A MobileNetV2 projection weight scaled by 1e6 (its BN unchanged): the block output overflows the
+    next producer of planes (the fused block kernel's input split, mbv2_split_pad_kernel, the layered
+    project GEMM, mbv2_split_kernel) -> check() raises, then clears."""
+    enc = engine.MobileNetImageEncoder(_edit('image_mbv2', {name: 1e6}), device=dev, precision='fp32x3')
+    enc.set_option('mbv2_layered', layered)
+    enc.forward(engine.to_device(syn.image_inputs(2, seed=5), dev))
+    _raises_then_clears(enc)
+
+
+def test_resnet_fp32x3_large_bn_adapts_plane_scale(dev):
+    """The stem BN's gamma x 1e6 (stem outputs near 1e7: past the f16 range unscaled): the estimate
+    follows the BN, so no flag, and the probabilities match the oracle on the same weights."""
+    w = _edit('image', {'base.bn1.weight': 1e6})
+    gray = syn.image_inputs(3, seed=5)
+    enc = engine.ImageEncoder(w, device=dev, precision='fp32x3')
+    feat, _, probs = _np(enc.forward(engine.to_device(gray, dev)))
+    enc.check()
+    rf, _, rp = o_i.forward(w, gray)
+    err = float(np.abs(probs - rp).max())
+    ferr = float(np.abs(feat - rf).max() / np.abs(rf).max())
+    print(f'bn1 gamma x 1e6: probs max|d| {err:.3g}, feat rel err {ferr:.3g}')
+    assert err <= PROB_TOL and ferr <= FEAT_RTOL and (probs.argmax(1) == rp.argmax(1)).all()
+
+
+# ------------------------------------------------------------------ small activations, model level
+def _resnet_scaled(c):
+    """ResNet50 weights computing the seeded network's function with every activation tensor c times
+    smaller: every BN's gamma and beta x c, every conv after the stem x 1/c (its input is c times
+    smaller; its BN sees the same pre-BN values), fc[1] x 1/c."""
+    w = dict(syn.weights('image'))
+    for k in list(w):
+        a = np.asarray(w[k], np.float32)
+        if (k.endswith('.weight') or k.endswith('.bias')) and a.ndim == 1 and ('bn' in k or 'downsample.1' in k):
+            w[k] = (a * np.float32(c)).astype(np.float32)
+        elif k.startswith('base.layer') and a.ndim == 4:
+            w[k] = (a / np.float32(c)).astype(np.float32)
+    w['base.fc.1.weight'] = (np.asarray(w['base.fc.1.weight']) / np.float32(c)).astype(np.float32)
+    return w
+
+
+@pytest.mark.parametrize('how', ['gamma_1e-3', 'activations_2^-14'])
+def test_resnet_fp32x3_small_activations_vs_oracle(dev, how):
+    """Small activations end to end on the fp32x3 path against the oracle on the same weights, at the
+    fp32 bars (probs 1e-5, feature 1e-4 relative, argmax exact):
+      * gamma_1e-3: every BN gamma x 1e-3 (activations near |beta| ~ 0.1 and below, the f16 lo plane's
+        subnormal range without a plane scale);
+      * activations_2^-14: every activation tensor 2^-14 times the seeded network's (_resnet_scaled),
+        the same function: probs must also equal the seeded network's within the bar.
+    The plane exponents follow the BN estimates (models.h activation_exp), so no lo plane is subnormal."""
+    if how == 'gamma_1e-3':
+        w = dict(syn.weights('image'))
+        for k in list(w):
+            if k.endswith('.weight') and np.asarray(w[k]).ndim == 1:
+                w[k] = (np.asarray(w[k]) * np.float32(1e-3)).astype(np.float32)
+    else:
+        w = _resnet_scaled(2.0 ** -14)
+    gray = syn.image_inputs(8, seed=77)
+    enc = engine.ImageEncoder(w, device=dev, precision='fp32x3')
+    feat, _, probs = _np(enc.forward(engine.to_device(gray, dev)))
+    enc.check()
+    rf, _, rp = o_i.forward(w, gray)
+    err = float(np.abs(probs - rp).max())
+    ferr = float(np.abs(feat - rf).max() / np.abs(rf).max())
+    print(f'resnet50 fp32x3 {how}: probs max|d| {err:.3g}, feat rel err {ferr:.3g}')
+    assert err <= PROB_TOL and ferr <= FEAT_RTOL and (probs.argmax(1) == rp.argmax(1)).all()
+    if how != 'gamma_1e-3':
+        _, _, rp0 = o_i.forward(syn.weights('image'), gray)
+        assert np.abs(probs - rp0).max() <= PROB_TOL
+
+
+def test_text_fp32x3_small_activations_vs_oracle(dev):
+    """BERT with the LayerNorm outputs, Q, V and the context 2^-12 times the seeded network's and K 2^12
+    times (every LN gamma / beta, bq, bv, bo, Wo2, bo2 x c; bk, Wi, the pooler x 1/c; Wk x 1/c^2: the
+    same function) on the fp32x3 path against the oracle at the fp32 bars; the plane exponents follow
+    the bounds (one each for Q, K, V)."""
+    c = np.float32(2.0 ** -12)
+    w = dict(syn.weights('text'))
+    for k in list(w):
+        a = np.asarray(w[k], np.float32)
+        if 'LayerNorm' in k or k.endswith(('query.bias', 'value.bias', 'attention.output.dense.bias',
+                                           'output.dense.weight', 'output.dense.bias')):
+            if not k.endswith('attention.output.dense.weight'):
+                w[k] = (a * c).astype(np.float32)
+        elif k.endswith(('intermediate.dense.weight', 'pooler.dense.weight', 'key.bias')):
+            w[k] = (a / c).astype(np.float32)
+        elif k.endswith('key.weight'):  # K = K_seeded / c, so the scores Q K^T are unchanged
+            w[k] = (a / (c * c)).astype(np.float32)
+    ids, mask = syn.text_inputs(6, 128, seed=78, ragged=True)
+    enc = engine.TextEncoder(w, device=dev, precision='fp32x3')
+    cls, _, probs = _np(enc.forward(engine.to_device(ids, dev), engine.to_device(mask, dev)))
+    enc.check()
+    rc, _, rp = o_t.forward(w, ids, mask)
+    _, _, rp0 = o_t.forward(syn.weights('text'), ids, mask)
+    err = float(np.abs(probs - rp).max())
+    ferr = float(np.abs(cls - rc).max() / np.abs(rc).max())
+    print(f'bert fp32x3 activations x 2^-12: probs max|d| {err:.3g} (seeded net {np.abs(probs - rp0).max():.3g}), '
+          f'cls rel err {ferr:.3g}, |cls| max {np.abs(rc).max():.3g}')
+    assert err <= PROB_TOL and ferr <= FEAT_RTOL and (probs.argmax(1) == rp.argmax(1)).all()
+
+
+def test_mobilenet_v2_fp32x3_small_activations_vs_oracle(dev):
+    """MobileNetV2 with every block output 2^-14 times the seeded network's (each projection BN's gamma /
+    beta x c, every expand conv and features[18]'s conv x 1/c: the same function), fused blocks and the
+    layered tail, against the oracle at the fp32 bars."""
+    from oracle import image_mbv2 as o_mb
+    c = np.float32(2.0 ** -14)
+    w = dict(syn.weights('image_mbv2'))
+    for i, (t, cin, hid, cout, st) in enumerate(syn.mbv2_blocks()):
+        p = f'base.features.{i + 1}.conv.'
+        bn = p + ('2' if t == 1 else '3')
+        for sfx in ('.weight', '.bias'):
+            w[bn + sfx] = (np.asarray(w[bn + sfx]) * c).astype(np.float32)
+        if t != 1:
+            w[p + '0.0.weight'] = (np.asarray(w[p + '0.0.weight']) / c).astype(np.float32)
+    w['base.features.18.0.weight'] = (np.asarray(w['base.features.18.0.weight']) / c).astype(np.float32)
+    gray = syn.image_inputs(6, seed=79)
+    rf, _, rp = o_mb.forward(w, gray)
+    for layered in (8, 0):
+        enc = engine.MobileNetImageEncoder(w, device=dev, precision='fp32x3')
+        enc.set_option('mbv2_layered', layered)
+        feat, _, probs = _np(enc.forward(engine.to_device(gray, dev)))
+        enc.check()
+        err = float(np.abs(probs - rp).max())
+        ferr = float(np.abs(feat - rf).max() / np.abs(rf).max())
+        print(f'mobilenet_v2 fp32x3 block outputs x 2^-14, mbv2_layered {layered}: probs max|d| {err:.3g}, '
+              f'feat rel err {ferr:.3g}')
+        assert err <= PROB_TOL and ferr <= FEAT_RTOL and (probs.argmax(1) == rp.argmax(1)).all()
 
 
 def test_fp32x3_untuned_tiles_match_autotuned(dev):
