@@ -21,8 +21,10 @@ The path runs at three precisions on the same inputs; rank 0 prints ONE JSON lin
             round the accumulator 8x less often: tests/test_gpu_fp32x3.py) -- `value`;
   nested    "fp32_exact_path": every operand and product in fp32 (v_mfma_f32_16x16x4_f32);
   nested    "f16_fast_path": BERT / ResNet50 on f16 MFMA operands with fp32 accumulation,
-            LayerNorm, softmax, GELU, residual stream and heads (north_star's probs <= 1e-3 bar;
-            narrower than the reference's arithmetic, so reported beside the headline, not as it).
+            LayerNorm, softmax, GELU, residual stream and heads: a speed option, narrower than the
+            reference's arithmetic, reported beside the headline, not as it. Its text probs error sits
+            near the north_star's 1e-3 bar with rows at risk, so its parity.north_star verdict reads
+            "outside the contract margin" (margin = half the bar, no at-risk rows).
 Each carries `parity`: the oracle (CPU fp32 restatement of the reference) on rows of the timed
 batch -- every row at B <= 256, rows from every quarter of the batch beyond -- with logits /
 probs max-abs-err, argmax agreement and the count of at-risk rows (oracle top-2 margin below
@@ -64,7 +66,8 @@ PEAK_TFLOPS = {'f16': 2500.0, 'fp32': 157.3, 'fp32x3': 2500.0}
 MFMA_FLOP_PER_FLOP = {'f16': 1, 'fp32': 1, 'fp32x3': 3}
 DTYPE = {'f16': 'f16 MFMA operands / fp32 accumulate, LN & softmax & residual fp32; speech+fusion fp32',
          'fp32': 'fp32 (exact-f32 MFMA GEMMs; every operand and product fp32)',
-         'fp32x3': 'fp32 (GEMM/conv operands as exact f16 hi+lo pairs, hi.hi + hi.lo + lo.hi on the f16 MFMA into '
+         'fp32x3': 'fp32 (GEMM/conv operands as f16 hi+lo plane pairs, 22 significant bits, activations at '
+                   'per-tensor power-of-two plane scales; hi.hi + hi.lo + lo.hi on the f16 MFMA into '
                    'one fp32 accumulator: per GEMM closer to float64 than the exact-f32 MFMA; LN, softmax, '
                    'attention, GELU, residual stream, heads, speech and fusion fp32)'}
 ROW = 34  # packed result row: 3x7 modality probs | 7 fused probs | 3 attention | 3 decision weights
@@ -309,6 +312,17 @@ def parity(out, ref, rows):
     res['rows'] = (f'all {len(rows)} rows of the timed batch' if len(rows) == out['fusion'][1].shape[0]
                    else f'{len(rows)} rows spread over the timed batch (first {rows[:4]}, last {rows[-3:]})')
     res['fused_reference'] = 'end-to-end oracle chain o_f(o_s, o_t, o_i) (multimodal_fusion.py:271-278)'
+    # north_star: argmax exact, probs within 1e-3. "with_margin": every modality's probs error at most half
+    # the bar and no row whose oracle top-2 margin is below twice that error (a path that meets the bar only
+    # narrowly, as the f16 one does, is reported as outside the contract's margin)
+    mods = [res[k] for k in ('speech', 'text', 'image', 'fusion')]
+    exact = all(m['argmax_agree'].split('/')[0] == m['argmax_agree'].split('/')[1] for m in mods)
+    within = all(m['probs_max_abs_err'] <= 1e-3 for m in mods)
+    margin = all(m['probs_max_abs_err'] <= 5e-4 and m['at_risk_rows'] == 0 for m in mods)
+    res['north_star'] = {'argmax_exact': exact, 'probs_within_1e-3': within, 'with_margin': margin,
+                         'verdict': ('held' if exact and within and margin else
+                                     'met on this batch, outside the contract margin' if exact and within else
+                                     'not met')}
     return res
 
 

@@ -56,10 +56,14 @@ int mec_create(int kind, const float* host_blob, size_t n, int device, mec_model
  * operand carried as a pair of f16 planes (x = hi + lo) and each product as hi.hi + hi.lo + lo.hi
  * on the f16 MFMA into one fp32 accumulator; LayerNorm, softmax, attention, GELU, depthwise convs,
  * residual stream and heads fp32. Envelope: weights are split after a per-matrix power-of-two
- * pre-scale (22 significant bits each); an activation keeps 22 significant bits for
- * 2^-3 <= |x| < 65520 and an absolute error <= 2^-25 below 2^-3 (the lo plane is then an f16
- * subnormal); at |x| >= 65520 (or NaN / inf) the producing kernel raises the handle's range flag
- * and mec_model_check fails. Speech, fusion and audio handles are fp32 at every setting. */
+ * pre-scale (22 significant bits each); each activation tensor is split at a power-of-two plane
+ * scale 2^s fixed at creation (hi = f16(x 2^s), lo = f16(x 2^s - hi); the consumer's epilogue folds
+ * in 2^-s, exactly): from rigorous bounds for BERT (LayerNorm outputs and their projections: no
+ * plane can overflow) and from the BatchNorm parameters for ResNet50 / MobileNetV2 (64x headroom
+ * over a 6-sigma estimate), so the planes hold 22 significant bits for the tensor's whole working
+ * range (INTEGRATION.md "fp32x3 envelope"). A plane value at |x 2^s| >= 65520 (activations far above
+ * what the BN parameters predict) or a NaN / inf raises the handle's range flag and mec_model_check
+ * fails. Speech, fusion and audio handles are fp32 at every setting. */
 enum { MEC_PREC_F16 = 0, MEC_PREC_FP32 = 1, MEC_PREC_FP32X3 = 2 };
 int mec_create_ex(int kind, const float* host_blob, size_t n, int device, int precision, mec_model** out);
 /* The handle's precision (MEC_PREC_*), -1 on a null handle. */
@@ -184,7 +188,12 @@ int mec_conv_f32(const float* x, const float* w, const float* bias, const float*
  *   "mbv2_x3_tile" 0|[4]   fp32x3 MobileNetV2: 4x4 output tiles for the stride-2 blocks at 56 / 28 outputs
  *   "mbv2_x3_tpw" 1|[2]..16 fp32x3 MobileNetV2 fused blocks: output tiles per workgroup, the next tile's
  *                          input loaded into registers while one computes (same bits for every value)
+ *   "mbv2_x3_occ" [3]|4    fp32x3 MobileNetV2 4x4-tile blocks: workgroups per CU the registers are
+ *                          allocated for (4: 128 VGPRs with an 84-B spill, 3: 168 VGPRs); same bits
+ *   "mbv2_x3_sesw" 0|[1]   fp32x3 MobileNetV2 fused blocks: the expanded chunk's rows chunk-swizzled per tile
+ *                          shape (fewer LDS bank conflicts on the depthwise reads) or unswizzled; same bits
  *   "mbv2_layered" 0|7..17 [8]  fp32x3 MobileNetV2: features[k..17] as expand GEMM -> depthwise -> project GEMM
+ *                          (0: every block fused but features[17], layered at every setting)
  *   "mbv2_layered16" 0|7..17 [8]  the same on the f16 path
  *   "mbv2_impl" [0]|1|2    MobileNetV2 block form: 0 = time both per block shape, 1 = workgroup, 2 = wave
  *   "fusion_r" 1|2|[4]     samples per fusion workgroup

@@ -114,8 +114,14 @@ struct Options {
   // at B = 256 (profiles/r04_ab_mbv2x3_tile.txt)
   int mbv2_x3_tile = 4;
   int mbv2_x3_tpw = 2;  // fp32x3 MobileNetV2 fused blocks: output tiles per workgroup (next tile's input prefetched)
+  // fp32x3 MobileNetV2 4x4-tile (stride-2) fused blocks: workgroups per CU their registers are allocated for
+  // (4: 128 VGPRs and an 84-B spill per lane; 3: 168 VGPRs, no spill); same bits
+  int mbv2_x3_occ = 3;
+  // fp32x3 MobileNetV2 fused blocks: the expanded chunk's f32 rows with a per-tile-shape 16-B chunk swizzle
+  // (1; fewer LDS bank conflicts on the depthwise reads) or unswizzled 36-float rows (0); same bits
+  int mbv2_x3_sesw = 1;
   // fp32x3 MobileNetV2: features[k..17] as expand GEMM -> depthwise kernel -> project GEMM on hi / lo
-  // planes (the "layered" form; k = 7..17, 0 = every block fused)
+  // planes (the "layered" form; k = 7..17, 0 = every block fused but features[17], which is always layered)
   int mbv2_layered = 8;
   int mbv2_layered16 = 8;  // the same on the f16 path (features[k..17] on f16 GEMMs; 0 = every block fused)
   // ping-pong GEMM tile order inside each XCD's contiguous tile range: 0 = row-major (all N

@@ -51,13 +51,41 @@ __device__ __forceinline__ float relu6x(float v) { return fminf(fmaxf(v, 0.f), 6
 // planes keep 22 significant bits down to 2^-16 and can never overflow
 constexpr float kDwUp = 8192.f;
 
-template <int S, int TO, int CINP, int HIDP, int COUTP, bool EXPAND, bool RES, int STEM>
+// 16-B chunk c of f16 plane row p of CH chunks sits at chunk mx_sw<CH>(p, c): the rows are unpadded, and
+// the XOR puts the 16 lanes of every ds_read_b128 lane group of a 16x16x32 fragment read (rows p, chunks
+// 4 k + (lane >> 4)) on 16 distinct 4-bank slots (MI355X_MICROARCH.md, LDS lane groups): CH = 4 (mod 8)
+// rows (64 / 192 / 320 B) take gemm_common.h's sw<32> swizzle, CH = 8 (128 B) its sw<64>. Same values,
+// same arithmetic: only the LDS addresses move.
+template <int CH>
+__device__ __forceinline__ int mx_sw(int p, int c) {
+  static_assert(CH % 4 == 0, "rows of whole 32-deep k chunks");
+  if constexpr (CH % 8 == 0) return c ^ ((p >> 1) & 7);
+  else return c ^ ((4 - ((p >> 2) & 3)) & 3);
+}
+
+template <int SEL>
+__device__ __forceinline__ int se_sw(int p) {
+  if constexpr (SEL < 0) return 0;  // unswizzled 36-float rows (opt().mbv2_x3_sesw 0)
+  else if constexpr (SEL == 0) return (p ^ (p >> 4)) & 7;
+  else if constexpr (SEL == 1) return (p ^ (p >> 1)) & 7;
+  else if constexpr (SEL == 2) return (p ^ (p >> 3)) & 7;
+  else return ((p >> 1) ^ (p >> 2)) & 7;
+}
+
+template <int S, int TO, int CINP, int HIDP, int COUTP, bool EXPAND, bool RES, int STEM, bool SW = true>
 struct MxGeom {
   static constexpr int IR = (TO - 1) * S + 3, NP = IR * IR, MP = (NP + 15) / 16 * 16;
-  static constexpr int XLD = CINP + 8;   // f16 plane row (halfs)
+  static constexpr int XLD = CINP;       // f16 plane row (halfs; chunks swizzled, mx_sw)
   static constexpr int XF = CINP + 4;    // f32 row of the non-expand (stem) input tile
-  static constexpr int EF = MX_HC + 4;   // f32 row of the expanded chunk
-  static constexpr int ELD = MX_HC + 8;  // f16 plane row of the depthwise output
+  // f32 row of the expanded chunk (floats) and the 16-B chunk swizzle se_sw of its rows, per tile shape:
+  // the rows the depthwise's ds_read_b128 lane groups read (4 - 8 input pixels, one per output pixel of
+  // the group, at one tap) spread over distinct 4-bank slots; the expand epilogue's ds_write_b128 stays
+  // conflict-free (a python search over every tap, lane group and row stride 32..64 floats: LDS cycles of
+  // the depthwise reads -40 / -50 / -15 / -60 % for the 4x4/2, 8x8/1, 7x7/1 and 7x7/2 tiles against the
+  // unswizzled 36-float rows)
+  static constexpr int SEL = !SW ? -1 : (S == 2 && TO == 4) ? 0 : (S == 1 && TO == 8) ? 1 : (S == 1) ? 2 : 3;
+  static constexpr int EF = SEL < 0 ? MX_HC + 4 : (SEL == 1 || SEL == 2) ? MX_HC : MX_HC + 16;
+  static constexpr int ELD = MX_HC;      // f16 plane row of the depthwise output (chunks swizzled)
   static constexpr int NQ = TO * TO;
   // depthwise-output rows: the output pixels rounded up to whole 16-pixel project fragments (16 for
   // a 4 x 4 tile, where 64 rows put the stride-2 blocks at three workgroups per CU instead of four)
@@ -69,9 +97,12 @@ struct MxGeom {
   static constexpr bool DWL = LDS_FIXED + HIDP * 9 * 4 <= 128 * 1024;
 };
 
-template <int S, int TO, int CINP, int HIDP, int COUTP, bool EXPAND, bool RES, int STEM>
-__global__ __launch_bounds__(256, 4) void mbv2_x3_kernel(const MbX3Args a) {
-  using G = MxGeom<S, TO, CINP, HIDP, COUTP, EXPAND, RES, STEM>;
+// OCC: workgroups per CU the register allocation targets (launch bounds). 4 for most shapes (16 waves per
+// CU; the wider ones exceed it and run at the occupancy their registers allow); the stride-2 4x4-tile
+// shapes take opt().mbv2_x3_occ (3: 168 VGPRs, no spill; 4: 128 VGPRs and an 84-B spill per lane).
+template <int S, int TO, int CINP, int HIDP, int COUTP, bool EXPAND, bool RES, int STEM, int OCC = 4, bool SW = true>
+__global__ __launch_bounds__(256, OCC) void mbv2_x3_kernel(const MbX3Args a) {
+  using G = MxGeom<S, TO, CINP, HIDP, COUTP, EXPAND, RES, STEM, SW>;
   constexpr int IR = G::IR, NP = G::NP, MP = G::MP, XLD = G::XLD, XF = G::XF, EF = G::EF, ELD = G::ELD;
   constexpr int NQ = G::NQ, NDR = G::NDR, OT = G::OT, KX = G::KX;
   static_assert(NQ <= 64, "tile");
@@ -172,8 +203,9 @@ __global__ __launch_bounds__(256, 4) void mbv2_x3_kernel(const MbX3Args a) {
         const half4 h = {(f16)u.x, (f16)u.y, (f16)u.z, (f16)u.w};
         const half4 l = {(f16)(u.x - (float)h[0]), (f16)(u.y - (float)h[1]), (f16)(u.z - (float)h[2]),
                          (f16)(u.w - (float)h[3])};
-        *reinterpret_cast<half4*>(sXh + p * XLD + c4 * 4) = h;
-        *reinterpret_cast<half4*>(sXl + p * XLD + c4 * 4) = l;
+        const int xo = p * XLD + mx_sw<CINP / 8>(p, c4 >> 1) * 8 + (c4 & 1) * 4;
+        *reinterpret_cast<half4*>(sXh + xo) = h;
+        *reinterpret_cast<half4*>(sXl + xo) = l;
         bad |= x3_out_of_range4(u);
       }
     }
@@ -258,8 +290,9 @@ __global__ __launch_bounds__(256, 4) void mbv2_x3_kernel(const MbX3Args a) {
         floatx4 e2[2] = {floatx4{0.f, 0.f, 0.f, 0.f}, floatx4{0.f, 0.f, 0.f, 0.f}};
 #pragma unroll
         for (int k = 0; k < KX; ++k) {
-          const half8 bh = *reinterpret_cast<const half8*>(sXh + p * XLD + 32 * k + 8 * lq);
-          const half8 bl = *reinterpret_cast<const half8*>(sXl + p * XLD + 32 * k + 8 * lq);
+          const int xo = p * XLD + mx_sw<CINP / 8>(p, 4 * k + lq) * 8;
+          const half8 bh = *reinterpret_cast<const half8*>(sXh + xo);
+          const half8 bl = *reinterpret_cast<const half8*>(sXl + xo);
 #pragma unroll
           for (int ht = 0; ht < 2; ++ht) {
             e2[ht] = __builtin_amdgcn_mfma_f32_16x16x32_f16(afl[ht][k], bh, e2[ht], 0, 0, 0);
@@ -274,7 +307,7 @@ __global__ __launch_bounds__(256, 4) void mbv2_x3_kernel(const MbX3Args a) {
           ev.y = valid ? relu6x(__builtin_fmaf(e2[ht][1], a.we_scale, eb[ht][1])) : 0.f;
           ev.z = valid ? relu6x(__builtin_fmaf(e2[ht][2], a.we_scale, eb[ht][2])) : 0.f;
           ev.w = valid ? relu6x(__builtin_fmaf(e2[ht][3], a.we_scale, eb[ht][3])) : 0.f;
-          *reinterpret_cast<float4*>(sE + p * EF + 16 * ht + 4 * lq) = ev;
+          *reinterpret_cast<float4*>(sE + p * EF + ((4 * ht + lq) ^ se_sw<G::SEL>(p)) * 4) = ev;
         }
       }
       if (h0 + MX_HC < HIDP) load_af(h0 + MX_HC);  // next chunk's expand weights: in flight during dw + project
@@ -302,9 +335,17 @@ __global__ __launch_bounds__(256, 4) void mbv2_x3_kernel(const MbX3Args a) {
         for (int ky = 0; ky < 3; ++ky)
 #pragma unroll
           for (int kx = 0; kx < 3; ++kx) {
-            const float* ep = src + (dp0 + ky * IR + kx) * sld + 8 * dcg;
-            const float4 e0 = *reinterpret_cast<const float4*>(ep);
-            const float4 e1 = *reinterpret_cast<const float4*>(ep + 4);
+            const int pp = dp0 + ky * IR + kx;
+            float4 e0, e1;
+            if constexpr (EXPAND) {  // sE: chunks swizzled (se_sw)
+              const int f = se_sw<G::SEL>(pp);
+              e0 = *reinterpret_cast<const float4*>(src + pp * sld + ((2 * dcg) ^ f) * 4);
+              e1 = *reinterpret_cast<const float4*>(src + pp * sld + ((2 * dcg + 1) ^ f) * 4);
+            } else {
+              const float* ep = src + pp * sld + 8 * dcg;
+              e0 = *reinterpret_cast<const float4*>(ep);
+              e1 = *reinterpret_cast<const float4*>(ep + 4);
+            }
             const float4 w0 = *reinterpret_cast<const float4*>(wd + (ky * 3 + kx) * 8);
             const float4 w1 = *reinterpret_cast<const float4*>(wd + (ky * 3 + kx) * 8 + 4);
             d[0] = __builtin_fmaf(e0.x, w0.x, d[0]); d[1] = __builtin_fmaf(e0.y, w0.y, d[1]);
@@ -320,8 +361,9 @@ __global__ __launch_bounds__(256, 4) void mbv2_x3_kernel(const MbX3Args a) {
         }
       }
       if (dq < NDR) {  // rows NQ .. NDR - 1: zeros for the last fragment's padding pixels
-        *reinterpret_cast<half8*>(sDh + dq * ELD + 8 * dcg) = oh;
-        *reinterpret_cast<half8*>(sDl + dq * ELD + 8 * dcg) = ol;
+        const int dof = dq * ELD + mx_sw<MX_HC / 8>(dq, dcg) * 8;
+        *reinterpret_cast<half8*>(sDh + dof) = oh;
+        *reinterpret_cast<half8*>(sDl + dof) = ol;
       }
     }
     __syncthreads();
@@ -329,8 +371,9 @@ __global__ __launch_bounds__(256, 4) void mbv2_x3_kernel(const MbX3Args a) {
     // ---- project: out^T[o][q] += Wp[o][h0..h0+31] . D[q][:]; wave w owns pixels 16w..16w+15 (the
     // waves past the tile's pixels have nothing to project)
     if (16 * wave < NDR) {
-      const half8 bh = *reinterpret_cast<const half8*>(sDh + (16 * wave + l16) * ELD + 8 * lq);
-      const half8 bl = *reinterpret_cast<const half8*>(sDl + (16 * wave + l16) * ELD + 8 * lq);
+      const int r = 16 * wave + l16, dof = r * ELD + mx_sw<MX_HC / 8>(r, lq) * 8;
+      const half8 bh = *reinterpret_cast<const half8*>(sDh + dof);
+      const half8 bl = *reinterpret_cast<const half8*>(sDl + dof);
 #pragma unroll
       for (int o = 0; o < OT; ++o) {
         acc[o] = __builtin_amdgcn_mfma_f32_16x16x32_f16(pfl[o], bh, acc[o], 0, 0, 0);
@@ -371,21 +414,6 @@ __global__ __launch_bounds__(256, 4) void mbv2_x3_kernel(const MbX3Args a) {
     }
   }
   }  // tiles
-}
-
-// f32 [n4 * 4] -> f16 hi / lo planes of x up (up = 2^s, exact; the features[18] GEMM's A operand)
-__global__ __launch_bounds__(256) void mbv2_split_kernel(const float* __restrict__ x, size_t n4, float up,
-                                                         f16* __restrict__ hi, long long lo, unsigned* flag) {
-  const size_t i = (size_t)blockIdx.x * 256 + threadIdx.x;
-  if (i >= n4) return;
-  float4 v = reinterpret_cast<const float4*>(x)[i];
-  v.x *= up; v.y *= up; v.z *= up; v.w *= up;
-  const half4 h = {(f16)v.x, (f16)v.y, (f16)v.z, (f16)v.w};
-  const half4 l = {(f16)(v.x - (float)h[0]), (f16)(v.y - (float)h[1]), (f16)(v.z - (float)h[2]),
-                   (f16)(v.w - (float)h[3])};
-  reinterpret_cast<half4*>(hi)[i] = h;
-  reinterpret_cast<half4*>(hi + lo)[i] = l;
-  x3_raise(flag, x3_out_of_range4(v));
 }
 
 // f32 [rows][cin] -> f16 hi / lo planes [rows][ld] of x up (up = 2^s; lo at + lo), channels cin .. ld-1
@@ -517,8 +545,23 @@ int launch_x3_block(const MbX3Args& a0, int B, hipStream_t s) {
   a.ntiles = B * tpr * tpr;
   // opt().mbv2_x3_tpw tiles per workgroup (1: one tile each, no prefetch)
   const int tpw = std::max(1, opt().mbv2_x3_tpw);
-  hipLaunchKernelGGL((mbv2_x3_kernel<S, TO, CINP, HIDP, COUTP, EXPAND, RES, STEM>), dim3((a.ntiles + tpw - 1) / tpw),
-                     dim3(256), 0, s, a);
+  const dim3 grid((a.ntiles + tpw - 1) / tpw);
+  // opt().mbv2_x3_sesw: the expanded chunk's rows swizzled (1) or unswizzled (0); same bits
+  const bool sw = opt().mbv2_x3_sesw != 0;
+  if constexpr (TO == 4) {
+    if (opt().mbv2_x3_occ == 3 && sw)
+      hipLaunchKernelGGL((mbv2_x3_kernel<S, TO, CINP, HIDP, COUTP, EXPAND, RES, STEM, 3, true>), grid, dim3(256), 0, s, a);
+    else if (opt().mbv2_x3_occ == 3)
+      hipLaunchKernelGGL((mbv2_x3_kernel<S, TO, CINP, HIDP, COUTP, EXPAND, RES, STEM, 3, false>), grid, dim3(256), 0, s, a);
+    else if (sw)
+      hipLaunchKernelGGL((mbv2_x3_kernel<S, TO, CINP, HIDP, COUTP, EXPAND, RES, STEM, 4, true>), grid, dim3(256), 0, s, a);
+    else
+      hipLaunchKernelGGL((mbv2_x3_kernel<S, TO, CINP, HIDP, COUTP, EXPAND, RES, STEM, 4, false>), grid, dim3(256), 0, s, a);
+  } else if (sw) {
+    hipLaunchKernelGGL((mbv2_x3_kernel<S, TO, CINP, HIDP, COUTP, EXPAND, RES, STEM, 4, true>), grid, dim3(256), 0, s, a);
+  } else {
+    hipLaunchKernelGGL((mbv2_x3_kernel<S, TO, CINP, HIDP, COUTP, EXPAND, RES, STEM, 4, false>), grid, dim3(256), 0, s, a);
+  }
   MEC_LAUNCH_CHECK();
   return 0;
 }
@@ -550,7 +593,8 @@ int dispatch_x3_block(const MbBlock& b, const MbX3Args& a, int B, int stem_c, hi
   MX_CASE(1, 7, 96, 576, 96, true)     // 96 -> 96 @ 14
   MX_CASE(2, 7, 96, 576, 160, false)   // 96 -> 160, 14 -> 7
   MX_CASE(1, 7, 160, 960, 160, true)   // 160 -> 160 @ 7
-  MX_CASE(1, 7, 160, 960, 320, false)  // 160 -> 320 @ 7
+  // (160 -> 320 @ 7, features[17], always runs layered: fused, its 20 project fragments of 16 channels
+  // (acc and hi / lo weights: 200 registers) spill at any occupancy)
 #undef MX_CASE
   set_error("mbv2 x3: no kernel instance for this block shape");
   return -1;
@@ -779,12 +823,11 @@ int MobileNetModel::forward_x3(const uint8_t* img, int B, int H, int W, int C, f
               "image_mbv2: fp32x3 weights missing");
   const bool fer = (H == 48 && W == 48 && C == 1);
   // layered tail: blocks[l0 ..] (features[l0 + 1 ..]) as expand GEMM -> depthwise -> project GEMM
-  size_t l0 = blocks.size();
-  if (opt().mbv2_layered) {
-    l0 = (size_t)opt().mbv2_layered - 1;
-    for (size_t i = l0; i < blocks.size(); ++i)
-      MEC_REQUIRE(blocks[i].lwe_off, "mbv2 x3: mbv2_layered names a block without a layered form");
-  }
+  // (features[17], 160 -> 320, is layered at every setting: dispatch_x3_block has no fused form of it)
+  size_t l0 = blocks.size() - 1;
+  if (opt().mbv2_layered) l0 = std::min(l0, (size_t)opt().mbv2_layered - 1);
+  for (size_t i = l0; i < blocks.size(); ++i)
+    MEC_REQUIRE(blocks[i].lwe_off, "mbv2 x3: mbv2_layered names a block without a layered form");
   // per-image element counts of the layered buffers: E (f32), D / block-I/O planes (halfs per plane)
   size_t pe = 0, pd = 0, pp = 0;
   {
@@ -801,8 +844,8 @@ int MobileNetModel::forward_x3(const uint8_t* img, int B, int H, int W, int C, f
     }
   }
   const size_t per_big = (size_t)112 * 112 * 16;  // largest block output (features[1]), floats
-  const size_t per_last = (size_t)49 * 1280, per_in = (size_t)49 * 320;
-  const size_t per_img = 224 * 224 + (2 * per_big + per_last + 1280) * sizeof(float) + per_in * 2 * sizeof(f16) +
+  const size_t per_last = (size_t)49 * 1280;
+  const size_t per_img = 224 * 224 + (2 * per_big + per_last + 1280) * sizeof(float) +
                          pe * sizeof(float) + (pd + 2 * pp) * 2 * sizeof(f16);
   const size_t need = per_img * (size_t)B + 8192;
   if (ws.bytes < need) MEC_TRY(ws.ensure(need));
@@ -813,7 +856,6 @@ int MobileNetModel::forward_x3(const uint8_t* img, int B, int H, int W, int C, f
   float* Y = reinterpret_cast<float*>(p); p += (size_t)B * per_big * sizeof(float);
   float* Lst = reinterpret_cast<float*>(p); p += (size_t)B * per_last * sizeof(float);
   float* pooled = reinterpret_cast<float*>(p); p += (size_t)B * 1280 * sizeof(float);
-  f16* Lin = reinterpret_cast<f16*>(p); p += (size_t)B * per_in * 2 * sizeof(f16);  // features[18]'s A planes
   float* Eb = reinterpret_cast<float*>(p); p += (size_t)B * pe * sizeof(float);
   const long long dlo = (long long)B * pd, plo = (long long)B * pp;  // plane offsets (halfs)
   f16* Db = reinterpret_cast<f16*>(p); p += (size_t)B * pd * 2 * sizeof(f16);
@@ -888,18 +930,8 @@ int MobileNetModel::forward_x3(const uint8_t* img, int B, int H, int W, int C, f
   }
   MEC_TRY(prof.end(TAG_MBV2_BLOCK, s));
   {  // features[18] 1x1 320 -> 1280 + BN + ReLU6 on the split GEMM engine
-    const size_t n4 = (size_t)B * h * h * 320 / 4;
-    long long llo = (long long)B * h * h * 320;
-    const f16* A = Lin;
-    if (l0 < blocks.size()) {  // the layered tail's planes (320 channels: no padding)
-      A = pin;
-      llo = plo;
-    } else {
-      hipLaunchKernelGGL(mbv2_split_kernel, dim3((unsigned)((n4 + 255) / 256)), dim3(256), 0, s,
-                         reinterpret_cast<const float*>(cur), n4, std::ldexp(1.0f, blocks.back().x3_s_out), Lin, llo,
-                         range_flag());
-      MEC_LAUNCH_CHECK();
-    }
+    const f16* A = pin;  // the layered tail's planes (320 channels: no padding)
+    const long long llo = plo;
     GemmParams g;
     g.split = 1; g.A = A; g.a_lo = llo; g.B = Wt + last_w_off; g.b_lo = wlo; g.oscale = x3_scale.back();
     g.bias = P + last_b_off; g.act = ACT_RELU6; g.C32 = Lst;
