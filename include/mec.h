@@ -192,6 +192,9 @@ int mec_conv_f32(const float* x, const float* w, const float* bias, const float*
  *                          allocated for (4: 128 VGPRs with an 84-B spill, 3: 168 VGPRs); same bits
  *   "mbv2_x3_sesw" 0|[1]   fp32x3 MobileNetV2 fused blocks: the expanded chunk's rows chunk-swizzled per tile
  *                          shape (fewer LDS bank conflicts on the depthwise reads) or unswizzled; same bits
+ *   "x3_plane_scale" 0|[1] fp32x3 activation-plane scales, read at mec_create_ex (set it as the process
+ *                          default first): 1 = per-tensor power-of-two exponents (the envelope above),
+ *                          0 = unscaled planes (A/B only: narrower envelope, different bits)
  *   "mbv2_layered" 0|7..17 [8]  fp32x3 MobileNetV2: features[k..17] as expand GEMM -> depthwise -> project GEMM
  *                          (0: every block fused but features[17], layered at every setting)
  *   "mbv2_layered16" 0|7..17 [8]  the same on the f16 path

@@ -1055,8 +1055,10 @@ int TextModel::create(const float* blob, size_t n) {
       }
       return mx;
     };
+    // opts.x3_plane_scale 0: every exponent 0 (the unscaled planes, A/B only)
+    auto aexp = [&](double b, double t) { return opts.x3_plane_scale ? activation_exp(b, t) : 0; };
     double b_in = ln_bound(lg, lb);
-    x3_s_emb = activation_exp(b_in, kX3BoundTarget);
+    x3_s_emb = aexp(b_in, kX3BoundTarget);
     std::vector<int> s_in(BLAYERS);
     x3_s_ln1.assign(BLAYERS, 0);
     x3_s_ln2.assign(BLAYERS, 0);
@@ -1071,13 +1073,13 @@ int TextModel::create(const float* blob, size_t n) {
       s_in[l] = l ? x3_s_ln2[l - 1] : x3_s_emb;
       int sqkv[3];
       for (int q = 0; q < 3; ++q)
-        sqkv[q] = activation_exp(proj_bound(b_in, wl + (size_t)q * BH * BH, pl + q * BH, BH, BH), kX3BoundTarget);
+        sqkv[q] = aexp(proj_bound(b_in, wl + (size_t)q * BH * BH, pl + q * BH, BH, BH), kX3BoundTarget);
       const double b1 = ln_bound(pl + 3072, pl + 3840);
-      x3_s_ln1[l] = activation_exp(b1, kX3BoundTarget);
+      x3_s_ln1[l] = aexp(b1, kX3BoundTarget);
       x3_s_ffn[l] =
-          activation_exp(proj_bound(b1, wl + (size_t)2304 * BH + BH * BH, pl + 4608, BI, BH), kX3BoundTarget);
+          aexp(proj_bound(b1, wl + (size_t)2304 * BH + BH * BH, pl + 4608, BI, BH), kX3BoundTarget);
       b_in = ln_bound(pl + 8448, pl + 9216);
-      x3_s_ln2[l] = activation_exp(b_in, kX3BoundTarget);
+      x3_s_ln2[l] = aexp(b_in, kX3BoundTarget);
       x3_s_q[l] = sqkv[0];
       x3_s_k[l] = sqkv[1];
       x3_s_v[l] = sqkv[2];

@@ -260,13 +260,19 @@ __device__ __forceinline__ void gemm_epilogue(const GemmParams& p, accv (&acc)[T
       if (row < M && (!NOSTORE || v[0] == 1234.5f)) {
         const size_t base = (size_t)row * N + col0;
         if (p.C16 && p.c_lo) {  // split output: planes of v * cscale, the lo plane carries the rest
+          float u[8];
+#pragma unroll
+          for (int q = 0; q < 8; ++q) u[q] = v[q];
+          if (p.cscale != 1.f) {  // (a uniform branch: most split outputs carry their scale in the bias)
+#pragma unroll
+            for (int q = 0; q < 8; ++q) u[q] *= p.cscale;
+          }
           half8 h, l;
 #pragma unroll
           for (int q = 0; q < 8; ++q) {
-            const float u = v[q] * p.cscale;
-            h[q] = (f16)u;
-            l[q] = (f16)(u - (float)h[q]);
-            x3bad |= x3_out_of_range(u);
+            h[q] = (f16)u[q];
+            l[q] = (f16)(u[q] - (float)h[q]);
+            x3bad |= x3_out_of_range(u[q]);
           }
           *reinterpret_cast<half8*>(p.C16 + base) = h;
           *reinterpret_cast<half8*>(p.C16 + p.c_lo + base) = l;

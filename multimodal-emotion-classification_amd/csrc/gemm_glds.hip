@@ -490,13 +490,17 @@ __device__ __forceinline__ void pp_epilogue(const GemmParams& p, floatx4 (&acc)[
       if (row < M && (!NOSTORE || v[0] == 1234.5f)) {
         const size_t base = (size_t)row * N + col;
         if (p.C16 && p.c_lo) {  // split output: planes of v * cscale, the lo plane carries the rest
+          float u[4] = {v[0], v[1], v[2], v[3]};
+          if (p.cscale != 1.f) {  // (a uniform branch: most split outputs carry their scale in the bias)
+#pragma unroll
+            for (int e = 0; e < 4; ++e) u[e] *= p.cscale;
+          }
           half4 h, l;
 #pragma unroll
           for (int e = 0; e < 4; ++e) {
-            const float u = v[e] * p.cscale;
-            h[e] = (f16)u;
-            l[e] = (f16)(u - (float)h[e]);
-            x3bad |= x3_out_of_range(u);
+            h[e] = (f16)u[e];
+            l[e] = (f16)(u[e] - (float)h[e]);
+            x3bad |= x3_out_of_range(u[e]);
           }
           *reinterpret_cast<half4*>(p.C16 + base) = h;
           *reinterpret_cast<half4*>(p.C16 + p.c_lo + base) = l;

@@ -117,6 +117,10 @@ struct Options {
   // fp32x3 MobileNetV2 4x4-tile (stride-2) fused blocks: workgroups per CU their registers are allocated for
   // (4: 128 VGPRs and an 84-B spill per lane; 3: 168 VGPRs, no spill); same bits
   int mbv2_x3_occ = 3;
+  // fp32x3 activation-plane scales (models.h activation_exp), read when a handle is created: 1 = per-tensor
+  // exponents from bounds / BN estimates, 0 = every exponent 0 (round 4's unscaled planes; A/B only: small
+  // activations then lose bits to the f16 subnormals, large ones overflow)
+  int x3_plane_scale = 1;
   // fp32x3 MobileNetV2 fused blocks: the expanded chunk's f32 rows with a per-tile-shape 16-B chunk swizzle
   // (1; fewer LDS bank conflicts on the depthwise reads) or unswizzled 36-float rows (0); same bits
   int mbv2_x3_sesw = 1;

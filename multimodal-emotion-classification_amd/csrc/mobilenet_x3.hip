@@ -137,17 +137,17 @@ __global__ __launch_bounds__(256, OCC) void mbv2_x3_kernel(const MbX3Args a) {
   }
   if (tid < COUTP / 4) reinterpret_cast<float4*>(sBp)[tid] = reinterpret_cast<const float4*>(a.bp)[tid];
 
-  // expand weights of the first chunk (A fragments, rows = hidden channels), hi and lo planes
-  half8 afh[2][KX], afl[2][KX];
+  // expand weights of a chunk (A fragments, rows = hidden channels), hi and lo planes: each wave computes
+  // one 16-channel half of the chunk (ht = wave & 1) for every other 16-pixel tile, so it loads that half
+  const int eht = wave & 1;
+  half8 afh[KX], afl[KX];
   auto load_af = [&](int h0) {
 #pragma unroll
-    for (int ht = 0; ht < 2; ++ht)
-#pragma unroll
-      for (int k = 0; k < KX; ++k) {
-        const size_t o = (size_t)(h0 + 16 * ht + l16) * CINP + 32 * k + 8 * lq;
-        afh[ht][k] = *reinterpret_cast<const half8*>(a.We + o);
-        afl[ht][k] = *reinterpret_cast<const half8*>(a.We + a.we_lo + o);
-      }
+    for (int k = 0; k < KX; ++k) {
+      const size_t o = (size_t)(h0 + 16 * eht + l16) * CINP + 32 * k + 8 * lq;
+      afh[k] = *reinterpret_cast<const half8*>(a.We + o);
+      afl[k] = *reinterpret_cast<const half8*>(a.We + a.we_lo + o);
+    }
   };
   // block input tile t (+ halo) -> registers: zeros outside the image and past cin
   constexpr int C4 = CINP / 4;
@@ -264,51 +264,48 @@ __global__ __launch_bounds__(256, OCC) void mbv2_x3_kernel(const MbX3Args a) {
 
 #pragma unroll 1
   for (int h0 = 0; h0 < HIDP; h0 += MX_HC) {
-    // project weights of this chunk (hi and lo): in flight during expand + depthwise
+    // project weights of this chunk (hi and lo): in flight during expand + depthwise; only the waves that
+    // project load them (a 4x4 tile's 16 pixels: wave 0 alone)
     half8 pfh[OT], pfl[OT];
+    if (16 * wave < NDR) {
 #pragma unroll
-    for (int o = 0; o < OT; ++o) {
-      const size_t off = (size_t)(16 * o + l16) * HIDP + h0 + 8 * lq;
-      pfh[o] = *reinterpret_cast<const half8*>(a.Wp + off);
-      pfl[o] = *reinterpret_cast<const half8*>(a.Wp + a.wp_lo + off);
+      for (int o = 0; o < OT; ++o) {
+        const size_t off = (size_t)(16 * o + l16) * HIDP + h0 + 8 * lq;
+        pfh[o] = *reinterpret_cast<const half8*>(a.Wp + off);
+        pfl[o] = *reinterpret_cast<const half8*>(a.Wp + a.wp_lo + off);
+      }
     }
     const float* src;  // fp32 depthwise input for this chunk: row p at src + p * sld
     int sld;
     if constexpr (EXPAND) {
       // E^T[h][p] = sum_c We[h0+h][c] X[p][c] (A = weights, B = X^T: a lane ends with 4 consecutive
-      // hidden channels of one pixel); per 32-deep k chunk the split engine's terms lo.hi, hi.lo, hi.hi
-      float eb[2][4];
+      // hidden channels of one pixel); per 32-deep k chunk the split engine's terms lo.hi, hi.lo, hi.hi.
+      // The (16-pixel tile, 16-channel half) units go round the waves: wave w takes half w & 1 of tiles
+      // (w >> 1), (w >> 1) + 2, ... (a 9x9 input tile's six pixel tiles: three units per wave, not 4-4-2-2)
+      float eb[4];
 #pragma unroll
-      for (int ht = 0; ht < 2; ++ht)
-#pragma unroll
-        for (int e = 0; e < 4; ++e) eb[ht][e] = sBe[h0 + 16 * ht + 4 * lq + e];
-      for (int pt = wave; pt < MP / 16; pt += 4) {
+      for (int e = 0; e < 4; ++e) eb[e] = sBe[h0 + 16 * eht + 4 * lq + e];
+      for (int pt = wave >> 1; pt < MP / 16; pt += 2) {
         const int p = pt * 16 + l16;
         const int py = p / IR, px = p - (p / IR) * IR;
         const int iy = iy0 + py, ix = ix0 + px;
         const bool valid = p < NP && iy >= 0 && iy < H && ix >= 0 && ix < H;
-        floatx4 e2[2] = {floatx4{0.f, 0.f, 0.f, 0.f}, floatx4{0.f, 0.f, 0.f, 0.f}};
+        floatx4 e2 = {0.f, 0.f, 0.f, 0.f};
 #pragma unroll
         for (int k = 0; k < KX; ++k) {
           const int xo = p * XLD + mx_sw<CINP / 8>(p, 4 * k + lq) * 8;
           const half8 bh = *reinterpret_cast<const half8*>(sXh + xo);
           const half8 bl = *reinterpret_cast<const half8*>(sXl + xo);
-#pragma unroll
-          for (int ht = 0; ht < 2; ++ht) {
-            e2[ht] = __builtin_amdgcn_mfma_f32_16x16x32_f16(afl[ht][k], bh, e2[ht], 0, 0, 0);
-            e2[ht] = __builtin_amdgcn_mfma_f32_16x16x32_f16(afh[ht][k], bl, e2[ht], 0, 0, 0);
-            e2[ht] = __builtin_amdgcn_mfma_f32_16x16x32_f16(afh[ht][k], bh, e2[ht], 0, 0, 0);
-          }
+          e2 = __builtin_amdgcn_mfma_f32_16x16x32_f16(afl[k], bh, e2, 0, 0, 0);
+          e2 = __builtin_amdgcn_mfma_f32_16x16x32_f16(afh[k], bl, e2, 0, 0, 0);
+          e2 = __builtin_amdgcn_mfma_f32_16x16x32_f16(afh[k], bh, e2, 0, 0, 0);
         }
-#pragma unroll
-        for (int ht = 0; ht < 2; ++ht) {
-          float4 ev;
-          ev.x = valid ? relu6x(__builtin_fmaf(e2[ht][0], a.we_scale, eb[ht][0])) : 0.f;  // dw zero pad
-          ev.y = valid ? relu6x(__builtin_fmaf(e2[ht][1], a.we_scale, eb[ht][1])) : 0.f;
-          ev.z = valid ? relu6x(__builtin_fmaf(e2[ht][2], a.we_scale, eb[ht][2])) : 0.f;
-          ev.w = valid ? relu6x(__builtin_fmaf(e2[ht][3], a.we_scale, eb[ht][3])) : 0.f;
-          *reinterpret_cast<float4*>(sE + p * EF + ((4 * ht + lq) ^ se_sw<G::SEL>(p)) * 4) = ev;
-        }
+        float4 ev;
+        ev.x = valid ? relu6x(__builtin_fmaf(e2[0], a.we_scale, eb[0])) : 0.f;  // dw zero pad
+        ev.y = valid ? relu6x(__builtin_fmaf(e2[1], a.we_scale, eb[1])) : 0.f;
+        ev.z = valid ? relu6x(__builtin_fmaf(e2[2], a.we_scale, eb[2])) : 0.f;
+        ev.w = valid ? relu6x(__builtin_fmaf(e2[3], a.we_scale, eb[3])) : 0.f;
+        *reinterpret_cast<float4*>(sE + p * EF + ((4 * eht + lq) ^ se_sw<G::SEL>(p)) * 4) = ev;
       }
       if (h0 + MX_HC < HIDP) load_af(h0 + MX_HC);  // next chunk's expand weights: in flight during dw + project
       __syncthreads();
@@ -320,7 +317,34 @@ __global__ __launch_bounds__(256, OCC) void mbv2_x3_kernel(const MbX3Args a) {
     }
 
     // ---- depthwise 3x3/S + BN + ReLU6 (fp32) -> sDh / sDl planes [q][h]
-    {
+    if constexpr (EXPAND && NQ == 16 && NDR == 16) {
+      // a 4x4 tile: its 16 pixels x 32 channels over all 256 threads (pixel tid >> 4, channels 2 (tid & 15)
+      // and + 1), so no wave waits at the next barrier for one wave's depthwise; each channel's FMAs in the
+      // same (ky, kx) order from the shift as below (the same bits)
+      const int q = tid >> 4, cp = tid & 15;
+      const int p0 = ((q >> 2) * S) * IR + (q & 3) * S;
+      const int hc = h0 + 2 * cp;
+      float d0 = sBd[hc], d1 = sBd[hc + 1];
+      const float* wd = wdsrc + (size_t)(hc / 8) * 72 + (hc & 7);
+#pragma unroll
+      for (int ky = 0; ky < 3; ++ky)
+#pragma unroll
+        for (int kx = 0; kx < 3; ++kx) {
+          const int pp = p0 + ky * IR + kx;
+          const float2 e = *reinterpret_cast<const float2*>(sE + pp * EF + ((cp >> 1) ^ se_sw<G::SEL>(pp)) * 4 +
+                                                            (cp & 1) * 2);
+          const float2 w = *reinterpret_cast<const float2*>(wd + (ky * 3 + kx) * 8);
+          d0 = __builtin_fmaf(e.x, w.x, d0);
+          d1 = __builtin_fmaf(e.y, w.y, d1);
+        }
+      const float v0 = relu6x(d0) * kDwUp, v1 = relu6x(d1) * kDwUp;  // in [0, 6 2^13]
+      typedef _Float16 h2 __attribute__((ext_vector_type(2)));
+      const h2 hh = {(f16)v0, (f16)v1};
+      const h2 hl = {(f16)(v0 - (float)hh[0]), (f16)(v1 - (float)hh[1])};
+      const int dof = q * ELD + mx_sw<MX_HC / 8>(q, cp >> 2) * 8 + (cp & 3) * 2;
+      *reinterpret_cast<h2*>(sDh + dof) = hh;
+      *reinterpret_cast<h2*>(sDl + dof) = hl;
+    } else {
       half8 oh = {0, 0, 0, 0, 0, 0, 0, 0}, ol = {0, 0, 0, 0, 0, 0, 0, 0};
       if (dq < NQ) {
         const int hc = h0 + 8 * dcg;
@@ -775,6 +799,8 @@ int MobileNetModel::create_x3(const float* blob, size_t n) {
   // along the residual chain. Block inputs are the previous stage's planes; the depthwise outputs are at
   // kDwUp. Every epilogue scale below folds in 2^(s_out - s_in) (the fused blocks' and the expand GEMMs'
   // outputs are f32: s_out = 0 there).
+  // opts.x3_plane_scale 0: every exponent 0 (the unscaled planes, A/B only)
+  auto aexp = [&](double b, double t) { return opts.x3_plane_scale ? activation_exp(b, t) : 0; };
   {
     int s_prev = 0;
     for (size_t b0 = 0; b0 < blocks.size();) {
@@ -785,7 +811,7 @@ int MobileNetModel::create_x3(const float* blob, size_t n) {
         e = blocks[i].x3_est + (i > b0 ? e : 0.0);
         e_max = std::max(e_max, e);
       }
-      const int st = activation_exp(e_max, kX3EstimateTarget);
+      const int st = aexp(e_max, kX3EstimateTarget);
       for (size_t i = b0; i < b1; ++i) {
         blocks[i].x3_s_in = i == b0 ? s_prev : st;
         blocks[i].x3_s_out = st;

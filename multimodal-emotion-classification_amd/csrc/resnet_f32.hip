@@ -487,7 +487,9 @@ int ImageModel::create_f32(const float* blob, size_t n) {
     // add commute with the power of two: the f32 values are the unscaled ones times 2^s_out exactly).
     // The downsample of a stage's first block reads the block input (s_in) beside conv3's T2 (s_t2)
     // in one dual GEMM: its weights are pre-scaled by 2^(s_t2 - s_in) so both halves of K carry 2^s_t2.
-    stem.x3_s = activation_exp(stem.x3_est, kX3EstimateTarget);
+    // opts.x3_plane_scale 0: every exponent 0 (the unscaled planes, A/B only)
+    auto aexp = [&](double b, double t) { return opts.x3_plane_scale ? activation_exp(b, t) : 0; };
+    stem.x3_s = aexp(stem.x3_est, kX3EstimateTarget);
     {
       int s_prev = stem.x3_s;
       double e_stream = stem.x3_est;
@@ -500,11 +502,11 @@ int ImageModel::create_f32(const float* blob, size_t n) {
           e_stream = bk.c3.x3_est + (bk.has_ds ? bk.ds.x3_est : e_stream);
           e_max = std::max(e_max, e_stream);
         }
-        const int s_stage = activation_exp(e_max, kX3EstimateTarget);
+        const int s_stage = aexp(e_max, kX3EstimateTarget);
         for (size_t bi = b0; bi < b1; ++bi) {
           Bottleneck& bk = blocks[bi];
-          bk.c1.x3_s = activation_exp(bk.c1.x3_est, kX3EstimateTarget);
-          bk.c2.x3_s = activation_exp(bk.c2.x3_est, kX3EstimateTarget);
+          bk.c1.x3_s = aexp(bk.c1.x3_est, kX3EstimateTarget);
+          bk.c2.x3_s = aexp(bk.c2.x3_est, kX3EstimateTarget);
           bk.c3.x3_s = s_stage;
           bk.x3_s_in = bi == b0 ? s_prev : s_stage;
         }

@@ -33,9 +33,15 @@ def main():
     ap.add_argument('--precision', default='f16', choices=['f16', 'fp32', 'fp32x3'])
     ap.add_argument('--save', help='write the first value\'s outputs to this .npz (cross-build bit comparisons, '
                                    'with MEC_LIB naming the other build)')
+    ap.add_argument('--set', action='append', default=[], metavar='KEY=VALUE',
+                    help='process-default option set before the handles are created (creation-time knobs such '
+                         'as x3_plane_scale)')
     a = ap.parse_args()
     dev = torch.device('cuda', 0)
     lib = _lib.load()
+    for kv in a.set:
+        k, v = kv.split('=')
+        _lib.check(lib.mec_set_option(k.encode(), int(v)), f'mec_set_option {kv}')
     if a.enc == 'pipeline':  # the bench step: speech + text + image + fusion on three streams
         m = engine.FusedPipeline(seed=1234, device=dev, precision=a.precision)
         ids, mask = syn.text_inputs(256, 128, seed=0)

@@ -10,7 +10,7 @@ tail -2 gpurun_out/r05_ab_mbv2x3_sesw.txt
 timeout -k 10 300 python -u tools/ab_option.py --enc image_mbv2 --precision fp32x3 --opt mbv2_x3_occ --values 3 4 \
   --rounds 7 > gpurun_out/r05_ab_mbv2x3_occ2.txt 2>&1 || exit $?
 tail -2 gpurun_out/r05_ab_mbv2x3_occ2.txt
-for e in text image pipeline; do
+for e in image_mbv2 text image pipeline; do
   ENC=$e PREC=fp32x3 ROUNDS=3 bash tools/gpu_ab_lib.sh > gpurun_out/r05_ab_lib_r04_$e.txt 2>&1 || exit $?
   tail -7 gpurun_out/r05_ab_lib_r04_$e.txt
 done
