@@ -192,6 +192,9 @@ int mec_conv_f32(const float* x, const float* w, const float* bias, const float*
  *                          allocated for (4: 128 VGPRs with an 84-B spill, 3: 168 VGPRs); same bits
  *   "mbv2_x3_sesw" 0|[1]   fp32x3 MobileNetV2 fused blocks: the expanded chunk's rows chunk-swizzled per tile
  *                          shape (fewer LDS bank conflicts on the depthwise reads) or unswizzled; same bits
+ *   "gemm_x3_restage" [0]|1|2 K-interleaved split tiles with 2 stages: refill a stage for k step t + 2 once
+ *                          every wave holds step t's fragments (two steps in flight) in every A mode (1), in the
+ *                          convs only (2), or never (0: after step t's barrier); same bits
  *   "x3_plane_scale" 0|[1] fp32x3 activation-plane scales, read at mec_create_ex (set it as the process
  *                          default first): 1 = per-tensor power-of-two exponents (the envelope above),
  *                          0 = unscaled planes (A/B only: narrower envelope, different bits)

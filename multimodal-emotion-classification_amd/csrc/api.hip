@@ -311,6 +311,7 @@ int set_option(Options& o, const std::string& k, int value) {
   if (k == "mbv2_x3_occ" && (value == 3 || value == 4)) { o.mbv2_x3_occ = value; return 0; }
   if (k == "mbv2_x3_sesw" && (value == 0 || value == 1)) { o.mbv2_x3_sesw = value; return 0; }
   if (k == "x3_plane_scale" && (value == 0 || value == 1)) { o.x3_plane_scale = value; return 0; }
+  if (k == "gemm_x3_restage" && value >= 0 && value <= 2) { o.gemm_x3_restage = value; return 0; }
   if (k == "mbv2_layered" && (value == 0 || (value >= 7 && value <= 17))) { o.mbv2_layered = value; return 0; }
   if (k == "mbv2_layered16" && (value == 0 || (value >= 7 && value <= 17))) { o.mbv2_layered16 = value; return 0; }
   if (k == "conv3x3_direct" && (value == 0 || value == 1)) { o.conv3x3_direct = value; return 0; }

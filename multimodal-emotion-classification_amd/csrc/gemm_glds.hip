@@ -30,7 +30,7 @@ namespace mec {
 __device__ __attribute__((aligned(64))) uint4 g_zero_page[16];
 
 template <int BM, int BN, int WM, int WN, int NS, int AM, int DBG = 0, int MF = 32, int BK = 64, int PRE = 0,
-          int ACT = -1, int SP = 0>
+          int ACT = -1, int SP = 0, int ER = 0>
 __global__ __launch_bounds__(64 * WM * WN, (WM * WN == 4) ? 2 : 1) void gemm_glds_kernel(const GemmParams p) {
   // MF: 32 = v_mfma_f32_32x32x16_f16 tiles, 16 = v_mfma_f32_16x16x32_f16 tiles
   // DBG (probe builds only): 1 = no operand loads inside the K loop, 2 = no epilogue
@@ -47,6 +47,11 @@ __global__ __launch_bounds__(64 * WM * WN, (WM * WN == 4) ? 2 : 1) void gemm_gld
   static_assert(BK == 64 || BK == 32, "BK");
   static_assert(SP == 0 || PRE == 0 || PRE == 3, "split operands: split residual prefetch only");
   static_assert(SP != 2 || MF == 16, "interleaved split: 16x16x32 tiles only");
+  // ER (early restage, opt().gemm_x3_restage; interleaved split tiles with a 2-stage ring and 32-deep stages):
+  // each k step reads its whole stage into fragment registers first, so once every wave holds them the
+  // stage is refilled with k step t + 2 while step t's MFMAs run -- two steps in flight on two buffers
+  // instead of one (bert_qkv_attn_x3_kernel's schedule). Same fragments, same MFMA order: same bits.
+  constexpr bool ERS = ER != 0 && SP == 2 && NS == 2 && BK == 32 && DBG == 0;
   constexpr int CH = BK / 8;                   // 16-B chunks per LDS row
   constexpr int RPI = 64 / CH;                 // rows per glds wave-instruction (1 KB)
   constexpr int NW = WM * WN;
@@ -209,10 +214,55 @@ __global__ __launch_bounds__(64 * WM * WN, (WM * WN == 4) ? 2 : 1) void gemm_gld
 
   const int nk = SP == 1 ? 3 * nk0 : nk0;
 #pragma unroll
-  for (int s = 0; s < NS - 1; ++s)
+  for (int s = 0; s < (ERS ? 2 : NS - 1); ++s)
     if (s < nk) issue(s, s);
 
   const int lr = lane & 31, lh = lane >> 5;
+  if constexpr (ERS) {
+    const int l16 = lane & 15, lq = lane >> 4;
+    for (int t = 0; t < nk; ++t) {
+      if (t + 1 < nk) wait_vm<LPT>();  // step t landed; step t + 1 may stay in flight
+      else wait_vm<0>();
+      __builtin_amdgcn_s_barrier();
+      asm volatile("" ::: "memory");
+      const f16* sA = smem + (t & 1) * STAGE;
+      const f16* sB = sA + BM * BK;
+      half8 af[2][TI], bf[2][TJ];  // [plane: 0 hi, 1 lo]
+#pragma unroll
+      for (int h = 0; h < 2; ++h) {
+#pragma unroll
+        for (int i = 0; i < TI; ++i) {
+          const int r = wm * TM + i * 16 + l16;
+          af[h][i] = *reinterpret_cast<const half8*>(sA + h * HALF + r * BK + sw<BK>(r, lq) * 8);
+        }
+#pragma unroll
+        for (int j = 0; j < TJ; ++j) {
+          const int r = wn * TN + j * 16 + l16;
+          bf[h][j] = *reinterpret_cast<const half8*>(sB + h * HALF + r * BK + sw<BK>(r, lq) * 8);
+        }
+      }
+      __builtin_amdgcn_sched_barrier(0);
+      asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+      __builtin_amdgcn_s_barrier();  // every wave holds its fragments: the stage is free
+      if (t + 2 < nk) issue(t & 1, t + 2);
+      __builtin_amdgcn_sched_barrier(0);
+#pragma unroll
+      for (int i = 0; i < TI; ++i)
+#pragma unroll
+        for (int j = 0; j < TJ; ++j)
+          acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_f16(af[1][i], bf[0][j], acc[i][j], 0, 0, 0);
+#pragma unroll
+      for (int i = 0; i < TI; ++i)
+#pragma unroll
+        for (int j = 0; j < TJ; ++j)
+          acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_f16(af[0][i], bf[1][j], acc[i][j], 0, 0, 0);
+#pragma unroll
+      for (int i = 0; i < TI; ++i)
+#pragma unroll
+        for (int j = 0; j < TJ; ++j)
+          acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_f16(af[0][i], bf[0][j], acc[i][j], 0, 0, 0);
+    }
+  } else
   for (int t = 0; t < nk; ++t) {
     // tile t must have landed; tiles t+1..t+ahead (issued) may stay in flight
     const int ahead = min(nk - 1 - t, NS - 2);
@@ -746,19 +796,30 @@ __global__ __launch_bounds__(512) void gemm_pp_kernel(const GemmParams p) {
 
 // BM=256 tiles: (BN, WM, WN, NS)
 
+// K-interleaved split operands (16x16x32, 32-deep stages) in each A mode; ER = the early-restage schedule
+template <int BM, int BN, int WM, int WN, int NS, int BK, int ER>
+static int launch_x3i(const GemmParams& p, hipStream_t s, int nwg, dim3 blk) {
+  if (BM * BN <= 128 * 128 && opt().gemm_prefetch_r && p.amode == A_PLAIN && p.R && p.r_lo && p.K <= 512) {
+    if constexpr (BM * BN <= 128 * 128)
+      hipLaunchKernelGGL((gemm_glds_kernel<BM, BN, WM, WN, NS, A_PLAIN, 0, 16, BK, 3, -1, 2, ER>), dim3(nwg), blk, 0, s, p);
+  } else if (p.amode == A_PLAIN)
+    hipLaunchKernelGGL((gemm_glds_kernel<BM, BN, WM, WN, NS, A_PLAIN, 0, 16, BK, 0, -1, 2, ER>), dim3(nwg), blk, 0, s, p);
+  else if (p.amode == A_CONV)
+    hipLaunchKernelGGL((gemm_glds_kernel<BM, BN, WM, WN, NS, A_CONV, 0, 16, BK, 0, -1, 2, ER>), dim3(nwg), blk, 0, s, p);
+  else
+    hipLaunchKernelGGL((gemm_glds_kernel<BM, BN, WM, WN, NS, A_DUAL, 0, 16, BK, 0, -1, 2, ER>), dim3(nwg), blk, 0, s, p);
+  MEC_LAUNCH_CHECK();
+  return 0;
+}
+
 template <int BM, int BN, int WM, int WN, int NS, int MF, int BK, int ACT>
 static int launch_cfg_act(const GemmParams& p, hipStream_t s, int nwg, dim3 blk) {
   if (p.split == 2) {  // split-f16 operands, K-interleaved terms (16x16x32 tiles only)
     if constexpr (MF == 16 && BK == 32 && 4 * (BM + BN) * BK * NS <= 160 * 1024) {
-      if (BM * BN <= 128 * 128 && opt().gemm_prefetch_r && p.amode == A_PLAIN && p.R && p.r_lo && p.K <= 512) {
-        if constexpr (BM * BN <= 128 * 128)
-          hipLaunchKernelGGL((gemm_glds_kernel<BM, BN, WM, WN, NS, A_PLAIN, 0, MF, BK, 3, -1, 2>), dim3(nwg), blk, 0, s, p);
-      } else if (p.amode == A_PLAIN)
-        hipLaunchKernelGGL((gemm_glds_kernel<BM, BN, WM, WN, NS, A_PLAIN, 0, MF, BK, 0, -1, 2>), dim3(nwg), blk, 0, s, p);
-      else if (p.amode == A_CONV)
-        hipLaunchKernelGGL((gemm_glds_kernel<BM, BN, WM, WN, NS, A_CONV, 0, MF, BK, 0, -1, 2>), dim3(nwg), blk, 0, s, p);
-      else
-        hipLaunchKernelGGL((gemm_glds_kernel<BM, BN, WM, WN, NS, A_DUAL, 0, MF, BK, 0, -1, 2>), dim3(nwg), blk, 0, s, p);
+      // ER: the early-restage schedule of the 2-stage tiles (opt().gemm_x3_restage; same bits)
+      if (NS == 2 && (opt().gemm_x3_restage == 1 || (opt().gemm_x3_restage == 2 && p.amode != A_PLAIN)))
+        return launch_x3i<BM, BN, WM, WN, NS, BK, 1>(p, s, nwg, blk);
+      return launch_x3i<BM, BN, WM, WN, NS, BK, 0>(p, s, nwg, blk);
     } else {
       set_error("gemm_glds: interleaved split operands need a 16x16x32 tile with 32-deep stages (tiles 7xxxx)");
       return -1;
@@ -797,6 +858,14 @@ static int launch_cfg(const GemmParams& p0, hipStream_t s) {
   const int nwg = ((p.M + BM - 1) / BM) * (p.N / BN);
   const dim3 blk(64 * WM * WN);
 #ifdef MEC_PROBES
+  // the K-interleaved split tile (the fp32x3 FFN1 roofline kernel) with no operand loads inside its K loop:
+  // MFMA + LDS fragment reads + epilogue only, so its time against the real kernel's prices the loads
+  if (opt().gemm_debug == 1 && p.split == 2 && BN == 256 && BM == 256 && p.amode == A_PLAIN) {
+    if constexpr (MF == 16 && BK == 32 && 4 * (BM + BN) * BK * NS <= 160 * 1024)
+      hipLaunchKernelGGL((gemm_glds_kernel<BM, BN, WM, WN, NS, A_PLAIN, 1, MF, BK, 0, -1, 2>), dim3(nwg), blk, 0, s, p);
+    MEC_LAUNCH_CHECK();
+    return 0;
+  }
   if (opt().gemm_debug && BN == 256 && BM == 256 && p.amode == A_PLAIN) {
     if (opt().gemm_debug == 1)
       hipLaunchKernelGGL((gemm_glds_kernel<BM, BN, WM, WN, NS, A_PLAIN, 1, MF, BK>), dim3(nwg), blk, 0, s, p);

@@ -144,6 +144,13 @@ struct Options {
   // MFMA, a higher held clock: text 18.84 -> 17.96 ms, ResNet50 10.06 -> 9.00, fused step 28.05 ->
   // 26.19 ms at B = 256 (profiles/r03_ab_x3order_*.txt)
   int gemm_x3_order = 1;
+  // K-interleaved split tiles with a 2-stage ring (70256, 71128, 71064, 70064): early restage (a stage is
+  // refilled for k step t + 2 as soon as every wave holds step t's fragments: two steps in flight) for
+  // 1 = every A mode, 2 = the implicit-GEMM convs only (ResNet), 0 = none (the ring refilled after the barrier
+  // of step t: one step in flight); same bits. Measured (same process, B = 256): ResNet50 alone gains up to
+  // 1 % (8.79 -> 8.71 ms), but the fused step loses 0.8 % (2) / 1.7 % (1) and BERT up to 0.9 %: 0 by default
+  // (profiles/r05_ab_restage_*.txt)
+  int gemm_x3_restage = 0;
   // K-interleaved split engine, per launch class: forced tile (7xxxx), 0 = autotune. BERT FFN1 is
   // pinned to 70256 by default: it and the other tiles time within a few % of each other alone, so an
   // autotune would flip between them run to run, and the bench's roofline kernel (and its PMC traffic
