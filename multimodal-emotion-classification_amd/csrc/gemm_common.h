@@ -91,6 +91,22 @@ __device__ __forceinline__ void wait_vm() {
   asm volatile("s_waitcnt vmcnt(%0)" ::"n"(N) : "memory");
 }
 
+// global_load_lds_dwordx4 (16 B per lane into LDS at m0 + 16 lane; counted on vmcnt) issued from asm.
+// The compiler models the builtin's LDS write as an LDS access through FLAT and counts it on lgkmcnt too:
+// while one is outstanding its LDS-read counting is out of order, so it drains every outstanding
+// ds_read (lgkmcnt(0)) before the first use of any fragment. Issued from asm, the load is invisible to
+// its counters and the fragment reads keep counted waits; the kernel waits for the load itself (wait_vm,
+// as before: vmcnt completes in order, so the compiler's own vmcnt waits only get stricter). m0 takes the
+// (uniform) LDS destination; a kernel that issues its loads through glds16 has no other m0 user.
+__device__ __forceinline__ void glds16(const void* src, lds_vptr dst) {
+#pragma clang diagnostic push
+#pragma clang diagnostic ignored "-Winline-asm"
+  asm volatile("s_mov_b32 m0, %1\n\ts_nop 0\n\tglobal_load_lds_dwordx4 %0, off" ::"v"(src),
+               "s"((unsigned)(size_t)dst)
+               : "memory", "m0");
+#pragma clang diagnostic pop
+}
+
 // Shared epilogue: accumulators (16x16x32 or 32x32x16 layout, wave tile (BM/WM)x(BN/WN))
 // -> bias, residual, activation -> C16 / C32. `smem` must be free (all waves past the
 // main loop's last LDS read).

@@ -133,7 +133,8 @@ __global__ __launch_bounds__(64 * WM * WN, (WM * WN == 4) ? 2 : 1) void gemm_gld
   const f16* zero = reinterpret_cast<const f16*>(g_zero_page);
 
   const int nk0 = K / BK;  // K tiles per pass
-  // one plane of K tile kt into stage `stage` (its half h): A at aoff, B at boff from the hi planes
+  // one plane of K tile kt into stage `stage` (its half h): A at aoff, B at boff from the hi planes (glds16:
+  // the fragment reads below keep counted lgkmcnt waits)
   auto issue_plane = [&](int stage, int kt, int h, long long aoff, long long boff) {
     const int k0 = kt * BK;
     f16* sA = smem + stage * STAGE + h * HALF;
@@ -142,14 +143,14 @@ __global__ __launch_bounds__(64 * WM * WN, (WM * WN == 4) ? 2 : 1) void gemm_gld
 #pragma unroll
       for (int i = 0; i < AI; ++i) {
         const f16* src = a_ok[i] ? a_src[i] + aoff + k0 : zero;
-        __builtin_amdgcn_global_load_lds((const void*)src, (lds_vptr)(sA + (wave * AI + i) * RPI * BK), 16, 0, 0);
+        glds16(src, (lds_vptr)(sA + (wave * AI + i) * RPI * BK));
       }
     } else if constexpr (AM == A_DUAL) {
       const bool first = k0 < p.K1;
 #pragma unroll
       for (int i = 0; i < AI; ++i) {  // split: both sources' lo planes at the same offset a_lo
         const f16* src = !a_ok[i] ? zero : (first ? a_src[i] + aoff + k0 : a2_src[i] + aoff + (k0 - p.K1));
-        __builtin_amdgcn_global_load_lds((const void*)src, (lds_vptr)(sA + (wave * AI + i) * RPI * BK), 16, 0, 0);
+        glds16(src, (lds_vptr)(sA + (wave * AI + i) * RPI * BK));
       }
     } else {
       const int tap = k0 / p.C;
@@ -161,13 +162,12 @@ __global__ __launch_bounds__(64 * WM * WN, (WM * WN == 4) ? 2 : 1) void gemm_gld
         const int ih = a_ih0[i] + kh, iw = a_iw0[i] + kw;
         const bool ok = a_ok[i] && ih >= 0 && ih < p.H && iw >= 0 && iw < p.W;
         const f16* src = ok ? a_src[i] + aoff + ((size_t)ih * p.W + iw) * p.C + c0 : zero;
-        __builtin_amdgcn_global_load_lds((const void*)src, (lds_vptr)(sA + (wave * AI + i) * RPI * BK), 16, 0, 0);
+        glds16(src, (lds_vptr)(sA + (wave * AI + i) * RPI * BK));
       }
     }
 #pragma unroll
     for (int j = 0; j < BI; ++j)
-      __builtin_amdgcn_global_load_lds((const void*)(b_src[j] + boff + k0), (lds_vptr)(sB + (wave * BI + j) * RPI * BK),
-                                       16, 0, 0);
+      glds16(b_src[j] + boff + k0, (lds_vptr)(sB + (wave * BI + j) * RPI * BK));
   };
   auto issue = [&](int stage, int kt) {
     if constexpr (SP == 1) {  // pass 0: A_lo . B_hi, pass 1: A_hi . B_lo, pass 2: A_hi . B_hi
@@ -310,29 +310,56 @@ __global__ __launch_bounds__(64 * WM * WN, (WM * WN == 4) ? 2 : 1) void gemm_gld
       }
     } else if constexpr (SP == 2) {
       // interleaved split: per 32-deep k chunk the hi and lo fragments of A and B, then the three
-      // terms term-major (each accumulator: lo.hi, hi.lo, hi.hi of the chunk, in that order)
+      // terms term-major (each accumulator: lo.hi, hi.lo, hi.hi of the chunk, in that order).
+      // The fragment reads go in two groups, each ahead of the terms that consume it: (B hi, A lo) for
+      // lo.hi, then (B lo, A hi) once the first I1 rows of lo.hi have their operands, so that no more than
+      // 15 LDS reads are ever outstanding. lgkmcnt is a 4-bit field: with all 2 (TI + TJ) reads issued at
+      // once (24 on the 256 x 256 tile) the compiler drains every one before the first MFMA, and the waves,
+      // in step after the barrier, leave the MFMAs idle while the LDS serves the whole stage. In groups,
+      // the second lands under the first's MFMAs. Same MFMAs in the same order per accumulator: same bits.
       const int l16 = lane & 15, lq = lane >> 4;
       constexpr int KS = BK / 32;
+      constexpr int GR = TI + TJ;  // reads per group
+      constexpr int I1 = 2 * GR <= 15 ? 0 : (TI + GR - 15 > 1 ? TI + GR - 15 : 1);
+      static_assert(GR <= 15 && I1 <= TI, "fragment read groups");
 #pragma unroll
       for (int s = 0; s < KS; ++s) {
         const int kcs = 4 * s + lq;
         half8 af[2][TI], bf[2][TJ];  // [plane: 0 hi, 1 lo]
-#pragma unroll
-        for (int h = 0; h < 2; ++h) {
+        auto read_a = [&](int h) {
 #pragma unroll
           for (int i = 0; i < TI; ++i) {
             const int r = wm * TM + i * 16 + l16;
             af[h][i] = *reinterpret_cast<const half8*>(sA + h * HALF + r * BK + sw<BK>(r, kcs) * 8);
           }
+        };
+        auto read_b = [&](int h) {
 #pragma unroll
           for (int j = 0; j < TJ; ++j) {
             const int r = wn * TN + j * 16 + l16;
             bf[h][j] = *reinterpret_cast<const half8*>(sB + h * HALF + r * BK + sw<BK>(r, kcs) * 8);
           }
+        };
+        read_b(0);
+        read_a(1);
+        if constexpr (I1 == 0) {
+          read_b(1);
+          read_a(0);
         }
         __builtin_amdgcn_sched_barrier(0);
+        if constexpr (I1 > 0) {
 #pragma unroll
-        for (int i = 0; i < TI; ++i)
+          for (int i = 0; i < I1; ++i)
+#pragma unroll
+            for (int j = 0; j < TJ; ++j)
+              acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_f16(af[1][i], bf[0][j], acc[i][j], 0, 0, 0);
+          __builtin_amdgcn_sched_barrier(0);
+          read_b(1);
+          read_a(0);
+          __builtin_amdgcn_sched_barrier(0);
+        }
+#pragma unroll
+        for (int i = I1; i < TI; ++i)
 #pragma unroll
           for (int j = 0; j < TJ; ++j)
             acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_f16(af[1][i], bf[0][j], acc[i][j], 0, 0, 0);
