@@ -68,6 +68,32 @@ __device__ __forceinline__ float gelu_f32(float x) {
   const float e = copysignf(a < 1.0f ? es : el, z);
   return (x * 0.5f) * (1.0f + e);
 }
+// gelu_f32 on two values: the same operations in the same order, each fma / mul / add as one v_pk_*_f32 for
+// both (every lane rounds as the scalar instruction does: the same bits at about half the VALU issue)
+__device__ __forceinline__ f32x2 gelu_f32_x2(f32x2 x) {
+  auto fma2 = [](f32x2 a, f32x2 b, f32x2 c) { return __builtin_elementwise_fma(a, b, c); };
+  auto k = [](unsigned u) { const float f = __builtin_bit_cast(float, u); return f32x2{f, f}; };
+  const f32x2 z = x * 0.70710678118654752f;
+  const f32x2 a = f32x2{fabsf(z.x), fabsf(z.y)};
+  const f32x2 s = z * z;
+  f32x2 ps = fma2(s, k(0xba1345e1u), k(0x3ba10414u));
+  ps = fma2(s, ps, k(0xbcdac9b8u));
+  ps = fma2(s, ps, k(0x3de703beu));
+  ps = fma2(s, ps, k(0xbec09330u));
+  ps = fma2(s, ps, k(0x3e0375d0u));
+  const f32x2 es = fma2(a, ps, a);
+  f32x2 q = fma2(a, k(0x378e98abu), k(0xb9c68948u));
+  q = fma2(a, q, k(0x3b7cd369u));
+  q = fma2(a, q, k(0xbcc618b2u));
+  q = fma2(a, q, k(0x3dda74e4u));
+  q = fma2(a, q, k(0x3f228afdu));
+  q = fma2(a, q, k(0x3e03c728u));
+  q = fma2(a, q, a);
+  const f32x2 t = q * -1.44269504088896341f;
+  const f32x2 el = 1.0f - f32x2{__builtin_amdgcn_exp2f(t.x), __builtin_amdgcn_exp2f(t.y)};
+  const f32x2 e = f32x2{copysignf(a.x < 1.0f ? es.x : el.x, z.x), copysignf(a.y < 1.0f ? es.y : el.y, z.y)};
+  return (x * 0.5f) * (1.0f + e);
+}
 
 // Tile coordinates of logical tile `bid` (after the XCD remap, which gives each XCD a
 // contiguous range): row-major over (bm, bn), or with group_m = G > 0 groups of G M panels
@@ -271,7 +297,11 @@ __device__ __forceinline__ void gemm_epilogue(const GemmParams& p, accv (&acc)[T
         for (int q = 0; q < 8; ++q) v[q] = (v[q] * 0.5f) * (1.0f + erff(v[q] * 0.70710678118654752f));
       } else if (act == ACT_GELU_F32) {
 #pragma unroll
-        for (int q = 0; q < 8; ++q) v[q] = gelu_f32(v[q]);
+        for (int q = 0; q < 8; q += 2) {
+          const f32x2 r = gelu_f32_x2(f32x2{v[q], v[q + 1]});
+          v[q] = r.x;
+          v[q + 1] = r.y;
+        }
       }
       if (row < M && (!NOSTORE || v[0] == 1234.5f)) {
         const size_t base = (size_t)row * N + col0;

@@ -474,7 +474,11 @@ __device__ __forceinline__ void pp_epilogue(const GemmParams& p, floatx4 (&acc)[
       for (int e = 0; e < 4; ++e) v[e] = (v[e] * 0.5f) * (1.0f + erff(v[e] * 0.70710678118654752f));
     } else if (act == ACT_GELU_F32) {
 #pragma unroll
-      for (int e = 0; e < 4; ++e) v[e] = gelu_f32(v[e]);
+      for (int e = 0; e < 4; e += 2) {
+        const f32x2 r = gelu_f32_x2(f32x2{v[e], v[e + 1]});
+        v[e] = r.x;
+        v[e + 1] = r.y;
+      }
     }
   };
   const float os = p.oscale;  // 1 except on split operands: fma(acc, 1, b) == acc + b
@@ -885,11 +889,17 @@ static int launch_cfg(const GemmParams& p0, hipStream_t s) {
   const int nwg = ((p.M + BM - 1) / BM) * (p.N / BN);
   const dim3 blk(64 * WM * WN);
 #ifdef MEC_PROBES
-  // the K-interleaved split tile (the fp32x3 FFN1 roofline kernel) with no operand loads inside its K loop:
-  // MFMA + LDS fragment reads + epilogue only, so its time against the real kernel's prices the loads
-  if (opt().gemm_debug == 1 && p.split == 2 && BN == 256 && BM == 256 && p.amode == A_PLAIN) {
-    if constexpr (MF == 16 && BK == 32 && 4 * (BM + BN) * BK * NS <= 160 * 1024)
-      hipLaunchKernelGGL((gemm_glds_kernel<BM, BN, WM, WN, NS, A_PLAIN, 1, MF, BK, 0, -1, 2>), dim3(nwg), blk, 0, s, p);
+  // the K-interleaved split tile (the fp32x3 FFN1 roofline kernel) with no operand loads inside its K loop
+  // (gemm_debug 1: MFMA + LDS fragment reads + epilogue only, so its time against the real kernel's prices
+  // the loads) or with no epilogue (gemm_debug 2: prices the epilogue)
+  if ((opt().gemm_debug == 1 || opt().gemm_debug == 2) && p.split == 2 && BN == 256 && BM == 256 &&
+      p.amode == A_PLAIN) {
+    if constexpr (MF == 16 && BK == 32 && 4 * (BM + BN) * BK * NS <= 160 * 1024) {
+      if (opt().gemm_debug == 1)
+        hipLaunchKernelGGL((gemm_glds_kernel<BM, BN, WM, WN, NS, A_PLAIN, 1, MF, BK, 0, -1, 2>), dim3(nwg), blk, 0, s, p);
+      else
+        hipLaunchKernelGGL((gemm_glds_kernel<BM, BN, WM, WN, NS, A_PLAIN, 2, MF, BK, 0, -1, 2>), dim3(nwg), blk, 0, s, p);
+    }
     MEC_LAUNCH_CHECK();
     return 0;
   }
