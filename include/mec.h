@@ -49,7 +49,9 @@ int mec_create(int kind, const float* host_blob, size_t n, int device, mec_model
 
 /* Arithmetic of a handle. MEC_PREC_F16 (mec_create's default, the fast path): BERT and the
  * image backbones on f16 MFMA operands with fp32 accumulation, LayerNorm, softmax, GELU,
- * residual stream and heads. MEC_PREC_FP32: every operand and product in fp32
+ * residual stream and heads; outside the north_star's 1e-3 / argmax-exact contract margin (text
+ * probs within 8.2e-4 of the oracle on the bench batch, rows with a smaller top-2 margin can flip:
+ * INTEGRATION.md). MEC_PREC_FP32: every operand and product in fp32
  * (v_mfma_f32_32x32x2_f32, an exact fmaf chain), the precision the reference computes in
  * (inference/text_inference.py:91-93, inference/image_inference.py:116-118).
  * MEC_PREC_FP32X3 (BERT, ResNet50, MobileNetV2): the fp32 path's arithmetic with every GEMM / conv
