@@ -168,7 +168,7 @@ int mec_conv_f32(const float* x, const float* w, const float* bias, const float*
  *   "gemm_glds_group_m" 0|2|4|[8]|16  the same tile order for the multi-stage GEMM engine
  *   "gemm_x3_order" 0|[1]  split-f16 (fp32x3) GEMM term order: 0 = pass-major (K for lo.hi, then
  *                          hi.lo, then hi.hi), 1 = K-interleaved (each 32-deep k chunk's three terms
- *                          back to back, 16x16x32 tiles 70256 / 70128 / 71128 / 71064 / 70064 only);
+ *                          back to back, 16x16x32 tiles 70256 / 70128 / 71128 / 71064 / 70064 / 72128 only);
  *                          both fp32-accurate, not the same bits
  *   "gemm_x3_tag" tag*100000+id  pin an interleaved split tile (7xxxx; 0 = autotune) for one launch
  *                          class (FusedPipeline pins BERT FFN2 to 70256 at fp32x3)

@@ -348,7 +348,7 @@ int set_option(Options& o, const std::string& k, int value) {
     const int v = id % 10000;
     const bool deep = id == 20256 || id == 30256 || id == 20128 || id == 40256 || id == 41256 || id == 50128 ||
                       id == 60128 || id == 50256 || id == 70256 || id == 70128 || id == 71128 || id == 71064 ||
-                      id == 70064;
+                      id == 70064 || id == 72128;
     return id == 0 || deep || (id < 20000 && (v == 64 || v == 128 || v == 256 || v == 1064 || v == 1128));
   };
   if (k == "gemm_bn" && tile_ok(value)) {

@@ -51,7 +51,10 @@ __global__ __launch_bounds__(64 * WM * WN, (WM * WN == 4) ? 2 : 1) void gemm_gld
   // each k step reads its whole stage into fragment registers first, so once every wave holds them the
   // stage is refilled with k step t + 2 while step t's MFMAs run -- two steps in flight on two buffers
   // instead of one (bert_qkv_attn_x3_kernel's schedule). Same fragments, same MFMA order: same bits.
-  constexpr bool ERS = ER != 0 && SP == 2 && NS == 2 && BK == 32 && DBG == 0;
+  // NS = 1 (tile 72128): one stage, read whole into fragments and restaged for step t + 1 under step t's MFMAs;
+  // 48 KB of LDS lets two workgroups share a CU, so one's barriers, loads and epilogue run under the other's
+  // MFMAs
+  constexpr bool ERS = ER != 0 && SP == 2 && (NS == 2 || NS == 1) && BK == 32 && DBG == 0;
   constexpr int CH = BK / 8;                   // 16-B chunks per LDS row
   constexpr int RPI = 64 / CH;                 // rows per glds wave-instruction (1 KB)
   constexpr int NW = WM * WN;
@@ -214,18 +217,18 @@ __global__ __launch_bounds__(64 * WM * WN, (WM * WN == 4) ? 2 : 1) void gemm_gld
 
   const int nk = SP == 1 ? 3 * nk0 : nk0;
 #pragma unroll
-  for (int s = 0; s < (ERS ? 2 : NS - 1); ++s)
+  for (int s = 0; s < (ERS ? NS : NS - 1); ++s)
     if (s < nk) issue(s, s);
 
   const int lr = lane & 31, lh = lane >> 5;
   if constexpr (ERS) {
     const int l16 = lane & 15, lq = lane >> 4;
     for (int t = 0; t < nk; ++t) {
-      if (t + 1 < nk) wait_vm<LPT>();  // step t landed; step t + 1 may stay in flight
+      if (NS == 2 && t + 1 < nk) wait_vm<LPT>();  // step t landed; step t + 1 may stay in flight
       else wait_vm<0>();
       __builtin_amdgcn_s_barrier();
       asm volatile("" ::: "memory");
-      const f16* sA = smem + (t & 1) * STAGE;
+      const f16* sA = smem + (NS == 1 ? 0 : (t & 1)) * STAGE;
       const f16* sB = sA + BM * BK;
       half8 af[2][TI], bf[2][TJ];  // [plane: 0 hi, 1 lo]
 #pragma unroll
@@ -244,7 +247,7 @@ __global__ __launch_bounds__(64 * WM * WN, (WM * WN == 4) ? 2 : 1) void gemm_gld
       __builtin_amdgcn_sched_barrier(0);
       asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
       __builtin_amdgcn_s_barrier();  // every wave holds its fragments: the stage is free
-      if (t + 2 < nk) issue(t & 1, t + 2);
+      if (t + NS < nk) issue(NS == 1 ? 0 : (t & 1), t + NS);
       __builtin_amdgcn_sched_barrier(0);
 #pragma unroll
       for (int i = 0; i < TI; ++i)
@@ -848,7 +851,8 @@ static int launch_cfg_act(const GemmParams& p, hipStream_t s, int nwg, dim3 blk)
   if (p.split == 2) {  // split-f16 operands, K-interleaved terms (16x16x32 tiles only)
     if constexpr (MF == 16 && BK == 32 && 4 * (BM + BN) * BK * NS <= 160 * 1024) {
       // ER: the early-restage schedule of the 2-stage tiles (opt().gemm_x3_restage; same bits)
-      if (NS == 2 && (opt().gemm_x3_restage == 1 || (opt().gemm_x3_restage == 2 && p.amode != A_PLAIN)))
+      if (NS == 1 ||
+          (NS == 2 && (opt().gemm_x3_restage == 1 || (opt().gemm_x3_restage == 2 && p.amode != A_PLAIN))))
         return launch_x3i<BM, BN, WM, WN, NS, BK, 1>(p, s, nwg, blk);
       return launch_x3i<BM, BN, WM, WN, NS, BK, 0>(p, s, nwg, blk);
     } else {
@@ -973,6 +977,9 @@ static int launch_bn(const GemmParams& p, hipStream_t s, int id) {
     case 71128: return launch_cfg<128, 128, 2, 2, 2, 16, 32>(p, s);
     case 71064: return launch_cfg<128, 64, 2, 2, 2, 16, 32>(p, s);
     case 70064: return launch_cfg<256, 64, 2, 2, 2, 16, 32>(p, s);
+    // 256 x 128 on 4 waves (wave tile 128 x 64) with ONE 48-KB stage (the restage schedule, ERS): two
+    // workgroups per CU
+    case 72128: return launch_cfg<256, 128, 2, 2, 1, 16, 32>(p, s);
     // (measured and dropped: 4-wave 128 x 256, 256 x 128 and 256 x 256 forms, one wave per SIMD with
     // 64 x 128 / 128 x 64 / 128 x 128 wave tiles: 10-45 % slower on every BERT shape,
     // profiles/r03_split_tiles_x3i.log)
@@ -1050,7 +1057,7 @@ static int tune_bn(const GemmParams& p, hipStream_t s, int* out_bn) {
   constexpr int REPS = 5;
   const int cands[] = {64,    128,   256,   1128,  1064,  10064, 10128, 10256, 11128,
                        11064, 20256, 30256, 20128, 40256, 41256, 50128, 60128, 50256};
-  const int cands_x3i[] = {70256, 70128, 71128, 71064, 70064};
+  const int cands_x3i[] = {70256, 70128, 71128, 71064, 70064, 72128};
   hipEvent_t ev[REPS + 1];
   for (auto& e : ev) MEC_HIP(hipEventCreate(&e));
   float best = 1e30f;
