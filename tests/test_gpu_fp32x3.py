@@ -123,7 +123,7 @@ def _split(a, scale=1.0):
 
 SPLIT_TILES = {0: [64, 128, 256, 1128, 1064, 10064, 10128, 10256, 11128, 11064, 20256, 30256, 20128, 50128, 60128,
                    50256, 40256, 41256],
-               1: [70256, 70128, 71128, 71064, 70064]}
+               1: [70256, 70128, 71128, 71064, 70064, 72128]}
 
 
 class x3_order:
