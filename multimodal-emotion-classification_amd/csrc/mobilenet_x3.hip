@@ -76,7 +76,10 @@ template <int S, int TO, int CINP, int HIDP, int COUTP, bool EXPAND, bool RES, i
 struct MxGeom {
   static constexpr int IR = (TO - 1) * S + 3, NP = IR * IR, MP = (NP + 15) / 16 * 16;
   static constexpr int XLD = CINP;       // f16 plane row (halfs; chunks swizzled, mx_sw)
-  static constexpr int XF = CINP + 4;    // f32 row of the non-expand (stem) input tile
+  // f32 row of the non-expand (stem) input tile: unpadded with its 16-B chunks XOR-swizzled by bit 1 of the
+  // row (SW: a depthwise / stem ds_*_b128 lane group covers 4 consecutive rows x 4 even or 4 odd chunks,
+  // which then fall on 16 distinct 4-bank slots), else padded to 36 floats
+  static constexpr int XF = SW ? CINP : CINP + 4;
   // f32 row of the expanded chunk (floats) and the 16-B chunk swizzle se_sw of its rows, per tile shape:
   // the rows the depthwise's ds_read_b128 lane groups read (4 - 8 input pixels, one per output pixel of
   // the group, at one tap) spread over distinct 4-bank slots; the expand epilogue's ds_write_b128 stays
@@ -125,6 +128,8 @@ __global__ __launch_bounds__(256, OCC) void mbv2_x3_kernel(const MbX3Args a) {
   const int tid = threadIdx.x, lane = tid & 63;
   const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
   const int tpr = a.OH / TO;
+  // float offset of 16-B chunk c of row p of the stem tile sXf
+  auto xf = [](int p, int c) { return p * XF + (SW ? (c ^ ((p >> 1) & 1)) : c) * 4; };
   const int H = a.H;
   const int l16 = lane & 15, lq = lane >> 4;
 
@@ -252,8 +257,8 @@ __global__ __launch_bounds__(256, OCC) void mbv2_x3_kernel(const MbX3Args a) {
 #pragma unroll
         for (int j = 0; j < 8; ++j) acc[j] = relu6x(acc[j]);
       }
-      *reinterpret_cast<float4*>(sXf + p * XF + cg * 8) = make_float4(acc[0], acc[1], acc[2], acc[3]);
-      *reinterpret_cast<float4*>(sXf + p * XF + cg * 8 + 4) = make_float4(acc[4], acc[5], acc[6], acc[7]);
+      *reinterpret_cast<float4*>(sXf + xf(p, 2 * cg)) = make_float4(acc[0], acc[1], acc[2], acc[3]);
+      *reinterpret_cast<float4*>(sXf + xf(p, 2 * cg + 1)) = make_float4(acc[4], acc[5], acc[6], acc[7]);
     }
   }
   __syncthreads();
@@ -365,10 +370,9 @@ __global__ __launch_bounds__(256, OCC) void mbv2_x3_kernel(const MbX3Args a) {
               const int f = se_sw<G::SEL>(pp);
               e0 = *reinterpret_cast<const float4*>(src + pp * sld + ((2 * dcg) ^ f) * 4);
               e1 = *reinterpret_cast<const float4*>(src + pp * sld + ((2 * dcg + 1) ^ f) * 4);
-            } else {
-              const float* ep = src + pp * sld + 8 * dcg;
-              e0 = *reinterpret_cast<const float4*>(ep);
-              e1 = *reinterpret_cast<const float4*>(ep + 4);
+            } else {  // sXf: chunks swizzled (xf)
+              e0 = *reinterpret_cast<const float4*>(sXf + xf(pp, h0 / 4 + 2 * dcg));
+              e1 = *reinterpret_cast<const float4*>(sXf + xf(pp, h0 / 4 + 2 * dcg + 1));
             }
             const float4 w0 = *reinterpret_cast<const float4*>(wd + (ky * 3 + kx) * 8);
             const float4 w1 = *reinterpret_cast<const float4*>(wd + (ky * 3 + kx) * 8 + 4);
