@@ -8,3 +8,5 @@ timeout -k 10 300 python3 -c "import __graft_entry__ as g; g.smoke(); print('__S
 rc=$?; tail -2 gpurun_out/r05p_smoke.log; [ $rc -ne 0 ] && exit $rc
 PREC=fp32x3 bash tools/gpu_prof_bench.sh > gpurun_out/r05p_prof.log 2>&1 || { tail -5 gpurun_out/r05p_prof.log; exit 1; }
 head -12 gpurun_out/bench_prof_grid_fp32x3.txt
+ENC=image_mbv2 PREC=fp32x3 bash tools/pmc_sq.sh > gpurun_out/r05p_pmcsq.log 2>&1 || { tail -5 gpurun_out/r05p_pmcsq.log; exit 1; }
+head -8 gpurun_out/pmcsq_fp32x3_image_mbv2.txt | cut -c1-72,200-260
