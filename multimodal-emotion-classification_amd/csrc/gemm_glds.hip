@@ -978,7 +978,7 @@ static int launch_bn(const GemmParams& p, hipStream_t s, int id) {
     case 71064: return launch_cfg<128, 64, 2, 2, 2, 16, 32>(p, s);
     case 70064: return launch_cfg<256, 64, 2, 2, 2, 16, 32>(p, s);
     // 256 x 128 on 4 waves (wave tile 128 x 64) with ONE 48-KB stage (the restage schedule, ERS): two
-    // workgroups per CU
+    // workgroups per CU (BERT FFN2's pin outside the fused step; not an autotune candidate)
     case 72128: return launch_cfg<256, 128, 2, 2, 1, 16, 32>(p, s);
     // (measured and dropped: 4-wave 128 x 256, 256 x 128 and 256 x 256 forms, one wave per SIMD with
     // 64 x 128 / 128 x 64 / 128 x 128 wave tiles: 10-45 % slower on every BERT shape,
@@ -1057,7 +1057,7 @@ static int tune_bn(const GemmParams& p, hipStream_t s, int* out_bn) {
   constexpr int REPS = 5;
   const int cands[] = {64,    128,   256,   1128,  1064,  10064, 10128, 10256, 11128,
                        11064, 20256, 30256, 20128, 40256, 41256, 50128, 60128, 50256};
-  const int cands_x3i[] = {70256, 70128, 71128, 71064, 70064, 72128};
+  const int cands_x3i[] = {70256, 70128, 71128, 71064, 70064};  // 72128: pinned only (mec_common.h gemm_x3_tag)
   hipEvent_t ev[REPS + 1];
   for (auto& e : ev) MEC_HIP(hipEventCreate(&e));
   float best = 1e30f;

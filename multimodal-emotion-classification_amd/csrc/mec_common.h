@@ -154,8 +154,12 @@ struct Options {
   // K-interleaved split engine, per launch class: forced tile (7xxxx), 0 = autotune. BERT FFN1 is
   // pinned to 70256 by default: it and the other tiles time within a few % of each other alone, so an
   // autotune would flip between them run to run, and the bench's roofline kernel (and its PMC traffic
-  // file) must be one kernel
-  int gemm_x3_tag[TAG_COUNT] = {0, 0, 0, 0, /*TAG_BERT_FFN1*/ 70256};
+  // file) must be one kernel. BERT FFN2 is pinned to the one-stage 72128 (two workgroups per CU: BERT
+  // alone 17.44 -> 17.12 ms, profiles/r05l_ab_tile72128_text_fp32x3.txt), a tile the autotuner does not
+  // offer: where the autotuner took it for a ResNet50 1x1 conv, and the one-stage 128-row tiles for most of
+  // them, the image leg ran faster alone but the fused step slower (profiles/r05s_ab_tile73xxx_*.txt). The
+  // fused step (FusedPipeline) pins FFN2 back to 70256 (profiles/r05m_ab_x3tag_ffn2.txt)
+  int gemm_x3_tag[TAG_COUNT] = {0, 0, 0, 0, /*TAG_BERT_FFN1*/ 70256, /*TAG_BERT_FFN2*/ 72128};
   // fp32x3 BERT FFN1 GELU: 1 = ACT_GELU_F32 (branch-free erf, one-instruction exp; max |error| /
   // max(|x|, 1) 1.21e-7 against float64, the correctly rounded erf's 1.06e-7), 0 = libm erff
   int gelu_x3 = 1;
