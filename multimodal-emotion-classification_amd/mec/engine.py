@@ -138,6 +138,14 @@ class TextEncoder(HipModel):
 
     VOCAB = 30522  # bert-base-uncased word embeddings
 
+    def __init__(self, *args, **kwargs):
+        super().__init__(*args, **kwargs)
+        # BERT's GEMMs walk their tiles in groups of 4 M panels per XCD (the handle default is 8, which
+        # ResNet50 keeps): fp32x3 fused step 25.51 -> 25.35 and 25.38 -> 25.31 ms, BERT alone 17.44 ->
+        # 17.32 ms, f16 fused step 10.76 -> 10.74 ms; the same bits (profiles/r05y_ab_groupm_*.txt,
+        # profiles/r05z_ab_groupm_*.txt)
+        self.set_option('gemm_glds_group_m', 4)
+
     def forward(self, ids: torch.Tensor, mask: torch.Tensor, check_ids: bool = False):
         """ids/mask int32 [B,128] -> (cls [B,768], logits [B,7], probs [B,7]).
 

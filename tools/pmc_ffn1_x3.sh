@@ -45,7 +45,7 @@ out = {'tile': int(os.environ['TILE']), 'M': 32768, 'kernel': k[:100], 'bytes_pe
        'source': 'rocprofv3 --pmc, separate FETCH_SIZE / WRITE_SIZE / SQ / TCC hit-miss passes (tools/pmc_ffn1_x3.sh) over the '
                  'fp32x3 text encoder at B=256; FETCH_SIZE doubled per MI355X_MICROARCH.md (gfx950); algorithmic '
                  'bytes = fp32-equivalent operands (each hi+lo pair is 4 B)'}
-out['gemm_glds_group_m'] = int(os.environ['GM']) if os.environ.get('GM') else 'default (8)'
+out['gemm_glds_group_m'] = int(os.environ['GM']) if os.environ.get('GM') else 'TextEncoder default (4)'
 json.dump(out, open('gpurun_out/ffn1_x3_traffic%s.json' % ('_gm' + os.environ['GM'] if os.environ.get('GM') else ''), 'w'), indent=1)
 print(json.dumps(out, indent=1))
 PY
