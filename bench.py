@@ -532,6 +532,9 @@ def run(a, precision, B, world, rank, dev, inputs):
     res = {
         'metric': METRIC,
         'value': total / el, 'unit': 'samples/s', 'n_gpus': world, 'steps': a.steps, 'warmup': a.warmup,
+        # samples each rank runs per step: a SCALE N = 8 line (1024 per rank) divides by an N = 1 line of
+        # the same per_rank_batch (bench.py --batch 1024), not by the 256-sample headline
+        'per_rank_batch': B,
         'ms_per_step': el / a.steps * 1e3, 'higher_is_better': True, 'scaling': 'weak', 'vs_baseline': None,
         'dtype': DTYPE[precision], 'precision': precision,
         'data': 'synthetic (seeded inputs: 56-d features, 128-token ids, 48x48 u8; seeded synthetic weights)',
@@ -648,7 +651,7 @@ def main_stub(a, world, rank):
     ok = bool(torch.equal(rows, stub_rows(0, world * B)))
     if rank == 0:
         line = {'metric': METRIC, 'value': None, 'unit': 'samples/s', 'n_gpus': world, 'steps': a.steps,
-                'warmup': a.warmup, 'ms_per_step': float(t.item()) / max(a.steps, 1) * 1e3,
+                'warmup': a.warmup, 'per_rank_batch': B, 'ms_per_step': float(t.item()) / max(a.steps, 1) * 1e3,
                 'higher_is_better': True, 'scaling': 'weak', 'vs_baseline': None, 'dtype': None,
                 'data': 'stub: no GPU visible, CPU stand-in rows', 'stub': True,
                 'config': {'workload': 'launcher / sharding / all-gather check (no encoders run)',

@@ -68,6 +68,20 @@ int mec_create(int kind, const float* host_blob, size_t n, int device, mec_model
  * fails. Speech, fusion and audio handles are fp32 at every setting. */
 enum { MEC_PREC_F16 = 0, MEC_PREC_FP32 = 1, MEC_PREC_FP32X3 = 2 };
 int mec_create_ex(int kind, const float* host_blob, size_t n, int device, int precision, mec_model** out);
+/* mec_create_ex with this handle's own knobs, "key=value[,key=value...]" (the keys of mec_set_option),
+ * applied over the process defaults BEFORE the weights are packed; NULL or "" = the defaults. The
+ * creation-time knobs live here: "x3_headroom" 0..24 [0] (fp32x3: every activation-plane exponent chosen
+ * for 2^-x3_headroom of the default target, i.e. that many binades more room above the bound / BN
+ * estimate before the range flag trips; the Python engine re-creates a handle with +8 after a trip, once
+ * the batch has been re-run on an MEC_PREC_FP32 handle) and "x3_plane_scale". Same semantics as the
+ * reference's model loads (see mec_create). */
+int mec_create_opt(int kind, const float* host_blob, size_t n, int device, int precision, const char* opts,
+                   mec_model** out);
+/* fp32x3 handles: the activation-plane exponents chosen at creation, one line per tensor (group),
+ * "name s=<exponent> bound=<rigorous bound or BN estimate>", after a first line with the creation knobs;
+ * "" for other precisions, NULL on a null handle. Owned by the handle (valid until mec_destroy). For
+ * diagnosing a range-flag failure (mec_model_check returning MEC_ERR_X3_RANGE). */
+const char* mec_model_x3_report(mec_model* m);
 /* The handle's precision (MEC_PREC_*), -1 on a null handle. */
 int mec_precision(const mec_model* m);
 int mec_destroy(mec_model* m);
@@ -171,7 +185,13 @@ int mec_conv_f32(const float* x, const float* w, const float* bias, const float*
  *                          back to back, 16x16x32 tiles 70256 / 70128 / 71128 / 71064 / 70064 / 72128 only);
  *                          both fp32-accurate, not the same bits
  *   "gemm_x3_tag" tag*100000+id  pin an interleaved split tile (7xxxx; 0 = autotune) for one launch
- *                          class (FusedPipeline pins BERT FFN2 to 70256 at fp32x3)
+ *                          class (FusedPipeline pins BERT FFN2 to 70256 at fp32x3); a pin applies where
+ *                          its grid has >= 128 tiles (half the CUs), smaller batches autotune (same bits)
+ *   GEMM shapes first launched inside hipGraph capture cannot be timed: split (fp32x3) shapes run
+ *   the heuristic tile uncached and are autotuned at their first eager launch (every split tile
+ *   gives the same bits); f16 / f32 shapes cache the heuristic tile for the handle's lifetime, so
+ *   an eager launch after the capture computes the same bits as the graph replay (tiles of those
+ *   engines differ in MFMA shape and k order)
  *   "gelu_x3" 0|[1]        fp32x3 BERT FFN1 GELU: 1 = branch-free erf with a one-instruction exp
  *                          (error 1.21e-7 x max(|x|, 1) vs float64), 0 = libm erff (not the same bits)
  *   "conv3x3_direct" 0|[1] layer1 3x3 conv on the halo-tile kernel (mec_conv_f16 too)
@@ -197,9 +217,12 @@ int mec_conv_f32(const float* x, const float* w, const float* bias, const float*
  *   "gemm_x3_restage" [0]|1|2 K-interleaved split tiles with 2 stages: refill a stage for k step t + 2 once
  *                          every wave holds step t's fragments (two steps in flight) in every A mode (1), in the
  *                          convs only (2), or never (0: after step t's barrier); same bits
- *   "x3_plane_scale" 0|[1] fp32x3 activation-plane scales, read at mec_create_ex (set it as the process
- *                          default first): 1 = per-tensor power-of-two exponents (the envelope above),
- *                          0 = unscaled planes (A/B only: narrower envelope, different bits)
+ *   "x3_plane_scale" 0|[1] fp32x3 activation-plane scales, creation-time (mec_create_opt, or the process
+ *                          default before mec_create_ex; mec_model_set_option rejects it): 1 = per-tensor
+ *                          power-of-two exponents (the envelope above), 0 = unscaled planes (A/B only:
+ *                          narrower envelope, different bits)
+ *   "x3_headroom" [0]..24  fp32x3 extra binades of plane headroom, creation-time like x3_plane_scale
+ *                          (mec_create_opt above)
  *   "mbv2_layered" 0|7..17 [8]  fp32x3 MobileNetV2: features[k..17] as expand GEMM -> depthwise -> project GEMM
  *                          (0: every block fused but features[17], layered at every setting)
  *   "mbv2_layered16" 0|7..17 [8]  the same on the f16 path
@@ -228,12 +251,14 @@ int mec_gemm_f32_query(int amode, int M, int N, int K);
 int mec_model_gemm_query(mec_model* m, int amode, int M, int N, int K);
 
 /* Errors a kernel can only report after the fact, since the handle's last check: 0 = none,
- * -1 = mec_last_error() says what (and the flag is cleared). Call once the stream that ran
+ * -1 = mec_last_error() says what (and the flag is cleared); MEC_ERR_X3_RANGE (-2) = the fp32x3
+ * range flag below (the batch can be re-run on an MEC_PREC_FP32 handle of the same weights). Call once the stream that ran
  * the handle's forwards has been synchronized. Speech: a stage hand-off wait of
  * speech_flow_kernel expired (that forward's probs are NaN). MEC_PREC_FP32X3 text / image
  * handles: an activation left the f16 hi / lo range (|x| >= 65520, NaN or inf; that forward's
  * outputs are invalid). Always 0 for the other kinds and precisions. No reference counterpart:
  * the reference's predict calls have no asynchronous failure (inference/speech_inference.py:69). */
+enum { MEC_ERR_X3_RANGE = -2 };
 int mec_model_check(mec_model* m);
 
 /* hipEvent timing hook: time every launch of kernel class `tag`. */

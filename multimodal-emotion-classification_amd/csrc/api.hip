@@ -1,6 +1,8 @@
 // extern "C" boundary (include/mec.h).
 #include "../../include/mec.h"
 
+#include <algorithm>
+#include <cstdlib>
 #include <exception>
 #include <new>
 
@@ -118,6 +120,11 @@ int mec_create(int kind, const float* host_blob, size_t n, int device, mec_model
 }
 
 int mec_create_ex(int kind, const float* host_blob, size_t n, int device, int precision, mec_model** out) {
+  return mec_create_opt(kind, host_blob, n, device, precision, nullptr, out);
+}
+
+int mec_create_opt(int kind, const float* host_blob, size_t n, int device, int precision, const char* opts,
+                   mec_model** out) {
   API_GUARD({
     if (!out) { set_error("mec_create: out is null"); return -1; }
     if (precision != MEC_PREC_F16 && precision != MEC_PREC_FP32 && precision != MEC_PREC_FP32X3) {
@@ -131,26 +138,52 @@ int mec_create_ex(int kind, const float* host_blob, size_t n, int device, int pr
       set_error("mec_create: blob has " + std::to_string(n) + " floats, expected " + std::to_string(want));
       return -1;
     }
+    // "key=value,key=value": this handle's knobs, applied over the process defaults before its weights are
+    // packed (so creation-time knobs such as x3_headroom take effect)
+    Options o = default_options();
+    if (opts && *opts) {
+      std::string all(opts);
+      size_t pos = 0;
+      while (pos <= all.size()) {
+        const size_t end = std::min(all.find(',', pos), all.size());
+        const std::string kv = all.substr(pos, end - pos);
+        const size_t eq = kv.find('=');
+        if (eq == std::string::npos || eq == 0) { set_error("mec_create_opt: bad option \"" + kv + "\" (key=value)"); return -1; }
+        char* tail = nullptr;
+        const long v = std::strtol(kv.c_str() + eq + 1, &tail, 10);
+        if (!tail || *tail || tail == kv.c_str() + eq + 1) { set_error("mec_create_opt: bad value in \"" + kv + "\""); return -1; }
+        if (set_option(o, kv.substr(0, eq), (int)v) != 0) return -1;
+        pos = end + 1;
+      }
+    }
     MEC_HIP(hipSetDevice(device));
     Model* impl = nullptr;
     int rc = -1;
     switch (kind) {
       // speech and fusion are fp32 at either precision
-      case KIND_SPEECH: { auto* p = new SpeechModel(); impl = p; rc = p->create(host_blob, n); break; }
-      case KIND_TEXT: { auto* p = new TextModel(); p->prec = precision; impl = p; rc = p->create(host_blob, n); break; }
-      case KIND_IMAGE: { auto* p = new ImageModel(); p->prec = precision; impl = p; rc = p->create(host_blob, n); break; }
-      case KIND_FUSION: { auto* p = new FusionModel(); impl = p; rc = p->create(host_blob, n); break; }
-      case KIND_IMAGE_MBV2: { auto* p = new MobileNetModel(); p->prec = precision; impl = p; rc = p->create(host_blob, n); break; }
-      case KIND_AUDIO: { auto* p = new AudioModel(); impl = p; rc = p->create(host_blob, n); break; }
+      case KIND_SPEECH: { auto* p = new SpeechModel(); impl = p; p->opts = o; rc = p->create(host_blob, n); break; }
+      case KIND_TEXT: { auto* p = new TextModel(); p->prec = precision; impl = p; p->opts = o; rc = p->create(host_blob, n); break; }
+      case KIND_IMAGE: { auto* p = new ImageModel(); p->prec = precision; impl = p; p->opts = o; rc = p->create(host_blob, n); break; }
+      case KIND_FUSION: { auto* p = new FusionModel(); impl = p; p->opts = o; rc = p->create(host_blob, n); break; }
+      case KIND_IMAGE_MBV2: { auto* p = new MobileNetModel(); p->prec = precision; impl = p; p->opts = o; rc = p->create(host_blob, n); break; }
+      case KIND_AUDIO: { auto* p = new AudioModel(); impl = p; p->opts = o; rc = p->create(host_blob, n); break; }
     }
     if (rc != 0) { delete impl; return -1; }
     impl->kind = kind;
     impl->device = device;
     impl->prec = (kind == KIND_SPEECH || kind == KIND_FUSION || kind == KIND_AUDIO) ? MEC_PREC_FP32 : precision;
     if (impl->prec == PREC_FP32X3 && impl->alloc_range_flag() != 0) { delete impl; return -1; }
+    if (impl->prec == PREC_FP32X3)
+      impl->x3_report = "x3_headroom=" + std::to_string(o.x3_headroom) + " x3_plane_scale=" +
+                        std::to_string(o.x3_plane_scale) + "\n" + impl->x3_report;
     *out = new mec_model{impl};
     return 0;
   })
+}
+
+const char* mec_model_x3_report(mec_model* m) {
+  if (!m || !m->impl) { set_error("mec_model_x3_report: null handle"); return nullptr; }
+  return m->impl->x3_report.c_str();
 }
 
 int mec_destroy(mec_model* m) {
@@ -311,6 +344,7 @@ int set_option(Options& o, const std::string& k, int value) {
   if (k == "mbv2_x3_occ" && (value == 3 || value == 4)) { o.mbv2_x3_occ = value; return 0; }
   if (k == "mbv2_x3_sesw" && (value == 0 || value == 1)) { o.mbv2_x3_sesw = value; return 0; }
   if (k == "x3_plane_scale" && (value == 0 || value == 1)) { o.x3_plane_scale = value; return 0; }
+  if (k == "x3_headroom" && value >= 0 && value <= 24) { o.x3_headroom = value; return 0; }
   if (k == "gemm_x3_restage" && value >= 0 && value <= 2) { o.gemm_x3_restage = value; return 0; }
   if (k == "mbv2_layered" && (value == 0 || (value >= 7 && value <= 17))) { o.mbv2_layered = value; return 0; }
   if (k == "mbv2_layered16" && (value == 0 || (value >= 7 && value <= 17))) { o.mbv2_layered16 = value; return 0; }
@@ -377,7 +411,13 @@ int mec_set_option(const char* key, int value) { return set_option(default_optio
 
 int mec_model_set_option(mec_model* m, const char* key, int value) {
   if (!m || !m->impl) { set_error("null model handle"); return -1; }
-  return set_option(m->impl->opts, key ? key : "", value);
+  const std::string k = key ? key : "";
+  if (k == "x3_plane_scale" || k == "x3_headroom") {  // read while the weights are packed: too late here
+    set_error("mec_model_set_option: \"" + k + "\" is a creation-time option (pass it to mec_create_opt, or set "
+              "the process default with mec_set_option before mec_create_ex)");
+    return -1;
+  }
+  return set_option(m->impl->opts, k, value);
 }
 
 int mec_build_flags(void) { return kProbes ? MEC_BUILD_PROBES : 0; }

@@ -1056,9 +1056,13 @@ int TextModel::create(const float* blob, size_t n) {
       return mx;
     };
     // opts.x3_plane_scale 0: every exponent 0 (the unscaled planes, A/B only)
-    auto aexp = [&](double b, double t) { return opts.x3_plane_scale ? activation_exp(b, t) : 0; };
+    // opts.x3_headroom: 2^-x3_headroom of the target (a handle re-created after a range trip)
+    auto aexp = [&](double b, double t) {
+      return opts.x3_plane_scale ? activation_exp(b, std::ldexp(t, -opts.x3_headroom)) : 0;
+    };
     double b_in = ln_bound(lg, lb);
     x3_s_emb = aexp(b_in, kX3BoundTarget);
+    x3_note("emb_ln", x3_s_emb, b_in);
     std::vector<int> s_in(BLAYERS);
     x3_s_ln1.assign(BLAYERS, 0);
     x3_s_ln2.assign(BLAYERS, 0);
@@ -1072,14 +1076,24 @@ int TextModel::create(const float* blob, size_t n) {
       const float* pl = pr.data() + PRM_LAYER * l;
       s_in[l] = l ? x3_s_ln2[l - 1] : x3_s_emb;
       int sqkv[3];
-      for (int q = 0; q < 3; ++q)
-        sqkv[q] = aexp(proj_bound(b_in, wl + (size_t)q * BH * BH, pl + q * BH, BH, BH), kX3BoundTarget);
+      double bqkv3[3];
+      for (int q = 0; q < 3; ++q) {
+        bqkv3[q] = proj_bound(b_in, wl + (size_t)q * BH * BH, pl + q * BH, BH, BH);
+        sqkv[q] = aexp(bqkv3[q], kX3BoundTarget);
+      }
       const double b1 = ln_bound(pl + 3072, pl + 3840);
       x3_s_ln1[l] = aexp(b1, kX3BoundTarget);
-      x3_s_ffn[l] =
-          aexp(proj_bound(b1, wl + (size_t)2304 * BH + BH * BH, pl + 4608, BI, BH), kX3BoundTarget);
+      const double bffn = proj_bound(b1, wl + (size_t)2304 * BH + BH * BH, pl + 4608, BI, BH);
+      x3_s_ffn[l] = aexp(bffn, kX3BoundTarget);
       b_in = ln_bound(pl + 8448, pl + 9216);
       x3_s_ln2[l] = aexp(b_in, kX3BoundTarget);
+      const std::string ln = "layer" + std::to_string(l) + ".";
+      x3_note(ln + "q", sqkv[0], bqkv3[0]);
+      x3_note(ln + "k", sqkv[1], bqkv3[1]);
+      x3_note(ln + "v", sqkv[2], bqkv3[2]);
+      x3_note(ln + "ln1", x3_s_ln1[l], b1);
+      x3_note(ln + "ffn", x3_s_ffn[l], bffn);
+      x3_note(ln + "ln2", x3_s_ln2[l], b_in);
       x3_s_q[l] = sqkv[0];
       x3_s_k[l] = sqkv[1];
       x3_s_v[l] = sqkv[2];

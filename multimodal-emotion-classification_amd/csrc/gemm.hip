@@ -38,13 +38,19 @@ int launch_gemm(const GemmParams& p0, hipStream_t s, Prof* prof, int tag) {
   }
   if (prof) MEC_TRY(prof->begin(tag, s));
   int rc;
-  if (p.split)  // split-f16 operands: the glds engine only (the halo conv kernels read one plane); autotuned,
-    // except the launch classes gemm_x3_tag pins (BERT FFN1 -> 70256 by default, mec_common.h); the
-    // pass-major order pins FFN1 to 10256 (it and the ping-pong tile time within 3-7 %, tools/bench_split.py)
+  if (p.split) {  // split-f16 operands: the glds engine only (the halo conv kernels read one plane); autotuned,
+    // except the launch classes gemm_x3_tag pins (BERT FFN1 -> 70256 by default, mec_common.h) where the
+    // pinned tile's grid fills half the chip; the pass-major order pins FFN1 to 10256 (it and the ping-pong
+    // tile time within 3-7 %, tools/bench_split.py)
+    int pin = (tag > 0 && tag < TAG_COUNT) ? opt().gemm_x3_tag[tag] : 0;
+    if (pin) {
+      const int bm = (pin / 1000) % 10 == 1 ? 128 : 256, bn = pin % 1000;
+      if ((long)((p.M + bm - 1) / bm) * (p.N / bn) < kX3PinMinTiles) pin = 0;  // small batch: autotune (same bits)
+    }
     rc = launch_gemm_glds(p, s, opt().gemm_bn ? opt().gemm_bn
                                 : !opt().gemm_x3_order ? (tag == TAG_BERT_FFN1 ? 10256 : 0)
-                                : (tag > 0 && tag < TAG_COUNT) ? opt().gemm_x3_tag[tag] : 0);
-  else if (opt().conv3x3_direct && !opt().gemm_bn && p.amode == A_CONV && p.ks == 3 && p.stride == 1 && p.pad == 1 && p.H == 56 &&
+                                : pin);
+  } else if (opt().conv3x3_direct && !opt().gemm_bn && p.amode == A_CONV && p.ks == 3 && p.stride == 1 && p.pad == 1 && p.H == 56 &&
       p.W == 56 && p.C == 64 && p.N == 64 && p.act == ACT_RELU && !p.R && p.C16 && !p.C32 && p.M % (56 * 56) == 0)
     rc = launch_conv3x3_c64(reinterpret_cast<const f16*>(p.A), p.B, p.bias, p.C16, p.M / (56 * 56), 56, 64, 64, s);
   else if (opt().conv3x3_halo && !opt().gemm_bn && p.amode == A_CONV && p.ks == 3 && p.stride == 1 && p.pad == 1 &&

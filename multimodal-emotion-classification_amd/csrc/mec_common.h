@@ -121,6 +121,11 @@ struct Options {
   // exponents from bounds / BN estimates, 0 = every exponent 0 (round 4's unscaled planes; A/B only: small
   // activations then lose bits to the f16 subnormals, large ones overflow)
   int x3_plane_scale = 1;
+  // fp32x3 extra headroom, read when a handle is created: every activation-plane exponent is chosen for a
+  // target 2^-x3_headroom times the default (models.h activation_exp), so the planes take values that many
+  // binades above the bound / BN estimate before the range flag trips. engine.HipModel re-creates a handle
+  // with more headroom after a trip (the batch itself is re-run on the fp32 engine)
+  int x3_headroom = 0;
   // fp32x3 MobileNetV2 fused blocks: the expanded chunk's f32 rows with a per-tile-shape 16-B chunk swizzle
   // (1; fewer LDS bank conflicts on the depthwise reads) or unswizzled 36-float rows (0); same bits
   int mbv2_x3_sesw = 1;
@@ -158,7 +163,9 @@ struct Options {
   // alone 17.44 -> 17.12 ms, profiles/r05l_ab_tile72128_text_fp32x3.txt), a tile the autotuner does not
   // offer: where the autotuner took it for a ResNet50 1x1 conv, and the one-stage 128-row tiles for most of
   // them, the image leg ran faster alone but the fused step slower (profiles/r05s_ab_tile73xxx_*.txt). The
-  // fused step (FusedPipeline) pins FFN2 back to 70256 (profiles/r05m_ab_x3tag_ffn2.txt)
+  // fused step (FusedPipeline) pins FFN2 back to 70256 (profiles/r05m_ab_x3tag_ffn2.txt). A pin applies only
+  // where its grid fills at least half the chip (kX3PinMinTiles tiles: FFN1 from B = 22, FFN2 from B = 43): a small batch
+  // (latency-mode text inference) autotunes among the 7xxxx tiles instead, which give the same bits
   int gemm_x3_tag[TAG_COUNT] = {0, 0, 0, 0, /*TAG_BERT_FFN1*/ 70256, /*TAG_BERT_FFN2*/ 72128};
   // fp32x3 BERT FFN1 GELU: 1 = ACT_GELU_F32 (branch-free erf, one-instruction exp; max |error| /
   // max(|x|, 1) 1.21e-7 against float64, the correctly rounded erf's 1.06e-7), 0 = libm erff
@@ -168,6 +175,8 @@ struct Options {
   int gemm_debug = 0, conv3x3_debug = 0, stem_debug = 0, audio_debug = 0, speech_debug = 0;  // probe builds only
   int speech_spin_limit = -1;  // probe builds only: speech_flow_kernel wait limit (forces expired waits)
 };
+
+constexpr long kX3PinMinTiles = 128;  // gemm_x3_tag pins apply from this many tiles (half of 256 CUs)
 
 // GEMM autotuner results: tile id per (engine, shape), per handle.
 struct TuneCache {

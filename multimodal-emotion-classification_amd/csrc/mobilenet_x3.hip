@@ -804,7 +804,10 @@ int MobileNetModel::create_x3(const float* blob, size_t n) {
   // kDwUp. Every epilogue scale below folds in 2^(s_out - s_in) (the fused blocks' and the expand GEMMs'
   // outputs are f32: s_out = 0 there).
   // opts.x3_plane_scale 0: every exponent 0 (the unscaled planes, A/B only)
-  auto aexp = [&](double b, double t) { return opts.x3_plane_scale ? activation_exp(b, t) : 0; };
+  // opts.x3_headroom: 2^-x3_headroom of the target (a handle re-created after a range trip)
+  auto aexp = [&](double b, double t) {
+    return opts.x3_plane_scale ? activation_exp(b, std::ldexp(t, -opts.x3_headroom)) : 0;
+  };
   {
     int s_prev = 0;
     for (size_t b0 = 0; b0 < blocks.size();) {
@@ -816,6 +819,7 @@ int MobileNetModel::create_x3(const float* blob, size_t n) {
         e_max = std::max(e_max, e);
       }
       const int st = aexp(e_max, kX3EstimateTarget);
+      x3_note("features" + std::to_string(b0 + 1) + "-" + std::to_string(b1) + ".out", st, e_max);
       for (size_t i = b0; i < b1; ++i) {
         blocks[i].x3_s_in = i == b0 ? s_prev : st;
         blocks[i].x3_s_out = st;

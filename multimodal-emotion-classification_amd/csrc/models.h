@@ -32,6 +32,10 @@ struct Model {
   unsigned* range_host = nullptr;
   unsigned* range_dev = nullptr;
   int alloc_range_flag();
+  // fp32x3 handles: one line per activation tensor (group) written at creation, "name s=<exponent>
+  // bound=<bound or BN estimate>" plus the headroom the exponents were chosen with (mec_model_x3_report)
+  std::string x3_report;
+  void x3_note(const std::string& name, int s, double bound);
   virtual ~Model();
   // errors a kernel could only report after the fact (mec_model_check): 0 = none since the last
   // check. Call after the stream that ran the handle's forwards has been synchronized.

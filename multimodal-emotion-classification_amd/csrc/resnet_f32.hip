@@ -488,10 +488,15 @@ int ImageModel::create_f32(const float* blob, size_t n) {
     // The downsample of a stage's first block reads the block input (s_in) beside conv3's T2 (s_t2)
     // in one dual GEMM: its weights are pre-scaled by 2^(s_t2 - s_in) so both halves of K carry 2^s_t2.
     // opts.x3_plane_scale 0: every exponent 0 (the unscaled planes, A/B only)
-    auto aexp = [&](double b, double t) { return opts.x3_plane_scale ? activation_exp(b, t) : 0; };
+    // opts.x3_headroom: 2^-x3_headroom of the target (a handle re-created after a range trip)
+    auto aexp = [&](double b, double t) {
+      return opts.x3_plane_scale ? activation_exp(b, std::ldexp(t, -opts.x3_headroom)) : 0;
+    };
     stem.x3_s = aexp(stem.x3_est, kX3EstimateTarget);
+    x3_note("stem", stem.x3_s, stem.x3_est);
     {
       int s_prev = stem.x3_s;
+      int stage = 0;
       double e_stream = stem.x3_est;
       for (size_t b0 = 0; b0 < blocks.size();) {
         size_t b1 = b0 + 1;
@@ -503,13 +508,19 @@ int ImageModel::create_f32(const float* blob, size_t n) {
           e_max = std::max(e_max, e_stream);
         }
         const int s_stage = aexp(e_max, kX3EstimateTarget);
+        const std::string st = "layer" + std::to_string(stage + 1);
+        x3_note(st + ".out", s_stage, e_max);
         for (size_t bi = b0; bi < b1; ++bi) {
           Bottleneck& bk = blocks[bi];
           bk.c1.x3_s = aexp(bk.c1.x3_est, kX3EstimateTarget);
           bk.c2.x3_s = aexp(bk.c2.x3_est, kX3EstimateTarget);
           bk.c3.x3_s = s_stage;
           bk.x3_s_in = bi == b0 ? s_prev : s_stage;
+          const std::string bn = st + "." + std::to_string(bi - b0);
+          x3_note(bn + ".conv1", bk.c1.x3_s, bk.c1.x3_est);
+          x3_note(bn + ".conv2", bk.c2.x3_s, bk.c2.x3_est);
         }
+        ++stage;
         s_prev = s_stage;
         b0 = b1;
       }

@@ -1,7 +1,9 @@
 // Runtime plumbing: thread-local error string, device buffers, hipEvent timing hook.
 #include <algorithm>
 #include <cmath>
+#include <cstdio>
 
+#include "../../include/mec.h"
 #include "models.h"
 
 namespace mec {
@@ -109,8 +111,16 @@ int Model::check() {
   if (!range_host || !*reinterpret_cast<volatile unsigned*>(range_host)) return 0;
   *range_host = 0;
   set_error("fp32x3: an activation left the f16 hi / lo range (|x| >= 65520, or NaN / inf) in a forward since "
-            "the last check; its outputs are invalid (use MEC_PREC_FP32 for such inputs)");
-  return -1;
+            "the last check; its outputs are invalid (re-run the batch on an MEC_PREC_FP32 handle, and create "
+            "the fp32x3 handle again with more x3_headroom: mec_create_opt; mec_model_x3_report lists the "
+            "exponents)");
+  return MEC_ERR_X3_RANGE;
+}
+
+void Model::x3_note(const std::string& name, int s, double bound) {
+  char buf[160];
+  snprintf(buf, sizeof buf, "%s s=%d bound=%.6g\n", name.c_str(), s, bound);
+  x3_report += buf;
 }
 
 float split_planes(const float* w, size_t n, f16* hi, f16* lo) {

@@ -60,10 +60,10 @@ class ImageInference:
 
     def _forward(self, arr: np.ndarray):
         x = engine.to_device(np.asarray(arr, np.uint8)[None], self.device)
-        feat, logits, probs = self.model.forward_u8(x)
-        feat, probs = feat.cpu().numpy()[0], probs.cpu().numpy()[0]  # synchronizes the stream
-        self.model.check()  # fp32x3: an activation outside the f16 range raises MecError, not NaN probs
-        return feat, probs
+        # synchronized and checked: an fp32x3 batch whose activations leave the planes' range is re-run on
+        # the fp32 engine (engine.HipModel.recover), never answered with NaN probs
+        feat, logits, probs = self.model.checked('forward_u8', x)
+        return feat.cpu().numpy()[0], probs.cpu().numpy()[0]
 
     @staticmethod
     def _as_dict(emotions, probs: np.ndarray) -> Dict:
@@ -101,7 +101,11 @@ class ImageInference:
         return self._forward(arr)
 
     def predict_batch(self, gray):
-        """gray: device u8 [B,48,48] -> (feat [B,512], logits [B,7], probs [B,7])."""
+        """gray: device u8 [B,48,48] -> (feat [B,512], logits [B,7], probs [B,7]). Asynchronous on the
+        current stream, except on an fp32x3 handle: there it synchronizes and checks, so a batch outside
+        the planes' range is answered by the fp32 engine (engine.HipModel.checked)."""
         if self.model is None:
             raise RuntimeError('image model not loaded')
+        if self.model.precision == 'fp32x3':
+            return self.model.checked('forward', gray)
         return self.model.forward(gray)

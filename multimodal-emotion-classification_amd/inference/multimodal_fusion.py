@@ -125,8 +125,10 @@ class MultimodalFusion:
         if self.fusion_model is None:
             raise RuntimeError('fusion model not loaded')
         sf, sl, sp = self.speech_inference.model.forward(x_speech)
-        tf, tl, tp = self.text_inference.model.forward(ids, mask)
-        imf, il, ip = self.image_inference.model.forward(gray)
+        # fp32x3 text / image handles: synchronized and checked (a batch outside the planes' range is
+        # answered by the fp32 engine before the fusion reads it; TextInference / ImageInference.predict_batch)
+        tf, tl, tp = self.text_inference.predict_batch(ids, mask)
+        imf, il, ip = self.image_inference.predict_batch(gray)
         fl, fp, aw, dw = self.fusion_model.forward(sf, tf, imf, sp, tp, ip)
         return {'speech': (sf, sl, sp), 'text': (tf, tl, tp), 'image': (imf, il, ip), 'fusion': (fl, fp, aw, dw)}
 

@@ -104,10 +104,11 @@ class TextInference:
         if ids.size and (ids.min() < 0 or ids.max() >= engine.TextEncoder.VOCAB):
             # the reference's nn.Embedding raises IndexError for such ids
             raise ValueError(f'token id out of range [0, {engine.TextEncoder.VOCAB})')
-        cls, logits, probs = self.model.forward(engine.to_device(ids, self.device), engine.to_device(mask, self.device))
-        cls, probs = cls.cpu().numpy()[0], probs.cpu().numpy()[0]  # synchronizes the stream
-        self.model.check()  # fp32x3: an activation outside the f16 range raises MecError, not NaN probs
-        return cls, probs
+        # synchronized and checked: an fp32x3 batch whose activations leave the planes' range is re-run on
+        # the fp32 engine (engine.HipModel.recover), never answered with NaN probs
+        cls, logits, probs = self.model.checked('forward', engine.to_device(ids, self.device),
+                                                engine.to_device(mask, self.device))
+        return cls.cpu().numpy()[0], probs.cpu().numpy()[0]
 
     @staticmethod
     def _as_dict(emotions, probs: np.ndarray) -> Dict:
@@ -150,13 +151,17 @@ class TextInference:
         if not texts:
             return []
         ids, mask = self.encode_batch(texts)
-        _, _, probs = self.model.forward(engine.to_device(ids, self.device), engine.to_device(mask, self.device))
+        _, _, probs = self.model.checked('forward', engine.to_device(ids, self.device),
+                                         engine.to_device(mask, self.device))
         probs = probs.cpu().numpy()
-        self.model.check()
         return [self._as_dict(self.emotions, p) for p in probs]
 
     def predict_batch(self, ids, mask):
-        """ids/mask: device int32 [B,128] -> (cls [B,768], logits [B,7], probs [B,7])."""
+        """ids/mask: device int32 [B,128] -> (cls [B,768], logits [B,7], probs [B,7]). Asynchronous on the
+        current stream, except on an fp32x3 handle: there it synchronizes and checks, so a batch outside
+        the planes' range is answered by the fp32 engine (engine.HipModel.checked)."""
         if self.model is None:
             raise RuntimeError('text model not loaded')
+        if self.model.precision == 'fp32x3':
+            return self.model.checked('forward', ids, mask, True)
         return self.model.forward(ids, mask, check_ids=True)

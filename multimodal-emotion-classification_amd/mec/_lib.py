@@ -25,6 +25,8 @@ SIGNATURES = {
     'mec_blob_size': (ctypes.c_longlong, [c_int]),
     'mec_create': (c_int, [c_int, c_fp, ctypes.c_size_t, c_int, ctypes.POINTER(c_vp)]),
     'mec_create_ex': (c_int, [c_int, c_fp, ctypes.c_size_t, c_int, c_int, ctypes.POINTER(c_vp)]),
+    'mec_create_opt': (c_int, [c_int, c_fp, ctypes.c_size_t, c_int, c_int, ctypes.c_char_p, ctypes.POINTER(c_vp)]),
+    'mec_model_x3_report': (ctypes.c_char_p, [c_vp]),
     'mec_precision': (c_int, [c_vp]),
     'mec_destroy': (c_int, [c_vp]),
     'mec_speech_fwd': (c_int, [c_vp, c_vp, c_int, c_vp, c_vp, c_vp, c_vp]),
@@ -67,8 +69,17 @@ TAGS = {'bert_qkv': 1, 'bert_attn': 2, 'bert_oproj': 3, 'bert_ffn1': 4, 'bert_ff
 PRECISIONS = {'f16': 0, 'fp32': 1, 'fp32x3': 2}
 
 
+# mec_model_check's return code for a raised fp32x3 range flag (include/mec.h MEC_ERR_X3_RANGE)
+ERR_X3_RANGE = -2
+
+
 class MecError(RuntimeError):
     pass
+
+
+class X3RangeError(MecError):
+    """An fp32x3 handle's activation planes left the f16 range (mec_model_check == MEC_ERR_X3_RANGE):
+    the batch's outputs are invalid; it can be re-run on an fp32 handle of the same weights."""
 
 
 _lib = None
@@ -96,4 +107,5 @@ def load(path: str = LIB_PATH):
 def check(rc: int, what: str):
     if rc != 0:
         err = load().mec_last_error()
-        raise MecError(f'{what} failed: {err.decode() if err else "unknown error"}')
+        raise (X3RangeError if rc == ERR_X3_RANGE else MecError)(
+            f'{what} failed: {err.decode() if err else "unknown error"}')

@@ -56,33 +56,55 @@ def require_gpu(device=None) -> torch.device:
 
 
 class HipModel:
-    """Owns one mec_model handle (packed device weights + workspace)."""
+    """Owns one mec_model handle (packed device weights + workspace).
+
+    fp32x3 handles answer on data outside their activation-plane envelope instead of failing: the
+    checked paths (`checked`, and through it the drop-in classes and FusedPipeline.check) notice a
+    raised range flag (mec_model_check == MEC_ERR_X3_RANGE), re-run the batch on an fp32 handle of the
+    same weights (`fp32_twin`, the exact-fp32 HIP engine, created on first use) and re-create this
+    handle with 8 more binades of plane headroom (`x3_headroom`), so later batches run fp32x3 again."""
 
     kind: str = ''
+    X3_HEADROOM_STEP = 8  # binades added per range trip (mec_create_opt "x3_headroom", at most 24)
 
-    def __init__(self, weights=None, seed: int = 1234, device=None, precision: str = 'f16'):
+    def __init__(self, weights=None, seed: int = 1234, device=None, precision: str = 'f16', opts=None):
         if precision not in _lib.PRECISIONS:
             raise ValueError(f"precision must be one of {sorted(_lib.PRECISIONS)}, got {precision!r}")
         self.lib = _lib.load()
         self.device = require_gpu(device)
         self.precision = precision
-        w = weights if weights is not None else synthetic.weights(self.kind, seed)
-        blob = synthetic.pack(self.kind, w)
+        # the weights dict (synthetic weights are cached per (kind, seed), so this holds no copy): a range
+        # trip re-creates the handle from it
+        self._w = weights if weights is not None else synthetic.weights(self.kind, seed)
+        self._seed = seed
+        self._copts = dict(opts or {})  # creation-time knobs (mec_create_opt)
+        self._knobs = []                # set_option calls, replayed onto a re-created handle
+        self._twin = None
+        self.x3_reruns = 0              # batches re-run on the fp32 engine after a range trip
+        self._lock = threading.Lock()
+        self.handle = None
+        self.handle = self._create(self._copts)
+
+    def _create(self, copts):
+        blob = synthetic.pack(self.kind, self._w)
         want = self.lib.mec_blob_size(KINDS[self.kind])
         if blob.size != want:
             raise MecError(f'{self.kind}: blob has {blob.size} floats, library expects {want}')
         h = ctypes.c_void_p()
         torch.cuda.set_device(self.device)
-        _lib.check(self.lib.mec_create_ex(KINDS[self.kind], blob.ctypes.data_as(_lib.c_fp), blob.size,
-                                          self.device.index, _lib.PRECISIONS[precision], ctypes.byref(h)),
-                   f'mec_create({self.kind}, {precision})')
-        self.handle = h
-        self._lock = threading.Lock()
+        spec = ','.join(f'{k}={int(v)}' for k, v in copts.items()).encode()
+        _lib.check(self.lib.mec_create_opt(KINDS[self.kind], blob.ctypes.data_as(_lib.c_fp), blob.size,
+                                           self.device.index, _lib.PRECISIONS[self.precision], spec, ctypes.byref(h)),
+                   f'mec_create({self.kind}, {self.precision})')
+        return h
 
     def close(self):
         if getattr(self, 'handle', None):
             self.lib.mec_destroy(self.handle)
             self.handle = None
+        if getattr(self, '_twin', None) is not None:
+            self._twin.close()
+            self._twin = None
 
     def __del__(self):
         try:
@@ -93,12 +115,71 @@ class HipModel:
     def set_option(self, key: str, value: int):
         """One tuning knob of THIS handle (mec_model_set_option; include/mec.h lists them)."""
         _lib.check(self.lib.mec_model_set_option(self.handle, key.encode(), int(value)), f'set_option({key}={value})')
+        self._knobs.append((key, int(value)))
 
     def check(self):
         """Raise MecError if a kernel of this handle flagged an error after the fact since the
         last check (mec_model_check; speech: an expired hand-off wait, whose forward's probs are
-        NaN). Call once the stream that ran the forwards has been synchronized."""
+        NaN; fp32x3: X3RangeError, an activation outside the planes' range). Call once the stream
+        that ran the forwards has been synchronized."""
         _lib.check(self.lib.mec_model_check(self.handle), f'{self.kind} forward')
+
+    def x3_report(self) -> str:
+        """The activation-plane exponents this fp32x3 handle was created with (mec_model_x3_report)."""
+        r = self.lib.mec_model_x3_report(self.handle)
+        return r.decode() if r else ''
+
+    @property
+    def x3_headroom(self) -> int:
+        return int(self._copts.get('x3_headroom', 0))
+
+    def fp32_twin(self):
+        """An exact-fp32 handle of the same kind and weights (created on first use)."""
+        if self._twin is None:
+            self._twin = type(self)(self._w, self._seed, self.device, 'fp32')
+        return self._twin
+
+    def x3_widen(self):
+        """Re-create this fp32x3 handle with X3_HEADROOM_STEP more binades of plane headroom."""
+        hr = min(24, self.x3_headroom + self.X3_HEADROOM_STEP)
+        if hr == self.x3_headroom:
+            return
+        copts = dict(self._copts, x3_headroom=hr)
+        with self._lock:
+            torch.cuda.synchronize(self.device)  # nothing of the old handle may still run
+            h = self._create(copts)
+            old, self.handle, self._copts = self.handle, h, copts
+            self.lib.mec_destroy(old)
+            for k, v in self._knobs:
+                _lib.check(self.lib.mec_model_set_option(self.handle, k.encode(), v), f'set_option({k}={v})')
+
+    def recover(self, method: str, args, outs):
+        """After a synchronized forward `getattr(self, method)(*args)` -> `outs`: check the handle; on an
+        fp32x3 range trip re-run the call on the fp32 twin, copy its results into `outs` (in place), widen
+        this handle, and return True. Other errors raise as `check` does."""
+        rc = self.lib.mec_model_check(self.handle)
+        if rc == 0:
+            return False
+        if rc != _lib.ERR_X3_RANGE or self.precision != 'fp32x3':
+            _lib.check(rc, f'{self.kind} forward')
+        twin = self.fp32_twin()
+        with torch.cuda.device(self.device):
+            res = getattr(twin, method)(*args)
+            for o, r in zip(outs, res):
+                o.copy_(r)
+            torch.cuda.synchronize(self.device)
+        twin.check()
+        self.x3_reruns += 1
+        self.x3_widen()
+        return True
+
+    def checked(self, method: str, *args):
+        """`getattr(self, method)(*args)`, synchronized and checked: an fp32x3 range trip is answered by
+        the fp32 engine (recover) instead of raising. Returns the forward's outputs."""
+        outs = getattr(self, method)(*args)
+        torch.cuda.synchronize(self.device)
+        self.recover(method, args, outs)
+        return outs
 
     def gemm_tile(self, M: int, N: int, K: int, amode: int = 0) -> int:
         """The tile this handle's autotuner chose for a GEMM shape it has run (0 = not seen)."""
@@ -220,6 +301,7 @@ class AudioFeaturizer(HipModel):
         self.device = require_gpu(device)
         self.precision = 'fp32'
         self.sample_rate, self.n_mfcc = int(sample_rate), int(n_mfcc)
+        self._knobs, self._twin, self._copts, self.x3_reruns = [], None, {}, 0
         self.n_features = self.n_mfcc + 16
         blob = np.array([sample_rate, N_FFT, HOP, N_MELS, n_mfcc], np.float32)
         h = ctypes.c_void_p()
@@ -333,6 +415,7 @@ class FusedPipeline:
         self._text = (torch.cuda.Stream(device=self.device, priority=0 if image_priority else -1)
                       if (concurrent and (text_priority or image_priority)) else None)
         self._tuned = set()  # batch sizes whose GEMM shapes were autotuned (serially)
+        self._last, self._since_check = None, 0
         if concurrent and precision == 'f16':
             # BERT FFN2 (M = 128 B, N = 768, K = 3072) on the 256 x 256 ping-pong tile beside the
             # image stream: BERT alone runs it fastest on 128 x 128 (the autotuner's pick, text
@@ -410,6 +493,8 @@ class FusedPipeline:
             out = {'speech': (sf, sl, sp), 'text': (tf, tl, tp), 'image': (imf, il, ip),
                    'fusion': (fl, fp, aw, dw)}
             extra = epilogue(out) if epilogue is not None else None
+        self._last = {'text': (ids, mask), 'image': (gray,), 'out': out}  # check() repairs this batch
+        self._since_check += 1
         return out if epilogue is None else (out, extra)
 
     def wait(self, stream=None):
@@ -418,11 +503,31 @@ class FusedPipeline:
             (stream or torch.cuda.current_stream(self.device)).wait_stream(self._tail)
 
     def check(self):
-        """Synchronize the device, then raise MecError if any handle flagged an after-the-fact
-        kernel error since the last check (mec_model_check)."""
+        """Synchronize the device, then check every handle (mec_model_check): raise MecError for an
+        after-the-fact kernel error. An fp32x3 range trip of the text or image handle is answered instead
+        of raised when one batch ran since the last check: that encoder is re-run on its fp32 twin, its
+        outputs and the fusion's are overwritten in place in the dict `forward` returned (an `epilogue`'s
+        results, computed before, are not), and the handle is re-created with more plane headroom
+        (HipModel.recover). With several batches since the last check a trip raises X3RangeError (it
+        cannot say which batch). Returns the modalities that were re-run."""
         torch.cuda.synchronize(self.device)
-        for m in self.models():
-            m.check()
+        last, n, redo = self._last, self._since_check, []
+        self._since_check = 0
+        for name, m in (('text', self.text), ('image', self.image)):
+            if last is not None and n == 1 and m.precision == 'fp32x3':
+                if m.recover('forward', last[name], last['out'][name]):
+                    redo.append(name)
+            else:
+                m.check()
+        self.speech.check()
+        self.fusion.check()
+        if redo:
+            o = last['out']
+            (sf, _, sp), (tf, _, tp), (imf, _, ip) = o['speech'], o['text'], o['image']
+            for d, r in zip(o['fusion'], self.fusion.forward(sf, tf, imf, sp, tp, ip)):
+                d.copy_(r)
+            torch.cuda.synchronize(self.device)
+        return redo
 
     @staticmethod
     def pack_rows(out) -> torch.Tensor:

@@ -94,6 +94,25 @@ def test_c_abi_argument_errors_without_gpu():
     assert b'null model' in lib.mec_last_error()
 
 
+def test_create_opt_parses_its_option_list_without_gpu():
+    """mec_create_opt validates its "key=value,..." list (the mec_set_option keys and values) before
+    any device call; mec_model_x3_report needs a handle."""
+    import ctypes
+    lib = _lib.load()
+    h = ctypes.c_void_p()
+    n = syn.blob_size('speech')
+    blob = np.zeros(n, np.float32)
+    for opts, msg in ((b'x3_headroom', b'key=value'), (b'=3', b'key=value'), (b'x3_headroom=', b'bad value'),
+                      (b'x3_headroom=2x', b'bad value'), (b'x3_headroom=25', b'bad value'),
+                      (b'x3_headroom=8,nope=1', b'unknown key'), (b'gemm_debug=1', b'MEC_PROBES')):
+        assert lib.mec_create_opt(0, blob.ctypes.data_as(_lib.c_fp), n, 0, 2, opts, ctypes.byref(h)) == -1, opts
+        assert msg in lib.mec_last_error(), (opts, lib.mec_last_error())
+        assert not h.value
+    assert lib.mec_model_x3_report(None) is None
+    assert b'null handle' in lib.mec_last_error()
+    assert lib.mec_set_option(b'x3_headroom', 4) == 0 and lib.mec_set_option(b'x3_headroom', 0) == 0
+
+
 def test_option_validation_without_gpu():
     """mec_set_option accepts each knob's documented values (include/mec.h) and rejects the
     rest, including every probe value (the product library is not a -DMEC_PROBES build); it
@@ -140,7 +159,7 @@ def test_option_validation_without_gpu():
                      (b'gemm_bn', 0),
                      (b'gemm_bn_tag', 3 * 100000 + 11128), (b'gemm_debug', 0), (b'gemm_group_m', 8),
                      (b'gemm_glds_group_m', 8), (b'gemm_f32_family', 16), (b'bert_ln_rows', 2),
-                     (b'bert_cls_last', 1), (b'gemm_x3_order', 1), (b'gelu_x3', 1), (b'gemm_x3_tag', 5 * 100000),
+                     (b'bert_cls_last', 1), (b'gemm_x3_order', 1), (b'gelu_x3', 1), (b'gemm_x3_tag', 5 * 100000 + 72128),
                      (b'pw_chain_x3', 2), (b'mbv2_layered', 8), (b'mbv2_layered16', 8), (b'mbv2_x3_tile', 4), (b'mbv2_x3_tpw', 2),
                      (b'resnet_chunk', 0), (b'bert_qkv_attn_x3_heads', 1), (b'bert_qkv_attn_heads', 1)]:
             lib.mec_set_option(k, v)
