@@ -217,6 +217,9 @@ int mec_conv_f32(const float* x, const float* w, const float* bias, const float*
  *   "gemm_x3_restage" [0]|1|2 K-interleaved split tiles with 2 stages: refill a stage for k step t + 2 once
  *                          every wave holds step t's fragments (two steps in flight) in every A mode (1), in the
  *                          convs only (2), or never (0: after step t's barrier); same bits
+ *   "gemm_x3_stagger" [0]..200  split tiles with two workgroups per CU: the first pass's second workgroups start
+ *                          this many microseconds late (co-resident epilogues and MFMAs desynchronized;
+ *                          measured neutral-to-slower on BERT FFN1); same bits
  *   "x3_plane_scale" 0|[1] fp32x3 activation-plane scales, creation-time (mec_create_opt, or the process
  *                          default before mec_create_ex; mec_model_set_option rejects it): 1 = per-tensor
  *                          power-of-two exponents (the envelope above), 0 = unscaled planes (A/B only:

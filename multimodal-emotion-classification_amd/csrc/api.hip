@@ -330,7 +330,7 @@ int set_option(Options& o, const std::string& k, int value) {
   }
   if (k == "fusion_split" && (value == 0 || value == 1)) { o.fusion_split = value; return 0; }
   if (k == "speech_spin_limit" && (value == -1 || (probe && value >= 0))) { o.speech_spin_limit = value; return 0; }
-  if (k == "gemm_debug" && (value == 0 || (probe && value >= 1 && value <= 5))) { o.gemm_debug = value; return 0; }
+  if (k == "gemm_debug" && (value == 0 || (probe && value >= 1 && value <= 6))) { o.gemm_debug = value; return 0; }
   if (k == "gemm_autotune" && (value == 0 || value == 1)) { o.gemm_autotune = value; return 0; }
   if (k == "gemm_f32_tile" && value >= 0 && value <= 8) { o.gemm_f32_tile = value; return 0; }
   if (k == "gemm_f32_tag" && value >= 0 && value / 100000 > 0 && value / 100000 < TAG_COUNT && value % 100000 <= 8) {
@@ -346,6 +346,7 @@ int set_option(Options& o, const std::string& k, int value) {
   if (k == "x3_plane_scale" && (value == 0 || value == 1)) { o.x3_plane_scale = value; return 0; }
   if (k == "x3_headroom" && value >= 0 && value <= 24) { o.x3_headroom = value; return 0; }
   if (k == "gemm_x3_restage" && value >= 0 && value <= 2) { o.gemm_x3_restage = value; return 0; }
+  if (k == "gemm_x3_stagger" && value >= 0 && value <= 200) { o.gemm_x3_stagger = value; return 0; }
   if (k == "mbv2_layered" && (value == 0 || (value >= 7 && value <= 17))) { o.mbv2_layered = value; return 0; }
   if (k == "mbv2_layered16" && (value == 0 || (value >= 7 && value <= 17))) { o.mbv2_layered16 = value; return 0; }
   if (k == "conv3x3_direct" && (value == 0 || value == 1)) { o.conv3x3_direct = value; return 0; }

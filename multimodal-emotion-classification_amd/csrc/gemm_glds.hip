@@ -90,6 +90,10 @@ __global__ __launch_bounds__(64 * WM * WN, (WM * WN == 4) ? 2 : 1) void gemm_gld
   int bm, bn;
   tile_coords(bid, nbm, nbn, p.group_m, bm, bn);
   const int m0 = bm * BM, n0 = bn * BN;
+  if (p.stagger && (int)blockIdx.x >= p.stagger_lo && (int)blockIdx.x < p.stagger_hi) {
+    const unsigned long long t0 = __builtin_amdgcn_s_memrealtime();
+    while (__builtin_amdgcn_s_memrealtime() - t0 < (unsigned long long)p.stagger) __builtin_amdgcn_s_sleep(16);
+  }
 
   // ---- per-lane DMA sources: lane -> (row in its 8-row group, physical chunk)
   const int lrow = lane / CH, pchunk = lane % CH;
@@ -423,8 +427,9 @@ __global__ __launch_bounds__(64 * WM * WN, (WM * WN == 4) ? 2 : 1) void gemm_gld
     if (s == 12345.678f) p.C32[0] = s;  // keeps the accumulators live
     return;
   }
-  gemm_epilogue<BM, BN, WM, WN, MF, accv, TI, TJ, PRE, false, ACT>(p, acc, smem, m0, n0, wm, wn, wave, lane, rpre,
-                                                                   rpre32, rplo);
+  // DBG 3 (probe builds only): the whole epilogue but (almost) no stores, pricing the plane stores
+  gemm_epilogue<BM, BN, WM, WN, MF, accv, TI, TJ, PRE, DBG == 3, ACT>(p, acc, smem, m0, n0, wm, wn, wave, lane, rpre,
+                                                                      rpre32, rplo);
 }
 
 
@@ -892,17 +897,32 @@ static int launch_cfg(const GemmParams& p0, hipStream_t s) {
   p.group_m = opt().gemm_glds_group_m;
   const int nwg = ((p.M + BM - 1) / BM) * (p.N / BN);
   const dim3 blk(64 * WM * WN);
+  // split tiles whose stages leave room for a second workgroup per CU (72128: one 48-KB stage; 71128 /
+  // 71064: 2 x 32 / 2 x 24 KB): the first pass's second workgroups (blocks 256..511) start late
+  if (p.split && opt().gemm_x3_stagger && NS * (BM + BN) * BK * 4 <= 80 * 1024 && nwg > 256) {
+    p.stagger = opt().gemm_x3_stagger * 100;
+    p.stagger_lo = 256;
+    p.stagger_hi = 512;
+  }
 #ifdef MEC_PROBES
   // the K-interleaved split tile (the fp32x3 FFN1 roofline kernel) with no operand loads inside its K loop
   // (gemm_debug 1: MFMA + LDS fragment reads + epilogue only, so its time against the real kernel's prices
   // the loads) or with no epilogue (gemm_debug 2: prices the epilogue)
-  if ((opt().gemm_debug == 1 || opt().gemm_debug == 2) && p.split == 2 && BN == 256 && BM == 256 &&
-      p.amode == A_PLAIN) {
+  // (gemm_debug 3: the epilogue without its stores; 6: with a plain (no GELU) epilogue -- prices the GELU)
+  if ((opt().gemm_debug == 1 || opt().gemm_debug == 2 || opt().gemm_debug == 3 || opt().gemm_debug == 6) &&
+      p.split == 2 && BN == 256 && BM == 256 && p.amode == A_PLAIN) {
     if constexpr (MF == 16 && BK == 32 && 4 * (BM + BN) * BK * NS <= 160 * 1024) {
       if (opt().gemm_debug == 1)
         hipLaunchKernelGGL((gemm_glds_kernel<BM, BN, WM, WN, NS, A_PLAIN, 1, MF, BK, 0, -1, 2>), dim3(nwg), blk, 0, s, p);
-      else
+      else if (opt().gemm_debug == 2)
         hipLaunchKernelGGL((gemm_glds_kernel<BM, BN, WM, WN, NS, A_PLAIN, 2, MF, BK, 0, -1, 2>), dim3(nwg), blk, 0, s, p);
+      else if (opt().gemm_debug == 3)
+        hipLaunchKernelGGL((gemm_glds_kernel<BM, BN, WM, WN, NS, A_PLAIN, 3, MF, BK, 0, -1, 2>), dim3(nwg), blk, 0, s, p);
+      else {
+        GemmParams q = p;
+        q.act = ACT_NONE;
+        hipLaunchKernelGGL((gemm_glds_kernel<BM, BN, WM, WN, NS, A_PLAIN, 0, MF, BK, 0, -1, 2>), dim3(nwg), blk, 0, s, q);
+      }
     }
     MEC_LAUNCH_CHECK();
     return 0;

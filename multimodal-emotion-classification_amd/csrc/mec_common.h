@@ -156,6 +156,9 @@ struct Options {
   // 1 % (8.79 -> 8.71 ms), but the fused step loses 0.8 % (2) / 1.7 % (1) and BERT up to 0.9 %: 0 by default
   // (profiles/r05_ab_restage_*.txt)
   int gemm_x3_restage = 0;
+  // split tiles with two or more workgroups per CU: the later-dispatched workgroups of the first pass start
+  // this many microseconds late (GemmParams::stagger), desynchronizing co-resident workgroups; 0 = off
+  int gemm_x3_stagger = 0;
   // K-interleaved split engine, per launch class: forced tile (7xxxx), 0 = autotune. BERT FFN1 is
   // pinned to 70256 by default: it and the other tiles time within a few % of each other alone, so an
   // autotune would flip between them run to run, and the bench's roofline kernel (and its PMC traffic
@@ -321,6 +324,11 @@ struct GemmParams {
   float cscale = 1.f;
   unsigned* ovf = nullptr;  // split output's range flag (x3_raise); launch_gemm fills in range_flag()
   long long r_lo = 0;  // != 0: the f16 residual R is a hi plane + a lo plane at R + r_lo (R = hi + lo)
+  // start stagger (opt().gemm_x3_stagger): blocks [stagger_lo, stagger_hi) -- the second resident workgroup of
+  // each CU in dispatch order -- wait `stagger` ticks of the 100-MHz realtime clock before starting, so the
+  // two workgroups sharing a CU run half a tile apart and one's epilogue (GELU, plane stores) overlaps the
+  // other's MFMAs instead of both bursting together. Speed only: no result depends on it
+  int stagger = 0, stagger_lo = 0, stagger_hi = 0;
 };
 
 int launch_gemm(const GemmParams& p, hipStream_t s, Prof* prof, int tag);
