@@ -217,6 +217,13 @@ int mec_conv_f32(const float* x, const float* w, const float* bias, const float*
  *   "gemm_x3_restage" [0]|1|2 K-interleaved split tiles with 2 stages: refill a stage for k step t + 2 once
  *                          every wave holds step t's fragments (two steps in flight) in every A mode (1), in the
  *                          convs only (2), or never (0: after step t's barrier); same bits
+ *   "gemm_x3_late_dma" 0|[1]|2|3  interleaved split tiles: the second wave of each SIMD issues its share of the
+ *                          next stage's LDS DMA after its first MFMA term group (1), its second (2), hi planes
+ *                          after the first and lo after the second (3), or right after the barrier with the
+ *                          first wave (0); same bits (1: fused fp32x3 step -1.2 to -1.6 %)
+ *   "gemm_x3_prio" [0]|1   the same tiles: MFMA sections at wave priority 1 (measured neutral); same bits
+ *   "qkv_x3_late_dma" [0]|1|2  fp32x3 fused QKV + attention: every other 256-block of workgroups issues its
+ *                          stage refill after its first / second MFMA term group (measured neutral); same bits
  *   "gemm_x3_stagger" [0]..200  split tiles with two workgroups per CU: the first pass's second workgroups start
  *                          this many microseconds late (co-resident epilogues and MFMAs desynchronized;
  *                          measured neutral-to-slower on BERT FFN1); same bits

@@ -347,6 +347,9 @@ int set_option(Options& o, const std::string& k, int value) {
   if (k == "x3_headroom" && value >= 0 && value <= 24) { o.x3_headroom = value; return 0; }
   if (k == "gemm_x3_restage" && value >= 0 && value <= 2) { o.gemm_x3_restage = value; return 0; }
   if (k == "gemm_x3_stagger" && value >= 0 && value <= 200) { o.gemm_x3_stagger = value; return 0; }
+  if (k == "gemm_x3_late_dma" && value >= 0 && value <= 3) { o.gemm_x3_late_dma = value; return 0; }
+  if (k == "gemm_x3_prio" && (value == 0 || value == 1)) { o.gemm_x3_prio = value; return 0; }
+  if (k == "qkv_x3_late_dma" && value >= 0 && value <= 2) { o.qkv_x3_late_dma = value; return 0; }
   if (k == "mbv2_layered" && (value == 0 || (value >= 7 && value <= 17))) { o.mbv2_layered = value; return 0; }
   if (k == "mbv2_layered16" && (value == 0 || (value >= 7 && value <= 17))) { o.mbv2_layered16 = value; return 0; }
   if (k == "conv3x3_direct" && (value == 0 || value == 1)) { o.conv3x3_direct = value; return 0; }

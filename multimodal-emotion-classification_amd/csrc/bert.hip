@@ -774,7 +774,7 @@ template <int HP>
 __global__ __launch_bounds__(256 * HP, HP == 1 ? 2 : 1) void bert_qkv_attn_x3_kernel(
     const f16* __restrict__ hs, long long hlo, const f16* __restrict__ wqkv, long long wlo, float oscale,
     const float* __restrict__ bqkv, const int32_t* __restrict__ mask, f16* __restrict__ ctx, long long clo, int nseq,
-    float qks, unsigned* flag) {
+    float qks, unsigned* flag, int late_dma) {
   static_assert(HP == 1 || HP == 2, "heads per workgroup");
   constexpr int NW = 4 * HP, WNC = 2 * HP;             // waves; waves along N
   constexpr int QBN = 192 * HP;                        // Q | K | V columns of the HP heads
@@ -866,16 +866,31 @@ __global__ __launch_bounds__(256 * HP, HP == 1 ? 2 : 1) void bert_qkv_attn_x3_ke
     __builtin_amdgcn_sched_barrier(0);
     asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
     __builtin_amdgcn_s_barrier();
-    if (kt + 2 < QX_NK) issue(kt + 2, kt & 1);
+    // late_dma (opt().qkv_x3_late_dma, HP = 1): every other 256-block of workgroups -- the second resident
+    // workgroup of a CU in the first dispatch pass -- issues the stage refill after its first MFMA term group
+    // (1) or its second (2), so the two workgroups' waves on a SIMD do not both sit in DMA issue while the
+    // matrix core idles; the refill still has the rest of this step and all of the next to land. Same bits
+    const bool late = late_dma && ((blockIdx.x >> 8) & 1);
+    if (kt + 2 < QX_NK && !late) issue(kt + 2, kt & 1);
     __builtin_amdgcn_sched_barrier(0);
 #pragma unroll
     for (int i = 0; i < 4; ++i)
 #pragma unroll
       for (int j = 0; j < 6; ++j) acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_f16(bf[0][j], af[1][i], acc[i][j], 0, 0, 0);
+    if (kt + 2 < QX_NK && late && late_dma == 1) {
+      __builtin_amdgcn_sched_barrier(0);
+      issue(kt + 2, kt & 1);
+      __builtin_amdgcn_sched_barrier(0);
+    }
 #pragma unroll
     for (int i = 0; i < 4; ++i)
 #pragma unroll
       for (int j = 0; j < 6; ++j) acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_f16(bf[1][j], af[0][i], acc[i][j], 0, 0, 0);
+    if (kt + 2 < QX_NK && late && late_dma == 2) {
+      __builtin_amdgcn_sched_barrier(0);
+      issue(kt + 2, kt & 1);
+      __builtin_amdgcn_sched_barrier(0);
+    }
 #pragma unroll
     for (int i = 0; i < 4; ++i)
 #pragma unroll
@@ -949,10 +964,10 @@ int launch_bert_qkv_attn_x3(const f16* hs, long long hlo, const f16* wqkv, long 
                             hipStream_t s) {
   if (opt().bert_qkv_attn_x3_heads == 1)
     hipLaunchKernelGGL(bert_qkv_attn_x3_kernel<1>, dim3(B * 12), dim3(256), 0, s, hs, hlo, wqkv, wlo, oscale, bqkv,
-                       mask, ctx, clo, B, qks, range_flag());
+                       mask, ctx, clo, B, qks, range_flag(), opt().qkv_x3_late_dma);
   else
     hipLaunchKernelGGL(bert_qkv_attn_x3_kernel<2>, dim3(B * 6), dim3(512), 0, s, hs, hlo, wqkv, wlo, oscale, bqkv,
-                       mask, ctx, clo, B, qks, range_flag());
+                       mask, ctx, clo, B, qks, range_flag(), 0);
   MEC_LAUNCH_CHECK();
   return 0;
 }

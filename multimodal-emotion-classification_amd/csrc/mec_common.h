@@ -159,6 +159,17 @@ struct Options {
   // split tiles with two or more workgroups per CU: the later-dispatched workgroups of the first pass start
   // this many microseconds late (GemmParams::stagger), desynchronizing co-resident workgroups; 0 = off
   int gemm_x3_stagger = 0;
+  // interleaved split tiles (not the restage schedule): the second wave of each SIMD issues its share of the
+  // next stage's LDS DMA after its first term group of MFMAs (1), after its second (2), or its hi planes after
+  // the first and lo planes after the second (3), not right after the step's barrier (0), so the two waves of
+  // a SIMD do not both sit in DMA issue while the matrix core idles; same bits. 1: fused fp32x3 step -1.2 /
+  // -1.6 %, BERT alone -0.7 / -1.4 %, ResNet50 neutral (profiles/r06f_ab_late_dma.txt, r06g_ab_late_dma.txt)
+  int gemm_x3_late_dma = 1;
+  // the same kernels: MFMA sections at wave priority 1, DMA issue and barriers at 0 (A/B knob)
+  int gemm_x3_prio = 0;
+  // fp32x3 fused QKV + attention (one head per workgroup): every other 256-block of workgroups issues its stage
+  // refill after its first (1) or second (2) MFMA term group instead of right after the barrier (0); same bits
+  int qkv_x3_late_dma = 0;
   // K-interleaved split engine, per launch class: forced tile (7xxxx), 0 = autotune. BERT FFN1 is
   // pinned to 70256 by default: it and the other tiles time within a few % of each other alone, so an
   // autotune would flip between them run to run, and the bench's roofline kernel (and its PMC traffic
@@ -329,6 +340,8 @@ struct GemmParams {
   // two workgroups sharing a CU run half a tile apart and one's epilogue (GELU, plane stores) overlaps the
   // other's MFMAs instead of both bursting together. Speed only: no result depends on it
   int stagger = 0, stagger_lo = 0, stagger_hi = 0;
+  int late_dma = 0;  // opt().gemm_x3_late_dma (gemm_glds_kernel, interleaved split tiles)
+  int x3_prio = 0;   // opt().gemm_x3_prio (the same kernels)
 };
 
 int launch_gemm(const GemmParams& p, hipStream_t s, Prof* prof, int tag);

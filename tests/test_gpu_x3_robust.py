@@ -154,27 +154,37 @@ def test_x3_creation_knobs_are_creation_time(dev):
 
 
 # ------------------------------------------------------------------ schedule knobs: the same bits
+@pytest.mark.parametrize('knob,values', [('gemm_x3_restage', (0, 1, 2)), ('gemm_x3_late_dma', (1, 0, 2, 3)),
+                                         ('gemm_x3_stagger', (0, 20)), ('gemm_x3_prio', (0, 1)),
+                                         ('qkv_x3_late_dma', (0, 1, 2))])
 @pytest.mark.parametrize('enc_kind', ['text', 'image'])
-def test_x3_restage_schedules_bit_identical(dev, enc_kind):
-    """gemm_x3_restage 1 / 2 (2-stage split tiles refilled for k step t + 2 as soon as every wave holds
-    step t's fragments, in every A mode / the convs only) against 0: the same fragments and MFMA order."""
+def test_x3_schedule_knobs_bit_identical(dev, enc_kind, knob, values):
+    """Split-tile schedule knobs against their default: gemm_x3_restage 1 / 2 (2-stage split tiles
+    refilled for k step t + 2 as soon as every wave holds step t's fragments, in every A mode / the convs
+    only), gemm_x3_late_dma 0 / 2 / 3 against the default 1 (where the second wave of each SIMD issues its DMA
+    share), gemm_x3_stagger (co-resident workgroups started apart), gemm_x3_prio (MFMA sections at wave
+    priority 1), qkv_x3_late_dma 1 / 2 (the fused QKV + attention kernel's refill issued late by every other
+    block of workgroups): the same fragments and MFMA order."""
+    if knob == 'qkv_x3_late_dma' and enc_kind == 'image':
+        pytest.skip('a BERT kernel')
     if enc_kind == 'text':
-        ids, mask = syn.text_inputs(32, 128, seed=71, ragged=True)
+        ids, mask = syn.text_inputs(48 if knob == 'qkv_x3_late_dma' else 32, 128, seed=71, ragged=True)
         enc = engine.TextEncoder(device=dev, precision='fp32x3')
-        enc.set_option('bert_qkv_attn', 0)  # the unfused QKV GEMM too
+        # the unfused QKV GEMM too (the fused kernel for its own knob: 576 workgroups, past block 256)
+        enc.set_option('bert_qkv_attn', 1 if knob == 'qkv_x3_late_dma' else 0)
         args = (engine.to_device(ids, dev), engine.to_device(mask, dev))
     else:
         enc = engine.ImageEncoder(device=dev, precision='fp32x3')
         args = (engine.to_device(syn.image_inputs(16, seed=72), dev),)
     enc.set_option('gemm_autotune', 0)  # heuristic tiles: 70256 / 71128 / 71064 (2 stages)
     outs = {}
-    for v in (0, 1, 2):
-        enc.set_option('gemm_x3_restage', v)
+    for v in values:
+        enc.set_option(knob, v)
         outs[v] = [t.cpu() for t in enc.forward(*args)]
     enc.check()
-    for v in (1, 2):
-        for i, (a, b) in enumerate(zip(outs[0], outs[v])):
-            assert torch.equal(a, b), f'restage {v}, output {i}: max |d| {float((a - b).abs().max())}'
+    for v in values[1:]:
+        for i, (a, b) in enumerate(zip(outs[values[0]], outs[v])):
+            assert torch.equal(a, b), f'{knob} {v}, output {i}: max |d| {float((a - b).abs().max())}'
 
 
 def test_mobilenet_v2_fp32x3_occ_and_sesw_bit_identical(dev):

@@ -33,6 +33,8 @@ def main():
     ap.add_argument('--precision', default='f16', choices=['f16', 'fp32', 'fp32x3'])
     ap.add_argument('--save', help='write the first value\'s outputs to this .npz (cross-build bit comparisons, '
                                    'with MEC_LIB naming the other build)')
+    ap.add_argument('--handles', default='', help="pipeline only: the handles that get --opt, e.g. 'text' "
+                                                  "(default: every handle)")
     ap.add_argument('--set', action='append', default=[], metavar='KEY=VALUE',
                     help='process-default option set before the handles are created (creation-time knobs such '
                          'as x3_plane_scale)')
@@ -67,15 +69,22 @@ def main():
             return [v for v in r.values() if torch.is_tensor(v)]
         return r if isinstance(r, (tuple, list)) else (r,)
 
+    def setopt(v):
+        if a.enc == 'pipeline' and a.handles:
+            for h in a.handles.split(','):
+                getattr(m, h).set_option(a.opt, v)
+        else:
+            m.set_option(a.opt, v)  # this handle's knob (the pipeline: every handle's)
+
     for v in a.values:
-        m.set_option(a.opt, v)  # this handle's knob (the pipeline: every handle's)
+        setopt(v)
         outs[v] = [t.clone() for t in fwd()]
         torch.cuda.synchronize()
         fwd()
     torch.cuda.synchronize()
     for _ in range(a.rounds):
         for v in a.values:
-            m.set_option(a.opt, v)
+            setopt(v)
             torch.cuda.synchronize()
             t0 = time.perf_counter()
             for _ in range(a.iters):
