@@ -298,6 +298,8 @@ __global__ __launch_bounds__(64 * WM * WN, (WM * WN == 4) ? 2 : 1) void gemm_gld
     // wave passed this barrier, so step t - 1's reads of it are done); same fragments and MFMAs: same bits
     // (late_dma 1: after the lo.hi terms; 2: after the hi.lo terms; 3: the hi planes after lo.hi, the lo planes
     // after hi.lo)
+    // (measured and dropped, DESIGN.md §0: the first half of the waves issuing after its first fragment reads;
+    // the second half issuing after the first I1 rows of lo.hi, or halfway through hi.lo)
     const bool late = SP == 2 && p.late_dma && wave >= NW / 2;
     const bool nxt = DBG != 1 && t + NS - 1 < nk;
     if (nxt && !late) issue((t + NS - 1) % NS, t + NS - 1);
