@@ -367,6 +367,7 @@ int set_option(Options& o, const std::string& k, int value) {
   if (k == "pw_chain" && (value >= 0 && value <= 2)) { o.pw_chain = value; return 0; }
   if (k == "pw_chain_form" && (value >= 0 && value <= 2)) { o.pw_chain_form = value; return 0; }
   if (k == "pw_chain_x3" && (value >= 0 && value <= 2)) { o.pw_chain_x3 = value; return 0; }
+  if (k == "pw_seam_x3" && (value >= 0 && value <= 2)) { o.pw_seam_x3 = value; return 0; }
   if (k == "bert_qkv_attn_x3_heads" && (value == 1 || value == 2)) { o.bert_qkv_attn_x3_heads = value; return 0; }
   if (k == "bert_qkv_attn_heads" && (value == 1 || value == 2)) { o.bert_qkv_attn_heads = value; return 0; }
   if (k == "conv3x3_debug" && (value == 0 || (probe && (value == 1 || value == 2 || value == 4 || value == 7)))) {

@@ -97,6 +97,11 @@ struct Options {
   // fp32x3 layer1 seam kernels (pw_chain_x3.hip): 0 off, 1 the 256 -> 64 seams (block 1 -> 2 with
   // the downsample, 2 -> 3), 2 also the 256 -> 128 seam into layer2
   int pw_chain_x3 = 2;
+  // fp32x3 layer-2 seam kernels (pw_seam_x3.hip): 0 off, 1 the 512 -> 128 seams (blocks 2 -> 3, 3 -> 4),
+  // 2 also the 512 -> 256 seam into layer3's first conv1 (whole-batch runs only: resnet_chunk 0). Same bits
+  // at every setting. Per seam at B = 256: 512 -> 128 356-364 us against 379 for the two split GEMMs,
+  // 512 -> 256 477 against 451 (profiles/r06l_seam_*.txt): 1 by default
+  int pw_seam_x3 = 1;
   int bert_qkv_attn = 1;    // fused BERT QKV projection + attention
   // fp32x3 fused QKV + attention: heads per workgroup (2: 8 waves, 128 KB of LDS, one per CU; 1: 4 waves,
   // 80 KB, two per CU so one's attention overlaps the other's GEMM); same bits

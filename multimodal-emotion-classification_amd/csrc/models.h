@@ -275,6 +275,11 @@ int launch_pw_chain_dual(const f16* t2, const f16* x0, const f16* w3ds, const fl
 int launch_pw_chain_x3(const f16* t2, const f16* xin, long long L, const f16* w3, long long w3_lo, float os3,
                        const float* b3, const f16* w1, long long w1_lo, float os1, const float* b1, f16* xout, f16* t1,
                        int M, int N2, bool dual, hipStream_t s);
+// fp32x3 layer-2 seam (pw_seam_x3.hip): conv3 (K3 = 128 -> 512) + identity residual + ReLU, then the next
+// conv1 (512 -> N1 = 128 | 256), the block output walked in 32-channel chunks; any M (row tails masked)
+int launch_pw_seam_x3(const f16* t2, const f16* xin, long long L, const f16* w3, long long w3_lo, float os3,
+                      const float* b3, const f16* w1, long long w1_lo, float os1, const float* b1, f16* xout, f16* t1,
+                      int M, int K3, int N1, hipStream_t s);
 
 
 }  // namespace mec

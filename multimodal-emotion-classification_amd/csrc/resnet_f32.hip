@@ -780,9 +780,12 @@ int ImageModel::forward_x3(const uint8_t* img, int B, int H, int W, int C, float
   MEC_TRY(prof.end(TAG_RESNET_STEM, s));
   // Bottleneck blocks [b0, b1) over images [i0, i0 + nb) (NHWC planes are image-major: an image range
   // is a pointer offset; the lo planes stay L elements after their hi planes). cur/other swap per block.
-  auto run_blocks = [&](size_t b0, size_t b1, int i0, int nb, int Hin, f16*& cur, f16*& other) -> int {
+  // a layer-2 seam into layer3's first block (pw_seam_x3 2) runs that block's conv1 in the previous call
+  bool carry_conv1 = false;
+  auto run_blocks = [&](size_t b0, size_t b1, int i0, int nb, int Hin, f16*& cur, f16*& other, bool cross) -> int {
     int Hc = Hin;
-    bool conv1_done = false;  // this block's conv1 already ran in the previous block's seam kernel
+    bool conv1_done = carry_conv1;  // this block's conv1 already ran in the previous block's seam kernel
+    carry_conv1 = false;
     for (size_t bi = b0; bi < b1; ++bi) {
       const Bottleneck& bk = blocks[bi];
       const int wd = bk.c1.cout, cin = bk.c1.cin, st = bk.c2.stride;
@@ -828,6 +831,24 @@ int ImageModel::forward_x3(const uint8_t* img, int B, int H, int W, int C, float
         Hc = OH;
         continue;
       }
+      // layer-2 seams (pw_seam_x3.hip): conv3 + identity residual + ReLU, then the next block's conv1 (in
+      // layer2, or layer3's first block when `cross`), the block output walked in 32-channel chunks
+      const int sq = opt().pw_seam_x3;
+      const Bottleneck* nq = bi + 1 < b1 ? &blocks[bi + 1] : (cross && bi + 1 < blocks.size() ? &blocks[bi + 1] : nullptr);
+      const bool seam2 = sq && nq && !bk.has_ds && wd == 128 && nq->c1.cin == 512 &&
+                         (nq->c1.cout == 128 || (sq == 2 && nq->c1.cout == 256));
+      if (seam2) {
+        MEC_TRY(prof.begin(TAG_RESNET_CONV1X1, s));
+        MEC_TRY(launch_pw_seam_x3(t2, in, L, Wt + bk.c3.w_off, wlo, bk.c3.x3_scale, P + bk.c3.x3b_off,
+                                  Wt + nq->c1.w_off, wlo, nq->c1.x3_scale, P + nq->c1.x3b_off, out,
+                                  T1 + (size_t)i0 * OH * OH * nq->c1.cout, nb * OH * OH, wd, nq->c1.cout, s));
+        MEC_TRY(prof.end(TAG_RESNET_CONV1X1, s));
+        if (bi + 1 < b1) conv1_done = true;
+        else carry_conv1 = true;
+        std::swap(cur, other);
+        Hc = OH;
+        continue;
+      }
       g = GemmParams();
       g.split = 1; g.a_lo = L; g.act = ACT_RELU; g.C16 = out; g.c_lo = L; g.M = nb * OH * OH; g.N = 4 * wd;
       if (bk.has_ds) {  // relu(bn3(conv3(t2)) + bn_ds(conv_ds/s(x))) as one GEMM over K = [w | cin]
@@ -855,11 +876,11 @@ int ImageModel::forward_x3(const uint8_t* img, int B, int H, int W, int C, float
   for (int i0 = 0; i0 < B; i0 += chunk) {
     f16* c = X;
     f16* o = Y;
-    MEC_TRY(run_blocks(0, kL12, i0, std::min(chunk, B - i0), 56, c, o));
+    MEC_TRY(run_blocks(0, kL12, i0, std::min(chunk, B - i0), 56, c, o, chunk == B));
     cur = c;
     other = o;
   }
-  MEC_TRY(run_blocks(kL12, blocks.size(), 0, B, 28, cur, other));
+  MEC_TRY(run_blocks(kL12, blocks.size(), 0, B, 28, cur, other, false));
   const int Hc = 7;
   hipLaunchKernelGGL(avgpool_split_kernel, dim3(B, 2048 / 256), dim3(256), 0, s, cur, L, Hc * Hc, 2048,
                      std::ldexp(1.0f, -x3_s_out), pooled);

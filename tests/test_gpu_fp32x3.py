@@ -724,6 +724,28 @@ def test_resnet_fp32x3_seams_bit_identical(dev, B, chunk):
             assert np.array_equal(a, b), f'pw_chain_x3 {seam}, output {k}: max |d| {np.abs(a - b).max()}'
 
 
+@pytest.mark.parametrize('B,chunk', [(3, 0), (5, 0), (40, 0), (40, 16), (256, 0)])
+def test_resnet_fp32x3_layer2_seams_bit_identical(dev, B, chunk):
+    """pw_seam_x3 1 / 2 (layer2's conv3 + identity residual + ReLU and the next block's conv1 -- layer3's
+    first conv1 at 2 -- in one kernel that walks the block output in 32-channel chunks,
+    csrc/pw_seam_x3.hip) against 0 (the two split GEMMs): conv1's k steps are summed in the same
+    ascending order with the same three terms each, and both epilogues are the GEMM's, so every output
+    is equal bit for bit. B = 3 / 5 leave row tails (784 B rows: 16 or 48 rows past the last 64-row
+    tile); resnet_chunk 16 runs layer2 per image chunk (the layer3 seam then stays unfused)."""
+    g = engine.to_device(syn.image_inputs(B, seed=53 + B), dev)
+    outs = []
+    for seam in (0, 1, 2):
+        enc = engine.ImageEncoder(device=dev, precision='fp32x3')
+        enc.set_option('pw_seam_x3', seam)
+        enc.set_option('resnet_chunk', chunk)
+        outs.append(_np(enc.forward(g)))
+        enc.check()
+        enc.close()
+    for seam, o in zip((1, 2), outs[1:]):
+        for k, (a, b) in enumerate(zip(outs[0], o)):
+            assert np.array_equal(a, b), f'pw_seam_x3 {seam}, output {k}: max |d| {np.abs(a - b).max()}'
+
+
 def test_mobilenet_v2_fp32x3_tile_forms_bit_identical(dev):
     """mbv2_x3_tile 4 (4x4 output tiles for the stride-2 blocks at 56 / 28 outputs) computes every
     output pixel with the same arithmetic as the 8x8 / 7x7 tiles: the same bits."""

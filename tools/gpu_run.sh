@@ -54,7 +54,7 @@ for step in "$@"; do
       tail -8 gpurun_out/${TAG}_ab_${E}_$P.txt ;;
     opt:*)
       IFS=: read -r _ E P O V <<< "$step"
-      timeout -k 10 400 python3 -u tools/ab_option.py --enc $E --precision $P --opt $O --values $V --rounds 5 \
+      timeout -k 10 400 python3 -u tools/ab_option.py --enc $E --precision $P --opt $O --values ${V//,/ } --rounds 5 \
         > gpurun_out/${TAG}_opt_${O}_${E}_$P.txt 2>&1 || { tail -5 gpurun_out/${TAG}_opt_${O}_${E}_$P.txt; exit 1; }
       tail -12 gpurun_out/${TAG}_opt_${O}_${E}_$P.txt ;;
     py:*)
