@@ -200,6 +200,7 @@ int mec_conv_f32(const float* x, const float* w, const float* bias, const float*
  *   "pw_chain" 0|1|[2]     layer1 seam kernels (1: the 256->64 seams, 2: also 256->128)
  *   "pw_chain_form" [0]|1|2  seam weight placement (LDS / registers)
  *   "pw_chain_x3" 0|1|[2]  fp32x3 layer1 seam kernels (1: the 256->64 seams incl. the downsample one, 2: also 256->128)
+ *   "pw_seam_x3" 0|[1]|2  fp32x3 layer2 seam kernels (1: the 512->128 seams, 2: also 512->256 into layer3; same bits)
  *   "bert_qkv_attn_x3_heads" [1]|2  fp32x3 fused QKV + attention: heads per workgroup (same bits)
  *   "bert_qkv_attn_heads" [1]|2  the same for the f16 fused QKV + attention
  *   "bert_qkv_attn" 0|[1]  fused BERT QKV projection + attention

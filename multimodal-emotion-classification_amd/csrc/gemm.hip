@@ -45,7 +45,11 @@ int launch_gemm(const GemmParams& p0, hipStream_t s, Prof* prof, int tag) {
     int pin = (tag > 0 && tag < TAG_COUNT) ? opt().gemm_x3_tag[tag] : 0;
     if (pin) {
       const int bm = (pin / 1000) % 10 == 1 ? 128 : 256, bn = pin % 1000;
-      if ((long)((p.M + bm - 1) / bm) * (p.N / bn) < kX3PinMinTiles) pin = 0;  // small batch: autotune (same bits)
+      // the one-stage 72128 tile pays off only with two workgroups on every CU (BERT B = 256: 768 tiles); at
+      // B = 128 (384 tiles, BASELINE configs[2]) it ran the text encoder at 8.81 ms against 8.45 autotuned
+      // (profiles/r06s_ab_ffn2pin_text_b128.txt)
+      const long min_tiles = pin == 72128 ? 2 * 256 : kX3PinMinTiles;
+      if ((long)((p.M + bm - 1) / bm) * (p.N / bn) < min_tiles) pin = 0;  // small batch: autotune (same bits)
     }
     rc = launch_gemm_glds(p, s, opt().gemm_bn ? opt().gemm_bn
                                 : !opt().gemm_x3_order ? (tag == TAG_BERT_FFN1 ? 10256 : 0)

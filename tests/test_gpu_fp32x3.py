@@ -426,12 +426,16 @@ def test_text_fp32x3_large_weights_adapt_plane_scale(dev, name):
                                        ('base.layer1.0.conv3.weight', 2),  # layer1 dual seam (pw_chain_x3)
                                        ('base.layer1.1.conv3.weight', 2),  # layer1 residual seam
                                        ('base.layer1.1.conv3.weight', 0),  # conv3 GEMM epilogue (residual)
-                                       ('base.layer3.0.conv3.weight', 2)])  # dual conv3 + downsample GEMM
+                                       ('base.layer3.0.conv3.weight', 2),  # dual conv3 + downsample GEMM
+                                       ('base.layer2.1.conv3.weight', 2),  # layer2 seam (pw_seam_x3), conv3
+                                       ('base.layer2.2.conv1.weight', 2)])  # layer2 seam, conv1 epilogue
 def test_resnet_fp32x3_overflow_raises_at_check(dev, name, seam):
     """A conv weight scaled by 1e6 with its BN unchanged: the activations leave the estimate's 64x
-    headroom and the f16 range -> check() raises; a handle with the seeded weights checks clean."""
+    headroom and the f16 range -> check() raises; a handle with the seeded weights checks clean.
+    `seam` sets both seam families (pw_chain_x3 for layer1, pw_seam_x3 > 0 for layer2)."""
     enc = engine.ImageEncoder(_edit('image', {name: 1e6}), device=dev, precision='fp32x3')
     enc.set_option('pw_chain_x3', seam)
+    enc.set_option('pw_seam_x3', min(seam, 1))
     enc.forward(engine.to_device(syn.image_inputs(2, seed=5), dev))
     _raises_then_clears(enc)
     ok = engine.ImageEncoder(device=dev, precision='fp32x3')

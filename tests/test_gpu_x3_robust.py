@@ -252,8 +252,8 @@ def test_capture_then_eager_gemm_same_bits(dev):
 
 # ------------------------------------------------------------------ FFN pins at small batches
 def test_ffn_pins_step_aside_at_small_batch(dev):
-    """BERT FFN1 / FFN2 pins (70256 / 72128) apply from 128 tiles; at B = 16 (48 / 24 tiles) the
-    handle autotunes among the 7xxxx tiles instead: the same bits as the pinned tile at B = 64."""
+    """BERT FFN1 / FFN2 pins (70256 / 72128) apply from 128 / 512 tiles; at B = 16 (48 / 24 tiles) the
+    handle autotunes among the 7xxxx tiles instead: the same bits as at B = 64 (FFN1 pinned)."""
     m = engine.TextEncoder(device=dev, precision='fp32x3')
     ids, mask = syn.text_inputs(64, 128, seed=74, ragged=True)
     args = [engine.to_device(a, dev) for a in (ids, mask)]

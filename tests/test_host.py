@@ -137,12 +137,13 @@ def test_option_validation_without_gpu():
           (b'bert_cls_last', 0), (b'bert_cls_last', 1), (b'gemm_x3_order', 0), (b'gemm_x3_order', 1),
           (b'gemm_bn', 70256), (b'gemm_bn', 71064), (b'gemm_bn', 0), (b'gemm_x3_tag', 5 * 100000 + 70256),
           (b'gemm_x3_tag', 5 * 100000), (b'gelu_x3', 0), (b'gelu_x3', 1),
-          (b'pw_chain_x3', 0), (b'pw_chain_x3', 1), (b'pw_chain_x3', 2), (b'mbv2_layered', 0),
+          (b'pw_chain_x3', 0), (b'pw_chain_x3', 1), (b'pw_chain_x3', 2), (b'pw_seam_x3', 0), (b'pw_seam_x3', 2),
+          (b'pw_seam_x3', 1), (b'mbv2_layered', 0),
           (b'mbv2_layered', 7), (b'mbv2_layered', 17), (b'mbv2_layered16', 0), (b'mbv2_layered16', 12),
           (b'mbv2_x3_tile', 0), (b'mbv2_x3_tile', 4), (b'mbv2_x3_tpw', 1), (b'mbv2_x3_tpw', 4), (b'resnet_chunk', 16), (b'resnet_chunk', 0),
           (b'bert_qkv_attn_x3_heads', 2), (b'bert_qkv_attn_x3_heads', 1), (b'bert_qkv_attn_heads', 2),
           (b'bert_qkv_attn_heads', 1)]
-    bad = [(b'pw_chain_x3', 3), (b'bert_qkv_attn_x3_heads', 0), (b'bert_qkv_attn_x3_heads', 3), (b'mbv2_layered', 6), (b'mbv2_layered', 18), (b'mbv2_layered16', 1),
+    bad = [(b'pw_chain_x3', 3), (b'pw_seam_x3', 3), (b'pw_seam_x3', -1), (b'bert_qkv_attn_x3_heads', 0), (b'bert_qkv_attn_x3_heads', 3), (b'mbv2_layered', 6), (b'mbv2_layered', 18), (b'mbv2_layered16', 1),
            (b'mbv2_x3_tile', 8), (b'mbv2_x3_tpw', 0), (b'mbv2_x3_tpw', 17), (b'resnet_chunk', -1),(b'bert_ln_rows', 3), (b'bert_cls_last', 2), (b'gemm_x3_order', 2), (b'gemm_bn', 72256),
            (b'gemm_x3_tag', 5 * 100000 + 10256), (b'gemm_x3_tag', 70256), (b'gelu_x3', 2), (b'gemm_f32_family', 8), (b'gemm_group_m', 3), (b'gemm_group_m', -1), (b'gemm_group_m', 32), (b'gemm_glds_group_m', 5), (b'gemm_f32_tile', 9), (b'fusion_r', 3), (b'fusion_split', 2), (b'bert_qkv_attn', 4), (b'gemm_bn', 12345),
            (b'gemm_bn', 42256), (b'gemm_bn_tag', 11128), (b'gemm_bn_tag', 15 * 100000 + 256),
@@ -160,7 +161,7 @@ def test_option_validation_without_gpu():
                      (b'gemm_bn_tag', 3 * 100000 + 11128), (b'gemm_debug', 0), (b'gemm_group_m', 8),
                      (b'gemm_glds_group_m', 8), (b'gemm_f32_family', 16), (b'bert_ln_rows', 2),
                      (b'bert_cls_last', 1), (b'gemm_x3_order', 1), (b'gelu_x3', 1), (b'gemm_x3_tag', 5 * 100000 + 72128),
-                     (b'pw_chain_x3', 2), (b'mbv2_layered', 8), (b'mbv2_layered16', 8), (b'mbv2_x3_tile', 4), (b'mbv2_x3_tpw', 2),
+                     (b'pw_chain_x3', 2), (b'pw_seam_x3', 1), (b'mbv2_layered', 8), (b'mbv2_layered16', 8), (b'mbv2_x3_tile', 4), (b'mbv2_x3_tpw', 2),
                      (b'resnet_chunk', 0), (b'bert_qkv_attn_x3_heads', 1), (b'bert_qkv_attn_heads', 1)]:
             lib.mec_set_option(k, v)
 

@@ -28,6 +28,7 @@ def main():
     ap.add_argument('--opt', required=True)
     ap.add_argument('--values', type=int, nargs='+', required=True)
     ap.add_argument('--iters', type=int, default=5)
+    ap.add_argument('--batch', type=int, default=256, help='text / image / image_mbv2 batch (BASELINE configs[2]: text 128)')
     ap.add_argument('--rounds', type=int, default=5)
     ap.add_argument('--probes', action='store_true', help='load libmec_hip_probes.so (probe option values)')
     ap.add_argument('--precision', default='f16', choices=['f16', 'fp32', 'fp32x3'])
@@ -56,12 +57,12 @@ def main():
         args += tuple(torch.softmax(torch.randn(256, 7, generator=g), 1).to(dev) for _ in range(3))
     elif a.enc == 'text':
         m = engine.TextEncoder(device=dev, precision=a.precision)
-        ids, mask = syn.text_inputs(256, 128, seed=0)
+        ids, mask = syn.text_inputs(a.batch, 128, seed=0)
         args = (engine.to_device(ids, dev), engine.to_device(mask, dev))
     else:
         m = (engine.ImageEncoder(device=dev, precision=a.precision) if a.enc == 'image'
              else engine.MobileNetImageEncoder(device=dev, precision=a.precision))
-        args = (engine.to_device(syn.image_inputs(256, seed=0), dev),)
+        args = (engine.to_device(syn.image_inputs(a.batch, seed=0), dev),)
     outs, times = {}, {v: [] for v in a.values}
     def fwd():
         r = m.forward(*args)

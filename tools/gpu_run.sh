@@ -8,7 +8,7 @@
 #   enc:<enc>:<prec>       rocprofv3 stats of one encoder alone at B = 256 (tools/gpu_enc_prof.sh)
 #   prof:<prec>            rocprofv3 stats of bench.py's timed window (tools/gpu_prof_bench.sh)
 #   ab:<enc>:<prec>:<n>    cross-build A/B, mec/libmec_hip_base.so vs mec/libmec_hip.so (tools/gpu_ab_lib.sh)
-#   opt:<enc>:<prec>:<opt>:<v1,v2,..>  same-build option A/B (tools/ab_option.py)
+#   opt:<enc>:<prec>:<opt>:<v1,v2,..>[:<batch>]  same-build option A/B (tools/ab_option.py)
 #   py:<script> [args]     any python script under tools/ (bounded to 300 s)
 # Usage: TAG=r06a bash tools/gpu_run.sh tests bench smoke
 cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
@@ -53,8 +53,8 @@ for step in "$@"; do
         || { cat gpurun_out/${TAG}_ab_${E}_$P.txt; exit 1; }
       tail -8 gpurun_out/${TAG}_ab_${E}_$P.txt ;;
     opt:*)
-      IFS=: read -r _ E P O V <<< "$step"
-      timeout -k 10 400 python3 -u tools/ab_option.py --enc $E --precision $P --opt $O --values ${V//,/ } --rounds 5 \
+      IFS=: read -r _ E P O V NB <<< "$step"
+      timeout -k 10 400 python3 -u tools/ab_option.py --enc $E --precision $P --opt $O --values ${V//,/ } --rounds 5 --batch ${NB:-256} \
         > gpurun_out/${TAG}_opt_${O}_${E}_$P.txt 2>&1 || { tail -5 gpurun_out/${TAG}_opt_${O}_${E}_$P.txt; exit 1; }
       tail -12 gpurun_out/${TAG}_opt_${O}_${E}_$P.txt ;;
     py:*)
