@@ -183,7 +183,8 @@ struct Options {
   // offer: where the autotuner took it for a ResNet50 1x1 conv, and the one-stage 128-row tiles for most of
   // them, the image leg ran faster alone but the fused step slower (profiles/r05s_ab_tile73xxx_*.txt). The
   // fused step (FusedPipeline) pins FFN2 back to 70256 (profiles/r05m_ab_x3tag_ffn2.txt). A pin applies only
-  // where its grid fills at least half the chip (kX3PinMinTiles tiles: FFN1 from B = 22, FFN2 from B = 43): a small batch
+  // where its grid fills at least half the chip (kX3PinMinTiles tiles: FFN1 from B = 22; the one-stage 72128 from 512
+  // tiles, two workgroups on every CU: FFN2 from B = 171, gemm.hip): a small batch
   // (latency-mode text inference) autotunes among the 7xxxx tiles instead, which give the same bits
   int gemm_x3_tag[TAG_COUNT] = {0, 0, 0, 0, /*TAG_BERT_FFN1*/ 70256, /*TAG_BERT_FFN2*/ 72128};
   // fp32x3 BERT FFN1 GELU: 1 = ACT_GELU_F32 (branch-free erf, one-instruction exp; max |error| /
